@@ -1,0 +1,141 @@
+/*
+ * surprise_amd.h -- C ABI of the MI355X matrix-factorization SGD library
+ * (libsurprise_amd.so, built from surprise_amd/csrc/mf_kernels.hip for gfx950).
+ *
+ * The reference (nickmvincent/Surprise) has no native ABI: its hot loop is the
+ * Cython method SVD.sgd / SVDpp.sgd, reached from Python through AlgoBase.fit().
+ * Each entry point below replaces one piece of that loop; the Python host
+ * (surprise_amd/matrix_factorization.py) binds them with ctypes exactly where
+ * the reference calls self.sgd(trainset) and self.estimate(u, i).
+ *
+ * Conventions (all entry points):
+ *   - every array pointer is a DEVICE pointer (e.g. torch.Tensor.data_ptr());
+ *   - no allocation, no host synchronisation, no exceptions cross the ABI;
+ *   - calls are ordered on `stream` (a hipStream_t passed as void*; NULL = legacy default);
+ *   - return 0 on success, otherwise a hipError_t code or one of MF_E_* below;
+ *     mf_last_error() returns a static message for the last failure on this thread;
+ *   - factor tables are row-major with leading dimension `ld` >= n_factors; columns
+ *     [n_factors, ld) must be zero and stay zero (the kernels never make them non-zero);
+ *   - `dtype` selects the arithmetic type of every floating array: MF_F32 or MF_F64.
+ */
+#ifndef SURPRISE_AMD_H
+#define SURPRISE_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MF_F32 0
+#define MF_F64 1
+
+/* Item-side update schedule of the Hogwild kernels. */
+#define MF_MODE_PLAIN   0 /* one shared item table, plain load/store (lock-free Hogwild)          */
+#define MF_MODE_ATOMIC  1 /* one shared item table, item deltas applied with float atomics         */
+#define MF_MODE_REPLICA 2 /* n_replicas item tables, replica = XCD id % n_replicas; merged by
+                             mf_replica_merge (sum of deltas) once per epoch-chunk                */
+
+#define MF_E_ARG          1001 /* invalid argument (shape, mode, dtype, n_factors too large)      */
+#define MF_E_UNSUPPORTED  1002 /* combination not compiled                                       */
+
+#define MF_MAX_FACTORS_F32 512
+#define MF_MAX_FACTORS_F64 256
+
+/* Learning rates / regularisation, resolved like SVD.__init__ (matrix_factorization.pyx:140-147)
+ * and SVDpp.__init__ (:398-407). global_mean is Trainset.global_mean (trainset.py:252-261),
+ * already zeroed by the caller when biased == 0 (matrix_factorization.pyx:238-239). */
+typedef struct mf_hyper {
+    double lr_bu, lr_bi, lr_pu, lr_qi, lr_yj;
+    double reg_bu, reg_bi, reg_pu, reg_qi, reg_yj;
+    double global_mean;
+} mf_hyper_t;
+
+/* The ratings of one shard, user-major CSR in Trainset.all_ratings() order (trainset.py:180-190):
+ * user u's ratings are items[row_ptr[u] .. row_ptr[u+1]) / ratings[...].  `items` and `ratings`
+ * are read only inside [row_ptr[0], row_ptr[n_users]). */
+typedef struct mf_csr {
+    const int64_t *row_ptr;  /* [n_users + 1]                     */
+    const int32_t *items;    /* [nnz] item inner ids              */
+    const void *ratings;     /* [nnz] dtype, offset applied       */
+    int32_t n_users;
+    int32_t n_items;
+} mf_csr_t;
+
+/*
+ * One epoch-chunk of SVD SGD over the users listed in sched[0..n_sched).
+ * Replaces the body of SVD.sgd's epoch loop (matrix_factorization.pyx:241-262):
+ * each wavefront owns a user (pu[u], bu[u] live in registers, updated in the
+ * reference's per-rating order) and applies lock-free Hogwild! updates to the
+ * shared item rows qi[i], bi[i].
+ *   qi/bi     : item tables; with MF_MODE_REPLICA n_replicas copies spaced by
+ *               rep_stride_q / rep_stride_b elements.
+ *   n_waves   : wavefronts to launch (<= 0: library default = fill the GPU);
+ *               1 gives the exact sequential reference order when sched = 0..n_users-1.
+ *   dup_items : non-zero if some user has the same item twice (enables in-register forwarding).
+ */
+int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
+                 void *qi, void *bi, int32_t n_factors, int32_t ld, int32_t biased,
+                 const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int64_t rep_stride_q,
+                 int64_t rep_stride_b, int32_t n_waves, int32_t dup_items, int32_t dtype,
+                 void *stream);
+
+/*
+ * One epoch-chunk of SVD++ SGD (SVDpp.sgd epoch body, matrix_factorization.pyx:463-498) in the
+ * exact per-user affine form: per user, one gather of y_j (j in I_u), the sequential rating
+ * loop with u_impl maintained incrementally, and one affine write-back y_j <- A y_j + c.
+ * yj is replicated like qi (rep_stride_q).
+ */
+int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
+                   void *qi, void *bi, void *yj, int32_t n_factors, int32_t ld,
+                   const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int64_t rep_stride_q,
+                   int64_t rep_stride_b, int32_t n_waves, int32_t dup_items, int32_t dtype,
+                   void *stream);
+
+/*
+ * Item-side merge of an epoch-chunk: for each of the `n_seg` segments
+ * (seg_ptr[s] = device pointer to replica 0 of that table, seg_len[s] elements, replicas
+ * spaced by seg_stride[s] elements, snapshot at seg_snap[s]) compute
+ *     delta = sum_r (rep_r - snap)                 into delta_out (packed, segment after segment)
+ * and, if apply != 0, also  snap += delta; rep_r = snap  for every r.
+ * With apply == 0 the caller all-reduces delta_out (RCCL SUM) and then calls mf_apply_delta.
+ * The descriptor arrays are HOST arrays (<= 8 segments).
+ */
+int mf_replica_merge(int32_t n_seg, void *const *seg_ptr, void *const *seg_snap,
+                     const int64_t *seg_len, const int64_t *seg_stride, int32_t n_replicas,
+                     void *delta_out, int32_t apply, int32_t dtype, void *stream);
+
+/* snap += delta; rep_r = snap for every replica (second half of mf_replica_merge). */
+int mf_apply_delta(int32_t n_seg, void *const *seg_ptr, void *const *seg_snap,
+                   const int64_t *seg_len, const int64_t *seg_stride, int32_t n_replicas,
+                   const void *delta, int32_t dtype, void *stream);
+
+/*
+ * Batched SVD.estimate (matrix_factorization.pyx:269-299): for x < n, with u[x] < 0 / i[x] < 0
+ * meaning an unknown user / item ('UKN__' ids, algo_base.py:137-144):
+ *   biased:   est = mu (+bu[u] if known u) (+bi[i] if known i) (+ qi[i].(pu[u] + imp[u]) if both)
+ *   unbiased: est = qi[i].pu[u] if both known, else impossible[x] = 1 (PredictionImpossible)
+ * imp (nullable) is the SVD++ implicit term per user (mf_svdpp_user_implicit); with it this is
+ * SVDpp.estimate (:506-522).  est is dtype, impossible is int32.
+ */
+int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, const void *qi,
+               const void *bu, const void *bi, const void *imp, int32_t n_factors, int32_t ld,
+               int32_t biased, double global_mean, void *est, int32_t *impossible, int32_t dtype,
+               void *stream);
+
+/* imp[u] = (sum_{j in I_u} yj[j]) / sqrt(|I_u|)  (SVDpp.estimate :518-520), zero for empty users. */
+int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, void *imp, int32_t n_factors,
+                           int32_t ld, int32_t dtype, void *stream);
+
+/* Self-test of the wavefront reduction: out[w] = sum of in[64w .. 64w+63], w < n_waves. */
+int mf_selftest_wave_sum(const void *in, void *out, int32_t n_waves, int32_t dtype, void *stream);
+
+/* Library version (major*10000 + minor*100 + patch) and last error message. */
+int mf_version(void);
+const char *mf_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SURPRISE_AMD_H */

@@ -1,0 +1,105 @@
+"""Loader for libsurprise_amd.so, the C ABI declared in include/surprise_amd.h.
+
+The library is built in-tree (``surprise_amd/libsurprise_amd.so``) by
+``surprise_amd.build.build()`` with ``hipcc --offload-arch=gfx950``.  There is
+no fallback: if the library is missing or the GPU is absent every training or
+inference entry point raises ``SurpriseAMDError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsurprise_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "surprise_amd.h")
+
+MF_F32, MF_F64 = 0, 1
+MF_MODE_PLAIN, MF_MODE_ATOMIC, MF_MODE_REPLICA = 0, 1, 2
+MODES = {"plain": MF_MODE_PLAIN, "atomic": MF_MODE_ATOMIC, "replica": MF_MODE_REPLICA}
+MAX_FACTORS = {MF_F32: 512, MF_F64: 256}
+
+
+class SurpriseAMDError(RuntimeError):
+    """A HIP / library failure surfaced from the C ABI."""
+
+
+class MfHyper(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "lr_bu", "lr_bi", "lr_pu", "lr_qi", "lr_yj",
+        "reg_bu", "reg_bi", "reg_pu", "reg_qi", "reg_yj", "global_mean")]
+
+
+class MfCsr(ctypes.Structure):
+    _fields_ = [("row_ptr", ctypes.c_void_p), ("items", ctypes.c_void_p),
+                ("ratings", ctypes.c_void_p), ("n_users", ctypes.c_int32),
+                ("n_items", ctypes.c_int32)]
+
+
+_vp, _i32, _i64, _dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+
+# name -> argtypes (all return int except mf_last_error)
+SIGNATURES = {
+    "mf_svd_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32,
+                     ctypes.POINTER(MfHyper), _i32, _i32, _i64, _i64, _i32, _i32, _i32, _vp],
+    "mf_svdpp_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
+                       ctypes.POINTER(MfHyper), _i32, _i32, _i64, _i64, _i32, _i32, _i32, _vp],
+    "mf_replica_merge": [_i32, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64),
+                         ctypes.POINTER(_i64), _i32, _vp, _i32, _i32, _vp],
+    "mf_apply_delta": [_i32, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64),
+                       ctypes.POINTER(_i64), _i32, _vp, _i32, _vp],
+    "mf_predict": [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _dbl, _vp, _vp,
+                   _i32, _vp],
+    "mf_svdpp_user_implicit": [ctypes.POINTER(MfCsr), _vp, _vp, _i32, _i32, _i32, _vp],
+    "mf_selftest_wave_sum": [_vp, _vp, _i32, _i32, _vp],
+    "mf_version": [],
+    "mf_last_error": [],
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load the shared library (no GPU access happens here)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SurpriseAMDError(
+            f"{path} is missing: build it with `python -c 'import surprise_amd.build as b; b.build()'`"
+            " (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_char_p if name == "mf_last_error" else ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().mf_last_error()
+        raise SurpriseAMDError(f"{what} failed with code {rc}: {msg.decode() if msg else ''}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)
+
+
+def require_gpu():
+    """Return the torch module once a HIP device is confirmed; raise otherwise."""
+    import torch
+    if not torch.cuda.is_available():
+        raise SurpriseAMDError(
+            "surprise_amd needs a HIP GPU (MI355X, gfx950): torch.cuda.is_available() is False. "
+            "There is no CPU fallback for the training path.")
+    load()
+    return torch
+
+
+def header_symbols(path: str = HEADER_PATH):
+    """Function names declared in include/surprise_amd.h (for the ABI test)."""
+    import re
+    text = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(mf_\w+)\s*\(", text, re.M)))

@@ -1,0 +1,280 @@
+"""SVD and SVD++ behind Surprise's AlgoBase plugin API, trained by HIP kernels.
+
+Mirrors surprise/prediction_algorithms/matrix_factorization.pyx:
+  SVD    __init__ :129-151, fit :153-170, sgd :172-267, estimate :269-299
+  SVDpp  __init__ :389-411, fit :413-418, sgd :420-504, estimate :506-522
+
+Same constructor arguments, defaults and learning-rate / regularisation
+fall-backs; same initialisation draws (get_rng, then rng.normal for pu, qi[, yj]
+in that order, fp64); same attributes after fit (``pu``, ``qi``, ``bu``, ``bi``
+[, ``yj``] as fp64 numpy).  ``sgd`` runs the epochs on the GPU through
+libsurprise_amd.so and raises if the library or the GPU is missing -- there is
+no CPU fallback.  Extra, keyword-only device options:
+
+  dtype              "float32" (default) or "float64" arithmetic on the device
+  mode               item-side Hogwild schedule: "replica" (per-XCD item tables merged by a
+                     sum of deltas once per epoch-chunk), "atomic", "plain" or "auto"
+  n_replicas         item replicas in "replica" mode (8 = one per XCD)
+  chunks_per_epoch   epoch-chunks (item merges / all-reduces per epoch)
+  deterministic      one wavefront, users in Trainset order: the reference's exact sequence
+  n_waves            wavefronts per launch (0 = fill the GPU)
+  distributed        shard users over torch.distributed ranks (one process per GPU)
+
+The fork's per-fit side effects in SVD.fit (:158-169: a print and an unused
+``movie_to_mean`` dict) do not change results and are not reproduced.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .algo_base import AlgoBase
+from .predictions import Prediction, PredictionImpossible
+from .trainset import Trainset
+from .utils import get_rng
+
+_REPLICA_BUDGET_BYTES = 4 << 30
+
+
+class _MFBase(AlgoBase):
+    _algo = "svd"
+
+    def _device_options(self, dtype, mode, n_replicas, chunks_per_epoch, deterministic, n_waves,
+                        distributed):
+        self.dtype = dtype
+        self.mode = mode
+        self.n_replicas = n_replicas
+        self.chunks_per_epoch = chunks_per_epoch
+        self.deterministic = deterministic
+        self.n_waves = n_waves
+        self.distributed = distributed
+        self._engine = None
+        self._imp = None
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        state["_engine"] = None  # device handles never pickle (dump.py, joblib workers)
+        state["_imp"] = None
+        return state
+
+    def _resolve_mode(self, n_items, ld):
+        if self.mode != "auto":
+            return self.mode
+        per = n_items * ld * (2 if self._algo == "svdpp" else 1) * \
+            (8 if self.dtype in ("float64", "f64") else 4)
+        return "replica" if per * self.n_replicas <= _REPLICA_BUDGET_BYTES else "atomic"
+
+    def _hyper(self, global_mean):
+        return dict(lr_bu=self.lr_bu, lr_bi=self.lr_bi, lr_pu=self.lr_pu, lr_qi=self.lr_qi,
+                    lr_yj=getattr(self, "lr_yj", 0.0), reg_bu=self.reg_bu, reg_bi=self.reg_bi,
+                    reg_pu=self.reg_pu, reg_qi=self.reg_qi, reg_yj=getattr(self, "reg_yj", 0.0),
+                    global_mean=float(global_mean))
+
+    def fit_arrays(self, row_ptr, items, ratings, n_items, rating_scale=(1, 5), offset=0):
+        """Array-native fit on a user-major CSR (no reference counterpart): for
+        trainsets too large for Python dicts."""
+        ts = Trainset.from_csr(row_ptr, items, ratings, n_items, rating_scale, offset)
+        return self.fit(ts)
+
+    def _run_sgd(self, trainset, with_yj):
+        from .engine import MFEngine, default_ld
+        from .dist import DistContext, shard_users
+
+        torch = _lib.require_gpu()
+        if isinstance(trainset, Trainset):
+            csr = trainset.csr()
+            user_order = trainset.sched_order()
+        else:  # a reference surprise.Trainset (duck-typed: ur dict-of-lists)
+            csr = Trainset(trainset.ur, None, trainset.n_users, trainset.n_items,
+                           trainset.n_ratings, trainset.rating_scale, trainset.offset, {}, {}).csr()
+            user_order = np.fromiter(trainset.ur.keys(), np.int32, len(trainset.ur))
+        global_mean = self.trainset.global_mean
+
+        rng = get_rng(self.random_state)
+        n_users, n_items, K = trainset.n_users, trainset.n_items, self.n_factors
+        pu = rng.normal(self.init_mean, self.init_std_dev, (n_users, K))
+        qi = rng.normal(self.init_mean, self.init_std_dev, (n_items, K))
+        yj = rng.normal(self.init_mean, self.init_std_dev, (n_items, K)) if with_yj else None
+
+        ctx = DistContext.from_env() if self.distributed else None
+        users = None
+        if ctx is not None and ctx.world > 1:
+            b = shard_users(csr[0], ctx.world)
+            users = np.arange(b[ctx.rank], b[ctx.rank + 1])
+        dt = _lib.MF_F64 if self.dtype in ("float64", "f64") else _lib.MF_F32
+        mode = self._resolve_mode(n_items, default_ld(K, dt))
+        eng = MFEngine(csr, n_items, K, algo=self._algo, hyper=self._hyper(global_mean),
+                       biased=getattr(self, "biased", True), dtype=self.dtype, mode=mode,
+                       n_replicas=self.n_replicas, n_chunks=self.chunks_per_epoch, users=users,
+                       deterministic=self.deterministic, user_order=user_order,
+                       n_waves=self.n_waves, world=1 if ctx is None else ctx.world)
+        eng.set_factors(pu, qi, yj=yj)
+        verbose = self.verbose
+
+        def on_epoch(e):
+            if verbose:
+                print("Processing epoch {}".format(e))
+
+        eng.run_epochs(self.n_epochs, ctx, on_epoch=on_epoch if verbose else None)
+        f = eng.get_factors()
+        self._engine = eng
+        self._imp = None
+        self.bu, self.bi, self.pu, self.qi = f["bu"], f["bi"], f["pu"], f["qi"]
+        if with_yj:
+            self.yj = f["yj"]
+        del torch
+
+    # ------------------------------------------------------------------ batched test()
+    def test(self, testset, verbose=False):
+        """AlgoBase.test (algo_base.py:191-218) with the estimates computed in one
+        batched HIP launch when the model is on the device; after unpickling (no
+        device state) it falls back to per-prediction estimate(), the reference's
+        own numpy path."""
+        if self._engine is None or verbose:
+            return AlgoBase.test(self, testset, verbose)
+        iterate_on = testset.tolist() if isinstance(testset, np.ndarray) else testset
+        rows = list(iterate_on)
+        ts = self.trainset
+        u = np.empty(len(rows), np.int32)
+        i = np.empty(len(rows), np.int32)
+        for x, (ruid, riid, _) in enumerate(rows):
+            try:
+                u[x] = ts.to_inner_uid(ruid)
+            except ValueError:
+                u[x] = -1
+            try:
+                i[x] = ts.to_inner_iid(riid)
+            except ValueError:
+                i[x] = -1
+        est, impossible = self._predict_inner(u, i)
+        est = np.where(impossible, self.default_prediction(), est) - ts.offset
+        lo, hi = ts.rating_scale
+        est = np.fmax(lo, np.fmin(hi, est))  # algo_base.py:166-169 (NaN -> upper bound)
+        out = []
+        reason = "User and item are unkown."
+        for x, (ruid, riid, r) in enumerate(rows):
+            d = {"was_impossible": bool(impossible[x])}
+            if impossible[x]:
+                d["reason"] = reason
+            out.append(Prediction(ruid, riid, r - ts.offset, float(est[x]), d))
+        return out
+
+
+class SVD(_MFBase):
+    """Biased MF / PMF trained by Hogwild! SGD on the GPU (matrix_factorization.pyx:19-299)."""
+
+    _algo = "svd"
+
+    def __init__(self, n_factors=100, n_epochs=20, biased=True, init_mean=0, init_std_dev=.1,
+                 lr_all=.005, reg_all=.02, lr_bu=None, lr_bi=None, lr_pu=None, lr_qi=None,
+                 reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, random_state=None,
+                 verbose=False, *, dtype="float32", mode="auto", n_replicas=8,
+                 chunks_per_epoch=1, deterministic=False, n_waves=0, distributed=True):
+        self.n_factors = n_factors
+        self.n_epochs = n_epochs
+        self.biased = biased
+        self.init_mean = init_mean
+        self.init_std_dev = init_std_dev
+        self.lr_bu = lr_bu if lr_bu is not None else lr_all
+        self.lr_bi = lr_bi if lr_bi is not None else lr_all
+        self.lr_pu = lr_pu if lr_pu is not None else lr_all
+        self.lr_qi = lr_qi if lr_qi is not None else lr_all
+        self.reg_bu = reg_bu if reg_bu is not None else reg_all
+        self.reg_bi = reg_bi if reg_bi is not None else reg_all
+        self.reg_pu = reg_pu if reg_pu is not None else reg_all
+        self.reg_qi = reg_qi if reg_qi is not None else reg_all
+        self.random_state = random_state
+        self.verbose = verbose
+        self._device_options(dtype, mode, n_replicas, chunks_per_epoch, deterministic, n_waves,
+                             distributed)
+        AlgoBase.__init__(self)
+
+    def fit(self, trainset):
+        AlgoBase.fit(self, trainset)
+        self.sgd(trainset)
+        return self
+
+    def sgd(self, trainset):
+        """mf.pyx:172-267 on the device: init on the host (bit-identical draws), epochs in HIP."""
+        self._run_sgd(trainset, with_yj=False)
+
+    def estimate(self, u, i):
+        """mf.pyx:269-299 (host numpy fp64, per call)."""
+        known_user = self.trainset.knows_user(u)
+        known_item = self.trainset.knows_item(i)
+        if self.biased:
+            est = self.trainset.global_mean
+            if known_user:
+                est += self.bu[u]
+            if known_item:
+                est += self.bi[i]
+            if known_user and known_item:
+                est += np.dot(self.qi[i], self.pu[u])
+        else:
+            if known_user and known_item:
+                est = np.dot(self.qi[i], self.pu[u])
+            else:
+                raise PredictionImpossible("User and item are unkown.")
+        return est
+
+    def _predict_inner(self, u, i):
+        return self._engine.predict(u, i, self.trainset.global_mean if self.biased else 0.0)
+
+
+class SVDpp(_MFBase):
+    """SVD++ trained on the GPU in the exact per-user affine form (mf.pyx:302-522)."""
+
+    _algo = "svdpp"
+
+    def __init__(self, n_factors=20, n_epochs=20, init_mean=0, init_std_dev=.1, lr_all=.007,
+                 reg_all=.02, lr_bu=None, lr_bi=None, lr_pu=None, lr_qi=None, lr_yj=None,
+                 reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, reg_yj=None,
+                 random_state=None, verbose=False, *, dtype="float32", mode="auto",
+                 n_replicas=8, chunks_per_epoch=1, deterministic=False, n_waves=0,
+                 distributed=True):
+        self.n_factors = n_factors
+        self.n_epochs = n_epochs
+        self.init_mean = init_mean
+        self.init_std_dev = init_std_dev
+        self.lr_bu = lr_bu if lr_bu is not None else lr_all
+        self.lr_bi = lr_bi if lr_bi is not None else lr_all
+        self.lr_pu = lr_pu if lr_pu is not None else lr_all
+        self.lr_qi = lr_qi if lr_qi is not None else lr_all
+        self.lr_yj = lr_yj if lr_yj is not None else lr_all
+        self.reg_bu = reg_bu if reg_bu is not None else reg_all
+        self.reg_bi = reg_bi if reg_bi is not None else reg_all
+        self.reg_pu = reg_pu if reg_pu is not None else reg_all
+        self.reg_qi = reg_qi if reg_qi is not None else reg_all
+        self.reg_yj = reg_yj if reg_yj is not None else reg_all
+        self.random_state = random_state
+        self.verbose = verbose
+        self._device_options(dtype, mode, n_replicas, chunks_per_epoch, deterministic, n_waves,
+                             distributed)
+        AlgoBase.__init__(self)
+
+    def fit(self, trainset):
+        AlgoBase.fit(self, trainset)
+        self.sgd(trainset)
+        return self
+
+    def sgd(self, trainset):
+        """mf.pyx:420-504 on the device (per-user affine form, exact without duplicate items)."""
+        self._run_sgd(trainset, with_yj=True)
+
+    def estimate(self, u, i):
+        """mf.pyx:506-522 (host numpy fp64, per call)."""
+        est = self.trainset.global_mean
+        if self.trainset.knows_user(u):
+            est += self.bu[u]
+        if self.trainset.knows_item(i):
+            est += self.bi[i]
+        if self.trainset.knows_user(u) and self.trainset.knows_item(i):
+            Iu = len(self.trainset.ur[u])
+            u_impl_feedback = (sum(self.yj[j] for (j, _) in self.trainset.ur[u]) / np.sqrt(Iu))
+            est += np.dot(self.qi[i], self.pu[u] + u_impl_feedback)
+        return est
+
+    def _predict_inner(self, u, i):
+        if self._imp is None:
+            self._imp = self._engine.user_implicit()
+        return self._engine.predict(u, i, self.trainset.global_mean, imp=self._imp)
