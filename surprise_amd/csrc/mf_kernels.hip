@@ -144,6 +144,14 @@ __device__ __forceinline__ int xcc_id() {
     return (int)(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 0xF);
 }
 
+// Item-side loads bypass the CU's vector L1 (global_load ... sc1, served by the XCD's L2):
+// the L1 is never refreshed by other CUs' stores, so a plain load of a hot item row can return
+// a stale copy for a long time and the following store then erases other waves' updates.
+template <typename T>
+__device__ __forceinline__ T ld_l2(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename T>
 __device__ __forceinline__ void atomic_add(T *p, T v) {
     atomicAdd(p, v);  // global_atomic_add_f32 / _f64, executed at the memory side (no CAS loop)
@@ -200,11 +208,14 @@ __global__ __launch_bounds__(kBlock) void svd_epoch_kernel(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, T *qi, T *bi, int K, int ld, int biased,
-    Hyper<T> hp, int n_rep, int64_t rep_stride_q, int64_t rep_stride_b, int dups)
+    Hyper<T> hp, int n_rep, int64_t rep_stride_q, int64_t rep_stride_b, int dups,
+    int64_t n_waves_req)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave;
-    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const int64_t grid_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
+    if (wave >= n_waves) return;  // whole wave exits (a 1-wave launch still uses a 4-wave block)
 
     T *q_tab = qi;
     T *b_tab = bi;
@@ -236,10 +247,10 @@ __global__ __launch_bounds__(kBlock) void svd_epoch_kernel(
             const int i = rs.item(k);
             s_i[slot] = i;
             s_r[slot] = rs.rating(k);
-            s_b[slot] = b_tab[i];
+            s_b[slot] = ld_l2(b_tab + i);
             const T *row = q_tab + (int64_t)i * ld + lane;
 #pragma unroll
-            for (int v = 0; v < V; ++v) s_q[slot][v] = fin[v] ? row[kWave * v] : T(0);
+            for (int v = 0; v < V; ++v) s_q[slot][v] = fin[v] ? ld_l2(row + kWave * v) : T(0);
         };
 #pragma unroll
         for (int d = 0; d < kPF; ++d)
@@ -313,11 +324,13 @@ __global__ __launch_bounds__(kBlock) void svdpp_epoch_kernel(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, T *qi, T *bi, T *yj, int K, int ld, Hyper<T> hp,
-    int n_rep, int64_t rep_stride_q, int64_t rep_stride_b, int dups)
+    int n_rep, int64_t rep_stride_q, int64_t rep_stride_b, int dups, int64_t n_waves_req)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave;
-    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const int64_t grid_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
+    if (wave >= n_waves) return;
 
     T *q_tab = qi, *y_tab = yj, *b_tab = bi;
     if (MODE == kReplica) {
@@ -351,7 +364,7 @@ __global__ __launch_bounds__(kBlock) void svdpp_epoch_kernel(
                 for (int a = 0; a < 8; ++a) {
                     const T *row = y_tab + (int64_t)readlane(jl, x + a) * ld + lane;
 #pragma unroll
-                    for (int v = 0; v < V; ++v) g[a][v] = fin[v] ? row[kWave * v] : T(0);
+                    for (int v = 0; v < V; ++v) g[a][v] = fin[v] ? ld_l2(row + kWave * v) : T(0);
                 }
 #pragma unroll
                 for (int a = 0; a < 8; ++a)
@@ -361,7 +374,7 @@ __global__ __launch_bounds__(kBlock) void svdpp_epoch_kernel(
             for (; x < cnt; ++x) {
                 const T *row = y_tab + (int64_t)readlane(jl, x) * ld + lane;
 #pragma unroll
-                for (int v = 0; v < V; ++v) imp[v] += (fin[v] ? row[kWave * v] : T(0)) / sqrt_n;
+                for (int v = 0; v < V; ++v) imp[v] += (fin[v] ? ld_l2(row + kWave * v) : T(0)) / sqrt_n;
             }
         }
 
@@ -383,10 +396,10 @@ __global__ __launch_bounds__(kBlock) void svdpp_epoch_kernel(
             const int i = rs.item(k);
             s_i[slot] = i;
             s_r[slot] = rs.rating(k);
-            s_b[slot] = b_tab[i];
+            s_b[slot] = ld_l2(b_tab + i);
             const T *row = q_tab + (int64_t)i * ld + lane;
 #pragma unroll
-            for (int v = 0; v < V; ++v) s_q[slot][v] = fin[v] ? row[kWave * v] : T(0);
+            for (int v = 0; v < V; ++v) s_q[slot][v] = fin[v] ? ld_l2(row + kWave * v) : T(0);
         };
 #pragma unroll
         for (int d = 0; d < kPF; ++d)
@@ -461,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void svdpp_epoch_kernel(
                 for (int a = 0; a < 8; ++a) {
                     rows[a] = y_tab + (int64_t)readlane(jl, x + a) * ld + lane;
 #pragma unroll
-                    for (int v = 0; v < V; ++v) g[a][v] = fin[v] ? rows[a][kWave * v] : T(0);
+                    for (int v = 0; v < V; ++v) g[a][v] = fin[v] ? ld_l2(rows[a] + kWave * v) : T(0);
                 }
 #pragma unroll
                 for (int a = 0; a < 8; ++a)
@@ -479,7 +492,7 @@ __global__ __launch_bounds__(kBlock) void svdpp_epoch_kernel(
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
                     if (!fin[v]) continue;
-                    const T y = row[kWave * v];
+                    const T y = ld_l2(row + kWave * v);
                     if (MODE == kAtomic)
                         atomic_add(row + kWave * v, (A - T(1)) * y + cacc[v]);
                     else
@@ -657,7 +670,7 @@ int launch_svd_v(const mf_csr_t *c, const int32_t *sched, int64_t n_sched, void 
     hipLaunchKernelGGL((svd_epoch_kernel<T, V, MODE>), dim3(grid_for_waves(waves)), dim3(kBlock), 0,
                        st, c->row_ptr, c->items, (const T *)c->ratings, sched, n_sched, (T *)pu,
                        (T *)bu, (T *)qi, (T *)bi, K, ld, biased, cast_hyper<T>(hp), n_rep, rsq, rsb,
-                       dups);
+                       dups, waves);
     return check_launch("svd_epoch_kernel");
 }
 
@@ -669,7 +682,7 @@ int launch_svdpp_v(const mf_csr_t *c, const int32_t *sched, int64_t n_sched, voi
     hipLaunchKernelGGL((svdpp_epoch_kernel<T, V, MODE>), dim3(grid_for_waves(waves)), dim3(kBlock),
                        0, st, c->row_ptr, c->items, (const T *)c->ratings, sched, n_sched,
                        (T *)pu, (T *)bu, (T *)qi, (T *)bi, (T *)yj, K, ld, cast_hyper<T>(hp),
-                       n_rep, rsq, rsb, dups);
+                       n_rep, rsq, rsb, dups, waves);
     return check_launch("svdpp_epoch_kernel");
 }
 
