@@ -14,8 +14,11 @@
  *   - calls are ordered on `stream` (a hipStream_t passed as void*; NULL = legacy default);
  *   - return 0 on success, otherwise a hipError_t code or one of MF_E_* below;
  *     mf_last_error() returns a static message for the last failure on this thread;
- *   - factor tables are row-major with leading dimension `ld` >= n_factors; columns
- *     [n_factors, ld) must be zero and stay zero (the kernels never make them non-zero);
+ *   - factor tables are row-major.  User rows pu[u] and implicit rows yj[j] have leading
+ *     dimension ldu >= n_factors; item rows have ldq >= n_factors + 1 and hold the item bias in
+ *     column n_factors: qb[i] = [q_i | b_i | 0 ...].  Padding columns must be zero and stay zero;
+ *   - item tables (qb, yj) come in n_replicas consecutive copies (n_items rows each) and must
+ *     be < 2 GiB per copy (32-bit buffer offsets);
  *   - `dtype` selects the arithmetic type of every floating array: MF_F32 or MF_F64.
  */
 #ifndef SURPRISE_AMD_H
@@ -35,6 +38,7 @@ extern "C" {
 #define MF_MODE_ATOMIC  1 /* one shared item table, item deltas applied with float atomics         */
 #define MF_MODE_REPLICA 2 /* n_replicas item tables, replica = XCD id % n_replicas; merged by
                              mf_replica_merge (sum of deltas) once per epoch-chunk                */
+#define MF_MODE_COHERENT 3 /* one shared item table, write-through (sc1) stores                    */
 
 #define MF_E_ARG          1001 /* invalid argument (shape, mode, dtype, n_factors too large)      */
 #define MF_E_UNSUPPORTED  1002 /* combination not compiled                                       */
@@ -67,30 +71,29 @@ typedef struct mf_csr {
  * Replaces the body of SVD.sgd's epoch loop (matrix_factorization.pyx:241-262):
  * each wavefront owns a user (pu[u], bu[u] live in registers, updated in the
  * reference's per-rating order) and applies lock-free Hogwild! updates to the
- * shared item rows qi[i], bi[i].
- *   qi/bi     : item tables; with MF_MODE_REPLICA n_replicas copies spaced by
- *               rep_stride_q / rep_stride_b elements.
+ * shared item rows qb[i] = [q_i | b_i].
+ *   pu [n_users][ldu], bu [n_users], qb [n_replicas][n_items][ldq]
+ *   biased    : 0 reproduces SVD(biased=False) (hp->global_mean must then be 0)
+ *   mode      : MF_MODE_*; n_replicas is used by MF_MODE_REPLICA only (else pass 1)
  *   n_waves   : wavefronts to launch (<= 0: library default = fill the GPU);
  *               1 gives the exact sequential reference order when sched = 0..n_users-1.
- *   dup_items : non-zero if some user has the same item twice (enables in-register forwarding).
+ *   dup_items : non-zero if some user lists the same item twice (enables in-register forwarding).
  */
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
-                 void *qi, void *bi, int32_t n_factors, int32_t ld, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int64_t rep_stride_q,
-                 int64_t rep_stride_b, int32_t n_waves, int32_t dup_items, int32_t dtype,
-                 void *stream);
+                 int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
+                 const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int32_t n_waves,
+                 int32_t dup_items, int32_t dtype, void *stream);
 
 /*
  * One epoch-chunk of SVD++ SGD (SVDpp.sgd epoch body, matrix_factorization.pyx:463-498) in the
  * exact per-user affine form: per user, one gather of y_j (j in I_u), the sequential rating
  * loop with u_impl maintained incrementally, and one affine write-back y_j <- A y_j + c.
- * yj is replicated like qi (rep_stride_q).
+ * yj [n_replicas][n_items][ldu] is replicated like qb.  Always biased (SVDpp has no option).
  */
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
-                   void *qi, void *bi, void *yj, int32_t n_factors, int32_t ld,
-                   const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int64_t rep_stride_q,
-                   int64_t rep_stride_b, int32_t n_waves, int32_t dup_items, int32_t dtype,
-                   void *stream);
+                   int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
+                   const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int32_t n_waves,
+                   int32_t dup_items, int32_t dtype, void *stream);
 
 /*
  * Item-side merge of an epoch-chunk: for each of the `n_seg` segments
@@ -113,19 +116,20 @@ int mf_apply_delta(int32_t n_seg, void *const *seg_ptr, void *const *seg_snap,
 /*
  * Batched SVD.estimate (matrix_factorization.pyx:269-299): for x < n, with u[x] < 0 / i[x] < 0
  * meaning an unknown user / item ('UKN__' ids, algo_base.py:137-144):
- *   biased:   est = mu (+bu[u] if known u) (+bi[i] if known i) (+ qi[i].(pu[u] + imp[u]) if both)
- *   unbiased: est = qi[i].pu[u] if both known, else impossible[x] = 1 (PredictionImpossible)
- * imp (nullable) is the SVD++ implicit term per user (mf_svdpp_user_implicit); with it this is
- * SVDpp.estimate (:506-522).  est is dtype, impossible is int32.
+ *   biased:   est = mu (+bu[u] if known u) (+b_i if known i) (+ q_i.(pu[u] + imp[u]) if both)
+ *   unbiased: est = q_i.pu[u] if both known, else impossible[x] = 1 (PredictionImpossible)
+ * imp (nullable, [n_users][ldu]) is the SVD++ implicit term per user (mf_svdpp_user_implicit);
+ * with it this is SVDpp.estimate (:506-522).  est is dtype, impossible is int32.
  */
-int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, const void *qi,
-               const void *bu, const void *bi, const void *imp, int32_t n_factors, int32_t ld,
+int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, const void *bu,
+               int32_t ldu, const void *qb, int32_t ldq, const void *imp, int32_t n_factors,
                int32_t biased, double global_mean, void *est, int32_t *impossible, int32_t dtype,
                void *stream);
 
-/* imp[u] = (sum_{j in I_u} yj[j]) / sqrt(|I_u|)  (SVDpp.estimate :518-520), zero for empty users. */
-int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, void *imp, int32_t n_factors,
-                           int32_t ld, int32_t dtype, void *stream);
+/* imp[u] = (sum_{j in I_u} yj[j]) / sqrt(|I_u|)  (SVDpp.estimate :518-520), zero for empty users;
+ * yj is replica 0, imp is [n_users][ldu]. */
+int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, int32_t ldu, void *imp,
+                           int32_t n_factors, int32_t dtype, void *stream);
 
 /* Self-test of the wavefront reduction: out[w] = sum of in[64w .. 64w+63], w < n_waves. */
 int mf_selftest_wave_sum(const void *in, void *out, int32_t n_waves, int32_t dtype, void *stream);

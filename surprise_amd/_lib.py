@@ -15,8 +15,9 @@ LIB_PATH = os.path.join(_HERE, "libsurprise_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "surprise_amd.h")
 
 MF_F32, MF_F64 = 0, 1
-MF_MODE_PLAIN, MF_MODE_ATOMIC, MF_MODE_REPLICA = 0, 1, 2
-MODES = {"plain": MF_MODE_PLAIN, "atomic": MF_MODE_ATOMIC, "replica": MF_MODE_REPLICA}
+MF_MODE_PLAIN, MF_MODE_ATOMIC, MF_MODE_REPLICA, MF_MODE_COHERENT = 0, 1, 2, 3
+MODES = {"plain": MF_MODE_PLAIN, "atomic": MF_MODE_ATOMIC, "replica": MF_MODE_REPLICA,
+         "coherent": MF_MODE_COHERENT}
 MAX_FACTORS = {MF_F32: 512, MF_F64: 256}
 
 
@@ -40,17 +41,17 @@ _vp, _i32, _i64, _dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.
 
 # name -> argtypes (all return int except mf_last_error)
 SIGNATURES = {
-    "mf_svd_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32,
-                     ctypes.POINTER(MfHyper), _i32, _i32, _i64, _i64, _i32, _i32, _i32, _vp],
-    "mf_svdpp_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
-                       ctypes.POINTER(MfHyper), _i32, _i32, _i64, _i64, _i32, _i32, _i32, _vp],
+    "mf_svd_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32, _i32,
+                     ctypes.POINTER(MfHyper), _i32, _i32, _i32, _i32, _i32, _vp],
+    "mf_svdpp_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp, _i32,
+                       ctypes.POINTER(MfHyper), _i32, _i32, _i32, _i32, _i32, _vp],
     "mf_replica_merge": [_i32, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64),
                          ctypes.POINTER(_i64), _i32, _vp, _i32, _i32, _vp],
     "mf_apply_delta": [_i32, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64),
                        ctypes.POINTER(_i64), _i32, _vp, _i32, _vp],
-    "mf_predict": [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _dbl, _vp, _vp,
+    "mf_predict": [_i64, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _dbl, _vp, _vp,
                    _i32, _vp],
-    "mf_svdpp_user_implicit": [ctypes.POINTER(MfCsr), _vp, _vp, _i32, _i32, _i32, _vp],
+    "mf_svdpp_user_implicit": [ctypes.POINTER(MfCsr), _vp, _i32, _vp, _i32, _i32, _vp],
     "mf_selftest_wave_sum": [_vp, _vp, _i32, _i32, _vp],
     "mf_version": [],
     "mf_last_error": [],

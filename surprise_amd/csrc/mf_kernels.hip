@@ -12,10 +12,10 @@
 //   * the item rows qi[i] / bi[i] (and yj for SVD++) are the shared, lock-free Hogwild! state;
 //   * a factor row is spread over the wave "strided": lane l holds elements l, l+64, l+128, ...
 //     so every gather/scatter instruction touches 64 consecutive dwords (256 B) of one row;
-//   * the user's (item, rating) stream is read in 64-entry chunks, one entry per lane, and the
-//     next PF item rows are gathered ahead of use (software pipeline) so that the dependent
-//     chain per rating is register-only: FMA partials -> DPP/permlane wave reduction -> error ->
-//     FMA updates;
+//   * the user's (item, rating) stream is read with scalar loads two groups ahead, and the item
+//     rows of the next kPF ratings are gathered ahead of use (software pipeline), so the
+//     dependent chain per rating is register-only: FMA partials -> DPP/permlane wave reduction
+//     -> error -> FMA updates;
 //   * the dot product is reduced with 4 DPP row ops + v_permlane16_swap + v_permlane32_swap
 //     (no LDS round trip), leaving the sum in every lane.
 // No MFMA: the path is gather/scatter-bound.
@@ -144,360 +144,270 @@ __device__ __forceinline__ int xcc_id() {
     return (int)(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 0xF);
 }
 
-// Item-side loads bypass the CU's vector L1 (global_load ... sc1, served by the XCD's L2):
-// the L1 is never refreshed by other CUs' stores, so a plain load of a hot item row can return
-// a stale copy for a long time and the following store then erases other waves' updates.
-template <typename T>
-__device__ __forceinline__ T ld_l2(const T *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// ---------------------------------------------------------------- buffer (SRSRC) memory ops
+//
+// Every load/store/atomic of the SGD pipeline goes through a buffer descriptor.  A lane that
+// must not touch memory (a factor column beyond the row, an item row of a masked "tail"
+// rating) gets a byte offset >= kOOB: the hardware range check turns its load into 0 and drops
+// its store, so the instruction stream has no exec-masked branches and every loop iteration
+// issues the same number of memory instructions -- which lets the compiler keep the row
+// prefetches of the next kPF ratings in flight behind counted vmcnt waits.
+
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;  // > every table's num_records (tables are < 2 GiB)
+constexpr int kSc1 = 16;                // gfx950 cache policy: sc1 (bypass the CU's L1)
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void *p, uint32_t bytes) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void *q = (void *)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)__builtin_amdgcn_readfirstlane(bytes),
+                                             0x00020000);
 }
 
 template <typename T>
-__device__ __forceinline__ void atomic_add(T *p, T v) {
-    atomicAdd(p, v);  // global_atomic_add_f32 / _f64, executed at the memory side (no CAS loop)
-}
+struct Buf;
 
-// The user's (item, rating) stream, read 64 entries per wave instruction (one per lane) and
-// double-buffered: `cur` covers [base, base+64), `nxt` covers [base+64, base+128).
-template <typename T>
-struct RatingStream {
-    const int32_t *items;
-    const T *ratings;
-    int64_t base;
-    int i_cur, i_nxt;
-    T r_cur, r_nxt;
-
-    int64_t end;
-
-    __device__ __forceinline__ void load(int64_t at, int lane, int &i, T &r) const {
-        const int64_t k = at + lane;
-        i = k < end ? items[k] : 0;
-        r = k < end ? ratings[k] : T(0);
+template <>
+struct Buf<float> {
+    template <int AUX>
+    __device__ static __forceinline__ float ld(rsrc_t r, uint32_t off) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX));
     }
-    __device__ __forceinline__ void init(const int32_t *it, const T *rt, int64_t s, int64_t e,
-                                         int lane) {
-        items = it; ratings = rt; base = s; end = e;
-        load(s, lane, i_cur, r_cur);
-        load(s + 64, lane, i_nxt, r_nxt);
+    template <int AUX>
+    __device__ static __forceinline__ void st(rsrc_t r, uint32_t off, float v) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, AUX);
     }
-    // entry k (base <= k < base + 128), uniform
-    __device__ __forceinline__ int item(int64_t k) const {
-        const int off = (int)(k - base);
-        return off < 64 ? readlane(i_cur, off) : readlane(i_nxt, off - 64);
-    }
-    __device__ __forceinline__ T rating(int64_t k) const {
-        const int off = (int)(k - base);
-        return off < 64 ? readlane(r_cur, off) : readlane(r_nxt, off - 64);
-    }
-    // keep k_next within the window: slide by one chunk once k_next passes base + 64
-    __device__ __forceinline__ void advance(int64_t k_next, int lane) {
-        if (k_next - base >= 64) {
-            base += 64;
-            i_cur = i_nxt; r_cur = r_nxt;
-            load(base + 64, lane, i_nxt, r_nxt);
-        }
+    __device__ static __forceinline__ void add(rsrc_t r, float *, uint32_t, uint32_t off, float v) {
+        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);  // memory-side add
     }
 };
 
-// ---------------------------------------------------------------- SVD epoch kernel
+template <>
+struct Buf<double> {
+    template <int AUX>
+    __device__ static __forceinline__ double ld(rsrc_t r, uint32_t off) {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX));
+    }
+    template <int AUX>
+    __device__ static __forceinline__ void st(rsrc_t r, uint32_t off, double v) {
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v), r,
+            off, 0, AUX);
+    }
+    // no buffer form of the f64 add: a predicated global atomic on the same bytes
+    __device__ static __forceinline__ void add(rsrc_t, double *base, uint32_t bytes, uint32_t off,
+                                               double v) {
+        if (off < bytes) atomicAdd(base + off / sizeof(double), v);
+    }
+};
 
-enum { kPlain = MF_MODE_PLAIN, kAtomic = MF_MODE_ATOMIC, kReplica = MF_MODE_REPLICA };
+// ---------------------------------------------------------------- SGD epoch kernel (SVD, SVD++)
 
-template <typename T, int V, int MODE>
-__global__ __launch_bounds__(kBlock) void svd_epoch_kernel(
+enum { kPlain = MF_MODE_PLAIN, kAtomic = MF_MODE_ATOMIC, kReplica = MF_MODE_REPLICA,
+       kCoherent = MF_MODE_COHERENT };
+
+// Item table row (ldq elements): [q_0 .. q_{K-1} | b_i | 0 ...].  The user row is extended in
+// registers with a constant 1 in column K, so <q_aug, p_aug> = <q_i, p_u> + b_i and the item
+// bias rides in the same gather / scatter as the item factors; its update
+// b_i += lr_bi (err * 1 - reg_bi b_i) is the factor rule with the per-column (lr, reg) swapped.
+template <typename T, int V, int MODE, bool PP, bool DUPS>
+__global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
-    T *__restrict__ pu, T *__restrict__ bu, T *qi, T *bi, int K, int ld, int biased,
-    Hyper<T> hp, int n_rep, int64_t rep_stride_q, int64_t rep_stride_b, int dups,
-    int64_t n_waves_req)
+    T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, int K, int biased,
+    Hyper<T> hp, int n_rep, int n_items, int64_t n_waves_req)
 {
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave;
+    // wave id through readfirstlane: the compiler then knows it (and every user index, CSR
+    // bound and loop counter derived from it) is wave-uniform -> SGPRs, scalar loads, scalar
+    // branches instead of exec-masked ones.
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int64_t grid_waves = ((int64_t)gridDim.x * kBlock) / kWave;
     const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
     if (wave >= n_waves) return;  // whole wave exits (a 1-wave launch still uses a 4-wave block)
 
-    T *q_tab = qi;
-    T *b_tab = bi;
-    if (MODE == kReplica) {
-        const int rep = xcc_id() % n_rep;
-        q_tab += rep * rep_stride_q;
-        b_tab += rep * rep_stride_b;
+    const int rep = MODE == kReplica ? xcc_id() % n_rep : 0;
+    const uint32_t qrow = (uint32_t)ldq * sizeof(T), yrow = (uint32_t)ldu * sizeof(T);
+    T *q_base = qb + (int64_t)rep * n_items * ldq;
+    T *y_base = PP ? yj + (int64_t)rep * n_items * ldu : nullptr;
+    const rsrc_t q_rs = make_rsrc(q_base, (uint32_t)n_items * qrow);
+    const rsrc_t y_rs = PP ? make_rsrc(y_base, (uint32_t)n_items * yrow) : q_rs;
+    constexpr int kStAux = MODE == kCoherent ? kSc1 : 0;
+
+    // per-lane column constants (column c = lane + 64 v)
+    uint32_t cq[V], cu[V];
+    T one[V], lrq[V], regq[V], lrp[V], regp[V], lry[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int c = lane + kWave * v;
+        cq[v] = c < ldq ? (uint32_t)c * sizeof(T) : kOOB;
+        cu[v] = c < ldu ? (uint32_t)c * sizeof(T) : kOOB;
+        const bool fac = c < K, bias = biased && c == K;
+        one[v] = bias ? T(1) : T(0);
+        lrq[v] = fac ? hp.lr_qi : (bias ? hp.lr_bi : T(0));
+        regq[v] = fac ? hp.reg_qi : (bias ? hp.reg_bi : T(0));
+        lrp[v] = fac ? hp.lr_pu : T(0);
+        regp[v] = fac ? hp.reg_pu : T(0);
+        lry[v] = fac ? hp.lr_yj : T(0);
     }
-    bool fin[V];  // lane holds a real factor column for slot v
-#pragma unroll
-    for (int v = 0; v < V; ++v) fin[v] = lane + kWave * v < K;
-
-    for (int64_t w = wave; w < n_sched; w += n_waves) {
-        const int u = sched[w];
-        const int64_t s = row_ptr[u], e = row_ptr[u + 1];
-        if (s >= e) continue;
-
-        T p[V];
-#pragma unroll
-        for (int v = 0; v < V; ++v) p[v] = fin[v] ? pu[(int64_t)u * ld + lane + kWave * v] : T(0);
-        T bu_u = bu[u];
-
-        RatingStream<T> rs;
-        rs.init(items, ratings, s, e, lane);
-
-        int s_i[kPF];
-        T s_r[kPF], s_b[kPF], s_q[kPF][V];
-        auto issue = [&](int slot, int64_t k) {
-            const int i = rs.item(k);
-            s_i[slot] = i;
-            s_r[slot] = rs.rating(k);
-            s_b[slot] = ld_l2(b_tab + i);
-            const T *row = q_tab + (int64_t)i * ld + lane;
-#pragma unroll
-            for (int v = 0; v < V; ++v) s_q[slot][v] = fin[v] ? ld_l2(row + kWave * v) : T(0);
-        };
-#pragma unroll
-        for (int d = 0; d < kPF; ++d)
-            if (s + d < e) issue(d, s + d);
-
-        for (int64_t t = s; t < e; t += kPF) {
-#pragma unroll
-            for (int d = 0; d < kPF; ++d) {
-                const int64_t k = t + d;
-                if (k >= e) break;
-                const int i = s_i[d];
-                const T r = s_r[d];
-                const T b_old = s_b[d];
-                // dot = <q_i, p_u>  (mf.pyx:247-249)
-                T part = T(0);
-#pragma unroll
-                for (int v = 0; v < V; ++v) part += s_q[d][v] * p[v];
-                const T dot = wave_sum(part);
-                const T err = r - (hp.gm + bu_u + b_old + dot);  // mf.pyx:250
-                T b_new = b_old;
-                if (biased) {  // mf.pyx:253-255
-                    bu_u += hp.lr_bu * (err - hp.reg_bu * bu_u);
-                    b_new = b_old + hp.lr_bi * (err - hp.reg_bi * b_old);
-                }
-                T q_new[V];
-#pragma unroll
-                for (int v = 0; v < V; ++v) {  // mf.pyx:258-262 (old puf, qif)
-                    const T puf = p[v], qif = s_q[d][v];
-                    p[v] = puf + hp.lr_pu * (err * qif - hp.reg_pu * puf);
-                    q_new[v] = qif + hp.lr_qi * (err * puf - hp.reg_qi * qif);
-                }
-                T *row = q_tab + (int64_t)i * ld + lane;
-                if (MODE == kAtomic) {
-#pragma unroll
-                    for (int v = 0; v < V; ++v)
-                        if (fin[v]) atomic_add(row + kWave * v, q_new[v] - s_q[d][v]);
-                    if (biased && lane == 0) atomic_add(b_tab + i, b_new - b_old);
-                } else {
-#pragma unroll
-                    for (int v = 0; v < V; ++v)
-                        if (fin[v]) row[kWave * v] = q_new[v];
-                    if (biased && lane == 0) b_tab[i] = b_new;
-                }
-                // next gather for this slot
-                const int64_t kn = k + kPF;
-                if (kn < e) issue(d, kn);
-                if (dups) {  // same item again within this user's window: forward the new row
-#pragma unroll
-                    for (int dd = 0; dd < kPF; ++dd) {
-                        if (s_i[dd] == i && (dd != d || kn < e)) {
-                            s_b[dd] = b_new;
-#pragma unroll
-                            for (int v = 0; v < V; ++v) s_q[dd][v] = q_new[v];
-                        }
-                    }
-                }
-            }
-            rs.advance(t + 2 * kPF, lane);
-        }
-#pragma unroll
-        for (int v = 0; v < V; ++v)
-            if (fin[v]) pu[(int64_t)u * ld + lane + kWave * v] = p[v];
-        if (lane == 0) bu[u] = bu_u;
-    }
-}
-
-// ---------------------------------------------------------------- SVD++ epoch kernel
-
-template <typename T, int V, int MODE>
-__global__ __launch_bounds__(kBlock) void svdpp_epoch_kernel(
-    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
-    const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
-    T *__restrict__ pu, T *__restrict__ bu, T *qi, T *bi, T *yj, int K, int ld, Hyper<T> hp,
-    int n_rep, int64_t rep_stride_q, int64_t rep_stride_b, int dups, int64_t n_waves_req)
-{
-    const int lane = threadIdx.x & (kWave - 1);
-    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave;
-    const int64_t grid_waves = ((int64_t)gridDim.x * kBlock) / kWave;
-    const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
-    if (wave >= n_waves) return;
-
-    T *q_tab = qi, *y_tab = yj, *b_tab = bi;
-    if (MODE == kReplica) {
-        const int rep = xcc_id() % n_rep;
-        q_tab += rep * rep_stride_q;
-        y_tab += rep * rep_stride_q;
-        b_tab += rep * rep_stride_b;
-    }
-    bool fin[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) fin[v] = lane + kWave * v < K;
+    const T lr_bu = biased ? hp.lr_bu : T(0);
     const T decay = T(1) - hp.lr_yj * hp.reg_yj;
 
     for (int64_t w = wave; w < n_sched; w += n_waves) {
         const int u = sched[w];
-        const int64_t s = row_ptr[u], e = row_ptr[u + 1];
-        if (s >= e) continue;
-        const T sqrt_n = sqrt(T(e - s));  // mf.pyx:470
+        const int64_t s = row_ptr[u];
+        const int n = (int)(row_ptr[u + 1] - s);  // |I_u| (< 2^31)
+        if (n <= 0) continue;
+        // the user's (item, rating) stream, read with scalar loads (uniform addresses ->
+        // s_load, counted by lgkmcnt, out of the vector-memory queue the row gathers use)
+        const int32_t *__restrict__ it = items + s;
+        const T *__restrict__ rt = ratings + s;
+        const rsrc_t p_rs = make_rsrc(pu + (int64_t)u * ldu, (uint32_t)K * sizeof(T));
+        const rsrc_t b_rs = make_rsrc(bu + u, sizeof(T));
 
-        // 1) u_impl = sum_j y_j / sqrt|I_u|   (mf.pyx:473-476, same per-term division)
-        T imp[V];
+        T p[V];
 #pragma unroll
-        for (int v = 0; v < V; ++v) imp[v] = T(0);
-        for (int64_t c0 = s; c0 < e; c0 += kWave) {
-            const int jl = c0 + lane < e ? items[c0 + lane] : 0;
-            const int cnt = e - c0 < kWave ? (int)(e - c0) : kWave;
-            int x = 0;
-            for (; x + 8 <= cnt; x += 8) {
+        for (int v = 0; v < V; ++v) p[v] = Buf<T>::template ld<0>(p_rs, cu[v]) + one[v];
+        T bu_u = Buf<T>::template ld<0>(b_rs, 0);
+        const T sqrt_n = sqrt(T(n));  // mf.pyx:470
+
+        // SVD++ (1): u_impl = sum_{j in I_u} y_j / sqrt|I_u|  (mf.pyx:473-476, per-term division)
+        T imp[V], cacc[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) imp[v] = cacc[v] = T(0);
+        if (PP) {
+            for (int x = 0; x < n; x += 8) {
                 T g[8][V];
 #pragma unroll
                 for (int a = 0; a < 8; ++a) {
-                    const T *row = y_tab + (int64_t)readlane(jl, x + a) * ld + lane;
+                    const int j = x + a < n ? x + a : n - 1;
+                    const uint32_t ro = (uint32_t)it[j] * yrow + (x + a < n ? 0u : kOOB);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) g[a][v] = fin[v] ? ld_l2(row + kWave * v) : T(0);
+                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kSc1>(y_rs, ro + cu[v]);
                 }
 #pragma unroll
                 for (int a = 0; a < 8; ++a)
 #pragma unroll
                     for (int v = 0; v < V; ++v) imp[v] += g[a][v] / sqrt_n;
             }
-            for (; x < cnt; ++x) {
-                const T *row = y_tab + (int64_t)readlane(jl, x) * ld + lane;
-#pragma unroll
-                for (int v = 0; v < V; ++v) imp[v] += (fin[v] ? ld_l2(row + kWave * v) : T(0)) / sqrt_n;
-            }
         }
-
-        // 2) the user's ratings in order, y_j kept implicit as y_j(start)*A + c
-        T p[V], cacc[V];
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-            p[v] = fin[v] ? pu[(int64_t)u * ld + lane + kWave * v] : T(0);
-            cacc[v] = T(0);
-        }
-        T bu_u = bu[u];
         T A = T(1);
 
-        RatingStream<T> rs;
-        rs.init(items, ratings, s, e, lane);
-        int s_i[kPF];
-        T s_r[kPF], s_b[kPF], s_q[kPF][V];
-        auto issue = [&](int slot, int64_t k) {
-            const int i = rs.item(k);
-            s_i[slot] = i;
-            s_r[slot] = rs.rating(k);
-            s_b[slot] = ld_l2(b_tab + i);
-            const T *row = q_tab + (int64_t)i * ld + lane;
-#pragma unroll
-            for (int v = 0; v < V; ++v) s_q[slot][v] = fin[v] ? ld_l2(row + kWave * v) : T(0);
+        // software pipeline: slot d holds the gathered row of rating j0 + d.  The item ids and
+        // ratings of a group travel one group ahead in VGPR lanes (lane l < kPF holds entry l),
+        // are loaded once per group by two unconditional vector loads, and are read with
+        // v_readlane when the group's rows are gathered.
+        auto grp_load = [&](int j0, int &gi, T &gr) {
+            int j = j0 + (lane & (kPF - 1));
+            j = j < n ? j : n - 1;
+            gi = it[j];
+            gr = rt[j];
         };
-#pragma unroll
-        for (int d = 0; d < kPF; ++d)
-            if (s + d < e) issue(d, s + d);
-
-        for (int64_t t = s; t < e; t += kPF) {
+        int gi_b, gi_n;
+        T gr_b, gr_n;
+        uint32_t s_off[kPF];
+        T s_r[kPF], s_q[kPF][V];
+        {
+            int gi_a;
+            T gr_a;
+            grp_load(0, gi_a, gr_a);
+            grp_load(kPF, gi_b, gr_b);
+            __builtin_amdgcn_sched_barrier(0);
+            // (an out-of-range rating adds kOOB to a real row offset instead of selecting kOOB,
+            // so the item id is used unconditionally and no branch is generated)
 #pragma unroll
             for (int d = 0; d < kPF; ++d) {
-                const int64_t k = t + d;
-                if (k >= e) break;
-                const int i = s_i[d];
-                const T r = s_r[d];
-                const T b_old = s_b[d];
-                T part = T(0);  // mf.pyx:479-481
+                s_off[d] = (uint32_t)readlane(gi_a, d) * qrow + (d < n ? 0u : kOOB);
+                s_r[d] = readlane(gr_a, d);
 #pragma unroll
-                for (int v = 0; v < V; ++v) part += s_q[d][v] * (p[v] + imp[v]);
-                const T dot = wave_sum(part);
-                const T err = r - (hp.gm + bu_u + b_old + dot);  // mf.pyx:483
-                bu_u += hp.lr_bu * (err - hp.reg_bu * bu_u);     // mf.pyx:486-487
-                const T b_new = b_old + hp.lr_bi * (err - hp.reg_bi * b_old);
-                T q_new[V];
+                for (int v = 0; v < V; ++v) s_q[d][v] = Buf<T>::template ld<kSc1>(q_rs, s_off[d] + cq[v]);
+                __builtin_amdgcn_sched_barrier(0);  // keep slot order: slot 0's row lands first
+            }
+        }
+        for (int j0 = 0; j0 < n; j0 += kPF) {
+            grp_load(j0 + 2 * kPF, gi_n, gr_n);
 #pragma unroll
-                for (int v = 0; v < V; ++v) {  // mf.pyx:490-498
-                    const T puf = p[v], qif = s_q[d][v];
-                    p[v] = puf + hp.lr_pu * (err * qif - hp.reg_pu * puf);
-                    q_new[v] = qif + hp.lr_qi * (err * (puf + imp[v]) - hp.reg_qi * qif);
-                    cacc[v] = decay * cacc[v] + hp.lr_yj * (err * qif / sqrt_n);
-                    imp[v] = decay * imp[v] + hp.lr_yj * err * qif;
-                }
-                A *= decay;
-                T *row = q_tab + (int64_t)i * ld + lane;
-                if (MODE == kAtomic) {
+            for (int d = 0; d < kPF; ++d) {
+                const bool valid = j0 + d < n;  // tail slots run masked (OOB row, no state change)
+                T part = T(0);
 #pragma unroll
-                    for (int v = 0; v < V; ++v)
-                        if (fin[v]) atomic_add(row + kWave * v, q_new[v] - s_q[d][v]);
-                    if (lane == 0) atomic_add(b_tab + i, b_new - b_old);
-                } else {
+                for (int v = 0; v < V; ++v) part += s_q[d][v] * (PP ? p[v] + imp[v] : p[v]);
+                const T dot = wave_sum(part);                 // <q_i, p_u (+imp)> + b_i
+                const T err = s_r[d] - (hp.gm + bu_u + dot);  // mf.pyx:250 / :483
+                T qn[V];
 #pragma unroll
-                    for (int v = 0; v < V; ++v)
-                        if (fin[v]) row[kWave * v] = q_new[v];
-                    if (lane == 0) b_tab[i] = b_new;
-                }
-                const int64_t kn = k + kPF;
-                if (kn < e) issue(d, kn);
-                if (dups) {
-#pragma unroll
-                    for (int dd = 0; dd < kPF; ++dd) {
-                        if (s_i[dd] == i && (dd != d || kn < e)) {
-                            s_b[dd] = b_new;
-#pragma unroll
-                            for (int v = 0; v < V; ++v) s_q[dd][v] = q_new[v];
-                        }
+                for (int v = 0; v < V; ++v) {  // mf.pyx:258-262 / :490-498, old puf and qif
+                    const T q = s_q[d][v], pv = p[v];
+                    const T pe = PP ? pv + imp[v] : pv;
+                    qn[v] = q + lrq[v] * (err * pe - regq[v] * q);
+                    const T pn = pv + lrp[v] * (err * q - regp[v] * pv);
+                    p[v] = valid ? pn : pv;
+                    if (PP) {
+                        const T cn = decay * cacc[v] + lry[v] * (err * q / sqrt_n);
+                        const T in = decay * imp[v] + lry[v] * err * q;
+                        cacc[v] = valid ? cn : cacc[v];
+                        imp[v] = valid ? in : imp[v];
                     }
                 }
+                const T bun = bu_u + lr_bu * (err - hp.reg_bu * bu_u);  // mf.pyx:253-254
+                bu_u = valid ? bun : bu_u;
+                if (PP) A = valid ? A * decay : A;
+                const uint32_t off = s_off[d];
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    if (MODE == kAtomic)
+                        Buf<T>::add(q_rs, q_base, (uint32_t)n_items * qrow, off + cq[v], qn[v] - s_q[d][v]);
+                    else
+                        Buf<T>::template st<kStAux>(q_rs, off + cq[v], qn[v]);
+                }
+                // keep the next gather below the last use of the slot's old row: hoisting it would
+                // need a second register set and a copy (and a wait) at the loop latch
+                __builtin_amdgcn_sched_barrier(0);
+                s_off[d] = (uint32_t)readlane(gi_b, d) * qrow + (j0 + kPF + d < n ? 0u : kOOB);
+                s_r[d] = readlane(gr_b, d);
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    s_q[d][v] = Buf<T>::template ld<kSc1>(q_rs, s_off[d] + cq[v]);
+                if (DUPS && off != kOOB) {  // same item again within the window: forward the row
+#pragma unroll
+                    for (int dd = 0; dd < kPF; ++dd)
+                        if (s_off[dd] == off)
+#pragma unroll
+                            for (int v = 0; v < V; ++v) s_q[dd][v] = qn[v];
+                }
             }
-            rs.advance(t + 2 * kPF, lane);
+            gi_b = gi_n;
+            gr_b = gr_n;
         }
 #pragma unroll
-        for (int v = 0; v < V; ++v)
-            if (fin[v]) pu[(int64_t)u * ld + lane + kWave * v] = p[v];
-        if (lane == 0) bu[u] = bu_u;
+        for (int v = 0; v < V; ++v) Buf<T>::template st<0>(p_rs, cu[v], p[v]);
+        Buf<T>::template st<0>(b_rs, lane == 0 ? 0u : kOOB, bu_u);
 
-        // 3) y_j <- A y_j + c  for every j in I_u
-        for (int64_t c0 = s; c0 < e; c0 += kWave) {
-            const int jl = c0 + lane < e ? items[c0 + lane] : 0;
-            const int cnt = e - c0 < kWave ? (int)(e - c0) : kWave;
-            int x = 0;
-            for (; x + 8 <= cnt; x += 8) {
+        // SVD++ (3): y_j <- A y_j + c for every j in I_u
+        if (PP) {
+            for (int x = 0; x < n; x += 8) {
                 T g[8][V];
-                T *rows[8];
+                uint32_t ro[8];
 #pragma unroll
                 for (int a = 0; a < 8; ++a) {
-                    rows[a] = y_tab + (int64_t)readlane(jl, x + a) * ld + lane;
+                    const int j = x + a < n ? x + a : n - 1;
+                    ro[a] = (uint32_t)it[j] * yrow + (x + a < n ? 0u : kOOB);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) g[a][v] = fin[v] ? ld_l2(rows[a] + kWave * v) : T(0);
+                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kSc1>(y_rs, ro[a] + cu[v]);
                 }
 #pragma unroll
                 for (int a = 0; a < 8; ++a)
 #pragma unroll
                     for (int v = 0; v < V; ++v) {
-                        if (!fin[v]) continue;
                         if (MODE == kAtomic)
-                            atomic_add(rows[a] + kWave * v, (A - T(1)) * g[a][v] + cacc[v]);
+                            Buf<T>::add(y_rs, y_base, (uint32_t)n_items * yrow, ro[a] + cu[v],
+                                        (A - T(1)) * g[a][v] + cacc[v]);
                         else
-                            rows[a][kWave * v] = A * g[a][v] + cacc[v];
+                            Buf<T>::template st<kStAux>(y_rs, ro[a] + cu[v], A * g[a][v] + cacc[v]);
                     }
-            }
-            for (; x < cnt; ++x) {
-                T *row = y_tab + (int64_t)readlane(jl, x) * ld + lane;
-#pragma unroll
-                for (int v = 0; v < V; ++v) {
-                    if (!fin[v]) continue;
-                    const T y = ld_l2(row + kWave * v);
-                    if (MODE == kAtomic)
-                        atomic_add(row + kWave * v, (A - T(1)) * y + cacc[v]);
-                    else
-                        row[kWave * v] = A * y + cacc[v];
-                }
             }
         }
     }
@@ -554,14 +464,15 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(SegDesc d, int n_rep, con
     }
 }
 
+
 // ---------------------------------------------------------------- inference
 
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void predict_kernel(
     int64_t n, const int32_t *__restrict__ uu, const int32_t *__restrict__ ii,
-    const T *__restrict__ pu, const T *__restrict__ qi, const T *__restrict__ bu,
-    const T *__restrict__ bi, const T *__restrict__ imp, int K, int ld, int biased, T gm,
-    T *__restrict__ est, int32_t *__restrict__ impossible)
+    const T *__restrict__ pu, const T *__restrict__ bu, int ldu, const T *__restrict__ qb,
+    int ldq, const T *__restrict__ imp, int K, int biased, T gm, T *__restrict__ est,
+    int32_t *__restrict__ impossible)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave;
@@ -575,9 +486,9 @@ __global__ __launch_bounds__(kBlock) void predict_kernel(
             for (int v = 0; v < V; ++v) {
                 const int f = lane + kWave * v;
                 if (f < K) {
-                    T pf = pu[(int64_t)u * ld + f];
-                    if (imp) pf += imp[(int64_t)u * ld + f];
-                    part += qi[(int64_t)i * ld + f] * pf;
+                    T pf = pu[(int64_t)u * ldu + f];
+                    if (imp) pf += imp[(int64_t)u * ldu + f];
+                    part += qb[(int64_t)i * ldq + f] * pf;
                 }
             }
         }
@@ -585,14 +496,14 @@ __global__ __launch_bounds__(kBlock) void predict_kernel(
         if (lane == 0) {
             int bad = 0;
             T e;
-            if (biased) {
+            if (biased) {  // mf.pyx:283-293 / :510-521
                 e = gm;
                 if (ku) e += bu[u];
-                if (ki) e += bi[i];
+                if (ki) e += qb[(int64_t)i * ldq + K];
                 if (ku && ki) e += dot;
             } else if (ku && ki) {
                 e = dot;
-            } else {
+            } else {  // PredictionImpossible (mf.pyx:295-296)
                 e = T(0);
                 bad = 1;
             }
@@ -605,7 +516,7 @@ __global__ __launch_bounds__(kBlock) void predict_kernel(
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void user_implicit_kernel(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items, int n_users,
-    const T *__restrict__ yj, T *__restrict__ imp, int K, int ld)
+    const T *__restrict__ yj, int ldu, T *__restrict__ imp, int K)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave;
@@ -615,8 +526,8 @@ __global__ __launch_bounds__(kBlock) void user_implicit_kernel(
         T acc[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) acc[v] = T(0);
-        for (int64_t k = s; k < e; ++k) {
-            const T *row = yj + (int64_t)items[k] * ld + lane;
+        for (int64_t k = s; k < e; ++k) {  // sum(yj[j] for j in ur[u]) in ur order (mf.pyx:518)
+            const T *row = yj + (int64_t)items[k] * ldu + lane;
 #pragma unroll
             for (int v = 0; v < V; ++v)
                 if (lane + kWave * v < K) acc[v] += row[kWave * v];
@@ -625,7 +536,7 @@ __global__ __launch_bounds__(kBlock) void user_implicit_kernel(
 #pragma unroll
         for (int v = 0; v < V; ++v) {
             const int f = lane + kWave * v;
-            if (f < ld) imp[u * ld + f] = (e > s && f < K) ? acc[v] / sq : T(0);
+            if (f < ldu) imp[u * ldu + f] = (e > s && f < K) ? acc[v] / sq : T(0);
         }
     }
 }
@@ -648,8 +559,7 @@ int grid_for_waves(int64_t waves) {
     return (int)blocks;
 }
 
-// Default grid: enough waves to hold every scheduled user, capped at 16 waves per CU.
-int64_t default_waves(int64_t n_sched) {
+int n_cus() {
     static int n_cu = 0;
     if (n_cu == 0) {
         int dev = 0;
@@ -658,63 +568,92 @@ int64_t default_waves(int64_t n_sched) {
             n_cu = prop.multiProcessorCount;
         if (n_cu <= 0) n_cu = 256;
     }
-    const int64_t cap = (int64_t)n_cu * 16;
+    return n_cu;
+}
+
+// Default grid: enough waves to hold every scheduled user, capped at 16 waves per CU.
+int64_t default_waves(int64_t n_sched) {
+    const int64_t cap = (int64_t)n_cus() * 16;
     return n_sched < cap ? n_sched : cap;
 }
 
-template <typename T, int V, int MODE>
-int launch_svd_v(const mf_csr_t *c, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
-                 void *qi, void *bi, int K, int ld, int biased, const mf_hyper_t *hp, int n_rep,
-                 int64_t rsq, int64_t rsb, int64_t waves, int dups, hipStream_t st)
-{
-    hipLaunchKernelGGL((svd_epoch_kernel<T, V, MODE>), dim3(grid_for_waves(waves)), dim3(kBlock), 0,
-                       st, c->row_ptr, c->items, (const T *)c->ratings, sched, n_sched, (T *)pu,
-                       (T *)bu, (T *)qi, (T *)bi, K, ld, biased, cast_hyper<T>(hp), n_rep, rsq, rsb,
-                       dups, waves);
-    return check_launch("svd_epoch_kernel");
-}
-
-template <typename T, int V, int MODE>
-int launch_svdpp_v(const mf_csr_t *c, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
-                   void *qi, void *bi, void *yj, int K, int ld, const mf_hyper_t *hp, int n_rep,
-                   int64_t rsq, int64_t rsb, int64_t waves, int dups, hipStream_t st)
-{
-    hipLaunchKernelGGL((svdpp_epoch_kernel<T, V, MODE>), dim3(grid_for_waves(waves)), dim3(kBlock),
-                       0, st, c->row_ptr, c->items, (const T *)c->ratings, sched, n_sched,
-                       (T *)pu, (T *)bu, (T *)qi, (T *)bi, (T *)yj, K, ld, cast_hyper<T>(hp),
-                       n_rep, rsq, rsb, dups, waves);
-    return check_launch("svdpp_epoch_kernel");
-}
-
 // V = elements per lane = ceil(ld / 64)
-template <typename T, int MODE, typename F>
+template <typename T, typename F>
 int dispatch_v(int ld, F &&f)
 {
     const int v = (ld + kWave - 1) / kWave;
     if (v <= 1) return f(std::integral_constant<int, 1>{});
     if (v <= 2) return f(std::integral_constant<int, 2>{});
+    if (v <= 3) return f(std::integral_constant<int, 3>{});
     if (v <= 4) return f(std::integral_constant<int, 4>{});
-    if (sizeof(T) == 4 && v <= 8) return f(std::integral_constant<int, 8>{});
+    if constexpr (sizeof(T) == 4) {
+        if (v <= 6) return f(std::integral_constant<int, 6>{});
+        if (v <= 9) return f(std::integral_constant<int, 9>{});
+    } else {
+        if (v <= 5) return f(std::integral_constant<int, 5>{});
+    }
     return set_err(MF_E_ARG, "n_factors/ld too large");
 }
 
-int check_common(const mf_csr_t *c, int K, int ld, int mode, int n_rep, int dtype)
+int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const void *bu,
+                const void *qb, const mf_hyper_t *hp, int K, int ldu, int ldq, int mode,
+                int n_rep, int dtype)
 {
     if (!c || !c->row_ptr || !c->items || !c->ratings) return set_err(MF_E_ARG, "null csr");
-    if (K < 1 || ld < K) return set_err(MF_E_ARG, "need 1 <= n_factors <= ld");
-    if (dtype == MF_F32 && ld > MF_MAX_FACTORS_F32) return set_err(MF_E_ARG, "ld > 512 (f32)");
-    if (dtype == MF_F64 && ld > MF_MAX_FACTORS_F64) return set_err(MF_E_ARG, "ld > 256 (f64)");
+    if (!sched || !pu || !bu || !qb || !hp) return set_err(MF_E_ARG, "null argument");
     if (dtype != MF_F32 && dtype != MF_F64) return set_err(MF_E_ARG, "bad dtype");
-    if (mode < MF_MODE_PLAIN || mode > MF_MODE_REPLICA) return set_err(MF_E_ARG, "bad mode");
-    if (mode == MF_MODE_REPLICA && (n_rep < 1 || n_rep > 16))
-        return set_err(MF_E_ARG, "n_replicas must be in [1, 16]");
+    const int maxk = dtype == MF_F32 ? MF_MAX_FACTORS_F32 : MF_MAX_FACTORS_F64;
+    if (K < 1 || K > maxk) return set_err(MF_E_ARG, "n_factors out of range");
+    if (ldu < K || ldq < K + 1) return set_err(MF_E_ARG, "need ldu >= n_factors, ldq >= n_factors+1");
+    if (mode < MF_MODE_PLAIN || mode > MF_MODE_COHERENT) return set_err(MF_E_ARG, "bad mode");
+    if (n_rep < 1 || n_rep > 16) return set_err(MF_E_ARG, "n_replicas must be in [1, 16]");
+    const size_t esz = dtype == MF_F32 ? 4 : 8;
+    if ((size_t)c->n_items * (size_t)ldq * esz >= (size_t)kOOB)
+        return set_err(MF_E_UNSUPPORTED, "item table >= 2 GiB per replica");
+    if ((size_t)K * esz >= (size_t)kOOB) return set_err(MF_E_UNSUPPORTED, "row too long");
     return 0;
+}
+
+template <bool PP>
+int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
+                 int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t K, int32_t biased,
+                 const mf_hyper_t *hp, int32_t mode, int32_t n_rep, int32_t n_waves,
+                 int32_t dups, int32_t dtype, void *stream)
+{
+    if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, n_rep, dtype)) return rc;
+    if (PP && !yj) return set_err(MF_E_ARG, "null yj");
+    if (n_sched <= 0) return 0;
+    const int64_t waves = n_waves > 0 ? n_waves : default_waves(n_sched);
+    hipStream_t st = (hipStream_t)stream;
+    auto run = [&](auto tag_t, auto mode_c) -> int {
+        using T = decltype(tag_t);
+        constexpr int M = decltype(mode_c)::value;
+        return dispatch_v<T>(ldq, [&](auto vc) -> int {
+            constexpr int V = decltype(vc)::value;
+            auto kern = dups ? mf_epoch_kernel<T, V, M, PP, true> : mf_epoch_kernel<T, V, M, PP, false>;
+            hipLaunchKernelGGL(kern, dim3(grid_for_waves(waves)), dim3(kBlock), 0, st,
+                               csr->row_ptr, csr->items, (const T *)csr->ratings, sched, n_sched,
+                               (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, K, biased,
+                               cast_hyper<T>(hp), n_rep, csr->n_items, waves);
+            return check_launch(PP ? "mf_epoch_kernel<svdpp>" : "mf_epoch_kernel<svd>");
+        });
+    };
+    auto by_mode = [&](auto tag_t) -> int {
+        switch (mode) {
+            case MF_MODE_PLAIN: return run(tag_t, std::integral_constant<int, kPlain>{});
+            case MF_MODE_ATOMIC: return run(tag_t, std::integral_constant<int, kAtomic>{});
+            case MF_MODE_REPLICA: return run(tag_t, std::integral_constant<int, kReplica>{});
+            default: return run(tag_t, std::integral_constant<int, kCoherent>{});
+        }
+    };
+    return dtype == MF_F32 ? by_mode(float{}) : by_mode(double{});
 }
 
 int build_segs(SegDesc &d, int n_seg, void *const *ptr, void *const *snap, const int64_t *len,
                const int64_t *stride)
 {
-    if (n_seg < 1 || n_seg > 8) return set_err(MF_E_ARG, "n_seg must be in [1, 8]");
+    if (n_seg < 1 || n_seg > 8 || !ptr || !snap || !len || !stride)
+        return set_err(MF_E_ARG, "n_seg must be in [1, 8] with non-null descriptors");
     d.n_seg = n_seg;
     d.off[0] = 0;
     for (int s = 0; s < n_seg; ++s) {
@@ -743,70 +682,26 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 100; }
+int mf_version(void) { return 200; }
 
 const char *mf_last_error(void) { return g_err; }
 
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
-                 void *qi, void *bi, int32_t n_factors, int32_t ld, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int64_t rep_stride_q,
-                 int64_t rep_stride_b, int32_t n_waves, int32_t dup_items, int32_t dtype,
-                 void *stream)
+                 int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
+                 const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int32_t n_waves,
+                 int32_t dup_items, int32_t dtype, void *stream)
 {
-    if (int rc = check_common(csr, n_factors, ld, mode, n_replicas, dtype)) return rc;
-    if (!hp || !sched || !pu || !bu || !qi || !bi) return set_err(MF_E_ARG, "null argument");
-    if (n_sched <= 0) return 0;
-    const int64_t waves = n_waves > 0 ? n_waves : default_waves(n_sched);
-    hipStream_t st = (hipStream_t)stream;
-    auto run = [&](auto tag_t, auto mode_c) -> int {
-        using T = decltype(tag_t);
-        constexpr int M = decltype(mode_c)::value;
-        return dispatch_v<T, M>(ld, [&](auto vc) -> int {
-            return launch_svd_v<T, decltype(vc)::value, M>(csr, sched, n_sched, pu, bu, qi, bi,
-                                                          n_factors, ld, biased, hp, n_replicas,
-                                                          rep_stride_q, rep_stride_b, waves,
-                                                          dup_items, st);
-        });
-    };
-    auto by_mode = [&](auto tag_t) -> int {
-        switch (mode) {
-            case MF_MODE_PLAIN: return run(tag_t, std::integral_constant<int, kPlain>{});
-            case MF_MODE_ATOMIC: return run(tag_t, std::integral_constant<int, kAtomic>{});
-            default: return run(tag_t, std::integral_constant<int, kReplica>{});
-        }
-    };
-    return dtype == MF_F32 ? by_mode(float{}) : by_mode(double{});
+    return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, nullptr, n_factors,
+                               biased, hp, mode, n_replicas, n_waves, dup_items, dtype, stream);
 }
 
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
-                   void *qi, void *bi, void *yj, int32_t n_factors, int32_t ld,
-                   const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int64_t rep_stride_q,
-                   int64_t rep_stride_b, int32_t n_waves, int32_t dup_items, int32_t dtype,
-                   void *stream)
+                   int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
+                   const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int32_t n_waves,
+                   int32_t dup_items, int32_t dtype, void *stream)
 {
-    if (int rc = check_common(csr, n_factors, ld, mode, n_replicas, dtype)) return rc;
-    if (!hp || !sched || !pu || !bu || !qi || !bi || !yj) return set_err(MF_E_ARG, "null argument");
-    if (n_sched <= 0) return 0;
-    const int64_t waves = n_waves > 0 ? n_waves : default_waves(n_sched);
-    hipStream_t st = (hipStream_t)stream;
-    auto run = [&](auto tag_t, auto mode_c) -> int {
-        using T = decltype(tag_t);
-        constexpr int M = decltype(mode_c)::value;
-        return dispatch_v<T, M>(ld, [&](auto vc) -> int {
-            return launch_svdpp_v<T, decltype(vc)::value, M>(csr, sched, n_sched, pu, bu, qi, bi,
-                                                            yj, n_factors, ld, hp, n_replicas,
-                                                            rep_stride_q, rep_stride_b, waves,
-                                                            dup_items, st);
-        });
-    };
-    auto by_mode = [&](auto tag_t) -> int {
-        switch (mode) {
-            case MF_MODE_PLAIN: return run(tag_t, std::integral_constant<int, kPlain>{});
-            case MF_MODE_ATOMIC: return run(tag_t, std::integral_constant<int, kAtomic>{});
-            default: return run(tag_t, std::integral_constant<int, kReplica>{});
-        }
-    };
-    return dtype == MF_F32 ? by_mode(float{}) : by_mode(double{});
+    return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, n_factors, 1, hp,
+                              mode, n_replicas, n_waves, dup_items, dtype, stream);
 }
 
 int mf_replica_merge(int32_t n_seg, void *const *seg_ptr, void *const *seg_snap,
@@ -850,23 +745,24 @@ int mf_apply_delta(int32_t n_seg, void *const *seg_ptr, void *const *seg_snap,
     return check_launch("apply_kernel");
 }
 
-int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, const void *qi,
-               const void *bu, const void *bi, const void *imp, int32_t n_factors, int32_t ld,
+int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, const void *bu,
+               int32_t ldu, const void *qb, int32_t ldq, const void *imp, int32_t n_factors,
                int32_t biased, double global_mean, void *est, int32_t *impossible, int32_t dtype,
                void *stream)
 {
     if (n <= 0) return 0;
-    if (!u || !i || !pu || !qi || !bu || !bi || !est || !impossible)
+    if (!u || !i || !pu || !bu || !qb || !est || !impossible)
         return set_err(MF_E_ARG, "null argument");
-    if (n_factors < 1 || ld < n_factors) return set_err(MF_E_ARG, "need 1 <= n_factors <= ld");
+    if (n_factors < 1 || ldu < n_factors || ldq < n_factors + 1)
+        return set_err(MF_E_ARG, "need ldu >= n_factors, ldq >= n_factors+1");
     const int64_t waves = default_waves(n);
     hipStream_t st = (hipStream_t)stream;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
-        return dispatch_v<T, 0>(ld, [&](auto vc) -> int {
+        return dispatch_v<T>(ldu, [&](auto vc) -> int {
             hipLaunchKernelGGL((predict_kernel<T, decltype(vc)::value>), dim3(grid_for_waves(waves)),
-                               dim3(kBlock), 0, st, n, u, i, (const T *)pu, (const T *)qi,
-                               (const T *)bu, (const T *)bi, (const T *)imp, n_factors, ld, biased,
+                               dim3(kBlock), 0, st, n, u, i, (const T *)pu, (const T *)bu, ldu,
+                               (const T *)qb, ldq, (const T *)imp, n_factors, biased,
                                (T)global_mean, (T *)est, impossible);
             return check_launch("predict_kernel");
         });
@@ -876,20 +772,20 @@ int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, co
     return set_err(MF_E_ARG, "bad dtype");
 }
 
-int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, void *imp, int32_t n_factors,
-                           int32_t ld, int32_t dtype, void *stream)
+int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, int32_t ldu, void *imp,
+                           int32_t n_factors, int32_t dtype, void *stream)
 {
     if (!csr || !csr->row_ptr || !csr->items || !yj || !imp) return set_err(MF_E_ARG, "null argument");
-    if (n_factors < 1 || ld < n_factors) return set_err(MF_E_ARG, "need 1 <= n_factors <= ld");
+    if (n_factors < 1 || ldu < n_factors) return set_err(MF_E_ARG, "need 1 <= n_factors <= ldu");
     if (csr->n_users <= 0) return 0;
     const int64_t waves = default_waves(csr->n_users);
     hipStream_t st = (hipStream_t)stream;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
-        return dispatch_v<T, 0>(ld, [&](auto vc) -> int {
+        return dispatch_v<T>(ldu, [&](auto vc) -> int {
             hipLaunchKernelGGL((user_implicit_kernel<T, decltype(vc)::value>),
                                dim3(grid_for_waves(waves)), dim3(kBlock), 0, st, csr->row_ptr,
-                               csr->items, csr->n_users, (const T *)yj, (T *)imp, n_factors, ld);
+                               csr->items, csr->n_users, (const T *)yj, ldu, (T *)imp, n_factors);
             return check_launch("user_implicit_kernel");
         });
     };

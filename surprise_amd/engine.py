@@ -1,13 +1,15 @@
 """Device-side training engine: owns the HBM layout and drives the C ABI.
 
-HBM layout for one rank (T = float32 or float64, ld = padded row length):
+HBM layout for one rank (T = float32 or float64; rows padded to 64-byte multiples):
   row_ptr int64[U+1], items int32[nnz], ratings T[nnz]     user-major CSR, all_ratings() order
   sched   int32[...] per epoch-chunk                        users heaviest-first (Hogwild) or in
                                                             ur order (deterministic mode)
-  pu T[U, ld], bu T[U]                                      user side, owned by one wave per user
-  qi T[R, I, ld], bi T[R, I], (yj T[R, I, ld])             item side, R = item replicas
-  qi_s, bi_s, (yj_s)                                        chunk-start snapshot (R > 1 or world > 1)
-  delta T[I*ld + I (+ I*ld)]                                packed item delta for the all-reduce
+  pu T[U, ldu], bu T[U]                                     user side, owned by one wave per user
+  qb T[R, I, ldq] = [q_i | b_i | 0..]                       item factors + item bias in one row,
+                                                            R = item replicas
+  yj T[R, I, ldu]                                           SVD++ implicit factors
+  qb_s, (yj_s)                                              chunk-start snapshot (R > 1 or world > 1)
+  delta T[I*ldq (+ I*ldu)]                                  packed item delta for the all-reduce
 
 Every compute step is a HIP kernel behind include/surprise_amd.h; torch only
 allocates device memory and supplies the stream.
@@ -22,13 +24,19 @@ from . import _lib
 from .dist import ItemSync, chunk_users
 
 
-def default_ld(n_factors: int, dtype: int) -> int:
-    """Row length in elements: rows of >= 64 factors are padded to 64-byte multiples so every row
-    starts on a memory-sector boundary; short rows are left unpadded."""
+def _pad64(n: int, dtype: int) -> int:
     per64 = 16 if dtype == _lib.MF_F32 else 8
-    if n_factors < 64:
-        return n_factors
-    return -(-n_factors // per64) * per64
+    return -(-n // per64) * per64
+
+
+def default_ld(n_factors: int, dtype: int) -> int:
+    """User / implicit row length (elements): n_factors padded to a 64-byte multiple."""
+    return _pad64(n_factors, dtype)
+
+
+def default_ldq(n_factors: int, dtype: int) -> int:
+    """Item row length: n_factors + the item bias column, padded to a 64-byte multiple."""
+    return _pad64(n_factors + 1, dtype)
 
 
 class MFEngine(ItemSync):
@@ -50,6 +58,7 @@ class MFEngine(ItemSync):
                              f"for {dtype}, got {n_factors}")
         self.K = int(n_factors)
         self.ld = int(ld) if ld else default_ld(self.K, self.dtype)
+        self.ldq = default_ldq(self.K, self.dtype)
         row_ptr, items, ratings = csr
         self.n_users = len(row_ptr) - 1
         self.n_items = int(n_items)
@@ -82,14 +91,14 @@ class MFEngine(ItemSync):
         self.dup_items = int(_has_duplicate_items(row_ptr, items))
 
         # ---- factor tables
-        U, I, ld, R = self.n_users, self.n_items, self.ld, self.n_replicas
+        U, I, ld, ldq, R = self.n_users, self.n_items, self.ld, self.ldq, self.n_replicas
         z = lambda *shape: torch.zeros(*shape, dtype=self.tdt, device=dev)
         self.pu, self.bu = z(U, ld), z(U)
-        self.qi, self.bi = z(R, I, ld), z(R, I)
+        self.qb = z(R, I, ldq)
         self.yj = z(R, I, ld) if algo == "svdpp" else None
         self.need_snap = R > 1 or self.world > 1
         if self.need_snap:
-            self.qi_s, self.bi_s = z(I, ld), z(I)
+            self.qb_s = z(I, ldq)
             self.yj_s = z(I, ld) if algo == "svdpp" else None
         self._delta = None
         self._hyper = _lib.MfHyper(**(hyper or {}))
@@ -111,14 +120,13 @@ class MFEngine(ItemSync):
         self.bu.copy_(t.from_numpy(np.zeros(self.n_users) if bu is None else
                                    np.asarray(bu, np.float64)).to(self.dev, self.tdt))
         for r in range(self.n_replicas):
-            put(self.qi[r], qi)
-            self.bi[r].copy_(t.from_numpy(np.zeros(self.n_items) if bi is None else
-                                          np.asarray(bi, np.float64)).to(self.dev, self.tdt))
+            put(self.qb[r], qi)
+            self.qb[r][:, K].copy_(t.from_numpy(np.zeros(self.n_items) if bi is None else
+                                                np.asarray(bi, np.float64)).to(self.dev, self.tdt))
             if self.yj is not None:
                 put(self.yj[r], yj)
         if self.need_snap:
-            self.qi_s.copy_(self.qi[0])
-            self.bi_s.copy_(self.bi[0])
+            self.qb_s.copy_(self.qb[0])
             if self.yj is not None:
                 self.yj_s.copy_(self.yj[0])
 
@@ -127,7 +135,8 @@ class MFEngine(ItemSync):
         self.stream.synchronize()
         K = self.K
         h = lambda x: x.to(self.torch.float64).cpu().numpy()
-        out = dict(pu=h(self.pu[:, :K]), qi=h(self.qi[0][:, :K]), bu=h(self.bu), bi=h(self.bi[0]))
+        out = dict(pu=h(self.pu[:, :K]), qi=h(self.qb[0][:, :K]), bu=h(self.bu),
+                   bi=h(self.qb[0][:, K]))
         out["yj"] = h(self.yj[0][:, :K]) if self.yj is not None else None
         return out
 
@@ -138,23 +147,20 @@ class MFEngine(ItemSync):
     def run_chunk(self, c: int):
         s = self.sched[c]
         st = ctypes.c_void_p(self.stream.cuda_stream)
-        rsq = self.n_items * self.ld
         if self.algo == "svd":
             _lib.call("mf_svd_epoch", ctypes.byref(self._csr), self._ptr(s), s.numel(),
-                      self._ptr(self.pu), self._ptr(self.bu), self._ptr(self.qi),
-                      self._ptr(self.bi), self.K, self.ld, int(self.biased),
-                      ctypes.byref(self._hyper), self.mode, self.n_replicas, rsq, self.n_items,
-                      self.n_waves, self.dup_items, self.dtype, st)
+                      self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
+                      self.ldq, self.K, int(self.biased), ctypes.byref(self._hyper), self.mode,
+                      self.n_replicas, self.n_waves, self.dup_items, self.dtype, st)
         else:
             _lib.call("mf_svdpp_epoch", ctypes.byref(self._csr), self._ptr(s), s.numel(),
-                      self._ptr(self.pu), self._ptr(self.bu), self._ptr(self.qi),
-                      self._ptr(self.bi), self._ptr(self.yj), self.K, self.ld,
-                      ctypes.byref(self._hyper), self.mode, self.n_replicas, rsq, self.n_items,
-                      self.n_waves, self.dup_items, self.dtype, st)
+                      self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
+                      self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper),
+                      self.mode, self.n_replicas, self.n_waves, self.dup_items, self.dtype, st)
 
     def _segs(self):
         I, ld = self.n_items, self.ld
-        segs = [(self.qi, self.qi_s, I * ld), (self.bi, self.bi_s, I)]
+        segs = [(self.qb, self.qb_s, I * self.ldq)]
         if self.yj is not None:
             segs.append((self.yj, self.yj_s, I * ld))
         n = len(segs)
@@ -171,7 +177,7 @@ class MFEngine(ItemSync):
 
     def _delta_buffer(self):
         if self._delta is None:
-            n = self.n_items * self.ld + self.n_items
+            n = self.n_items * self.ldq
             if self.yj is not None:
                 n += self.n_items * self.ld
             self._delta = self.torch.zeros(n, dtype=self.tdt, device=self.dev)
@@ -202,7 +208,7 @@ class MFEngine(ItemSync):
         """imp[u] = sum_{j in I_u} yj[j] / sqrt|I_u| on device (SVDpp.estimate :518-520)."""
         imp = self.torch.zeros(self.n_users, self.ld, dtype=self.tdt, device=self.dev)
         _lib.call("mf_svdpp_user_implicit", ctypes.byref(self._csr), self._ptr(self.yj[0]),
-                  self._ptr(imp), self.K, self.ld, self.dtype,
+                  self.ld, self._ptr(imp), self.K, self.dtype,
                   ctypes.c_void_p(self.stream.cuda_stream))
         return imp
 
@@ -215,8 +221,8 @@ class MFEngine(ItemSync):
         est = t.zeros(n, dtype=self.tdt, device=self.dev)
         bad = t.zeros(n, dtype=t.int32, device=self.dev)
         _lib.call("mf_predict", n, self._ptr(du), self._ptr(di), self._ptr(self.pu),
-                  self._ptr(self.qi[0]), self._ptr(self.bu), self._ptr(self.bi[0]),
-                  None if imp is None else self._ptr(imp), self.K, self.ld, int(self.biased),
+                  self._ptr(self.bu), self.ld, self._ptr(self.qb[0]), self.ldq,
+                  None if imp is None else self._ptr(imp), self.K, int(self.biased),
                   float(global_mean), self._ptr(est), self._ptr(bad), self.dtype,
                   ctypes.c_void_p(self.stream.cuda_stream))
         self.stream.synchronize()

@@ -1,0 +1,46 @@
+"""The C-ABI library loads and exports every symbol include/surprise_amd.h declares (no GPU)."""
+import ctypes
+import os
+
+import pytest
+
+from surprise_amd import _lib
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        from surprise_amd import build
+        build.build()
+    return _lib.load()
+
+
+def test_header_declares_expected_entry_points():
+    syms = _lib.header_symbols()
+    assert set(syms) == set(_lib.SIGNATURES), syms
+
+
+def test_library_exports_every_header_symbol(lib):
+    for name in _lib.header_symbols():
+        assert hasattr(lib, name), name
+        assert isinstance(getattr(lib, name), ctypes._CFuncPtr)
+
+
+def test_version_and_error_without_device(lib):
+    assert lib.mf_version() == 200
+    # argument validation happens before any device call
+    rc = lib.mf_replica_merge(0, None, None, None, None, 1, None, 1, 0, None)
+    assert rc == 1001
+    assert b"n_seg" in lib.mf_last_error()
+    csr = _lib.MfCsr(0, 0, 0, 0, 0)
+    rc = lib.mf_svd_epoch(ctypes.byref(csr), None, 1, None, None, 16, None, 16, 10, 1, None,
+                          0, 1, 0, 0, 0, None)
+    assert rc == 1001 and b"null csr" in lib.mf_last_error()
+
+
+def test_header_constants_match_python():
+    text = open(_lib.HEADER_PATH).read()
+    for name, val in (("MF_F32", 0), ("MF_F64", 1), ("MF_MODE_PLAIN", 0), ("MF_MODE_ATOMIC", 1),
+                      ("MF_MODE_REPLICA", 2), ("MF_MODE_COHERENT", 3), ("MF_MAX_FACTORS_F32", 512),
+                      ("MF_MAX_FACTORS_F64", 256)):
+        assert "#define %s" % name in text and str(val) in text.split("#define %s" % name)[1].split("\n")[0]

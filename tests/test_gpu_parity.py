@@ -42,7 +42,7 @@ def test_library_is_the_in_tree_hip_build(torch):
     from surprise_amd import _lib
     lib = _lib.load()
     assert lib._name == _lib.LIB_PATH
-    assert lib.mf_version() >= 100
+    assert lib.mf_version() >= 200
 
 
 @pytest.mark.parametrize("dtype", ["float32", "float64"])

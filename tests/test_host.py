@@ -1,0 +1,234 @@
+"""Host-side mirror of the reference's plugin API and data model (no GPU needed)."""
+import os
+import pickle
+import warnings
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from surprise_amd import (SVD, SVDpp, AlgoBase, Dataset, Prediction, PredictionImpossible,
+                          Reader, Trainset, accuracy, synthetic)
+from surprise_amd.model_selection import (KFold, PredefinedKFold, ShuffleSplit, get_cv,
+                                          train_test_split)
+from surprise_amd.utils import get_rng
+
+
+def test_reader_offset_and_parse():
+    r = Reader(line_format="user item rating", sep=",", rating_scale=(-10, 10))
+    assert r.offset == 11
+    assert r.parse_line("a, b, -3") == ("a", "b", 8.0, None)
+    assert Reader("ml-100k").sep == "\t" and Reader("ml-1m").sep == "::"
+    with pytest.raises(ValueError):
+        Reader("nope")
+    with pytest.raises(ValueError):
+        Reader(line_format="user item stars")
+
+
+def test_get_rng_semantics():
+    assert get_rng(None) is np.random.mtrand._rand
+    a, b = get_rng(3), get_rng(3)
+    assert a.normal() == b.normal()
+    rs = np.random.RandomState(1)
+    assert get_rng(rs) is rs
+    with pytest.raises(ValueError):
+        get_rng("x")
+
+
+def test_trainset_all_ratings_order_and_dicts(u1):
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    trip = list(ts.all_ratings())
+    assert len(trip) == ts.n_ratings
+    us = np.array([t[0] for t in trip])
+    assert np.all(np.diff(us) >= 0)  # user-major, inner-id order
+    np.testing.assert_array_equal([t[1] for t in trip], items)
+    # ur built lazily from the CSR agrees with all_ratings; ir holds every rating once
+    assert sum(len(v) for v in ts.ur.values()) == ts.n_ratings
+    assert sum(len(v) for v in ts.ir.values()) == ts.n_ratings
+    assert ts.knows_user(0) and not ts.knows_user(ts.n_users) and not ts.knows_user("UKN__1")
+    assert ts.knows_item(0) and not ts.knows_item("UKN__x")
+    raw = ts.to_raw_uid(5)
+    assert ts.to_inner_uid(raw) == 5
+    with pytest.raises(ValueError):
+        ts.to_inner_uid("no-such-user")
+    assert len(ts.build_testset()) == ts.n_ratings
+
+
+def test_trainset_ir_raw_order_matches_reference_construct(u1):
+    """ir lists keep raw insertion order (dataset.py:236-237)."""
+    ts, _ = u1
+    rows = [l.split("\t") for l in open(os.path.join(GOLDEN, "u1_ml100k_train"))]
+    first_item = rows[0][1]
+    iid = ts.to_inner_iid(first_item)
+    expected = [(ts.to_inner_uid(r[0]), float(r[2])) for r in rows if r[1] == first_item]
+    assert ts.ir[iid] == expected
+
+
+def test_dict_built_trainset_csr_roundtrip(u1):
+    ts, _ = u1
+    ts2 = Trainset(ts.ur, None, ts.n_users, ts.n_items, ts.n_ratings, ts.rating_scale, ts.offset,
+                   {}, {})
+    for a, b in zip(ts.csr(), ts2.csr()):
+        np.testing.assert_array_equal(a, b)
+    assert ts2.global_mean == ts.global_mean
+
+
+def test_kfold_partitions_and_determinism():
+    u, i, r = synthetic.shape("tiny")
+    data = Dataset.load_from_arrays(u, i, r)
+    folds = list(KFold(4, random_state=2).split(data))
+    assert sum(len(te) for _, te in folds) == len(r)
+    assert all(tr.n_ratings + len(te) == len(r) for tr, te in folds)
+    folds2 = list(KFold(4, random_state=2).split(data))
+    for (a, ta), (b, tb) in zip(folds, folds2):
+        for x, y in zip(a.csr(), b.csr()):
+            np.testing.assert_array_equal(x, y)
+    with pytest.raises(ValueError):
+        next(KFold(1).split(data))
+    assert isinstance(get_cv(None), KFold) and get_cv(3).n_splits == 3
+
+
+def test_shuffle_split_sizes():
+    u, i, r = synthetic.shape("tiny")
+    data = Dataset.load_from_arrays(u, i, r)
+    tr, te = train_test_split(data, test_size=.25, random_state=0)
+    assert len(te) == 300 and tr.n_ratings == 900
+    tr, te = next(ShuffleSplit(1, test_size=100, train_size=500, random_state=0).split(data))
+    assert len(te) == 100 and tr.n_ratings == 500
+
+
+def test_load_from_df_structured_array():
+    import pandas as pd
+    df = pd.DataFrame({"u": [1, 2, 2, 3], "i": [10, 10, 20, 30], "r": [4, 3, 5, 1]})
+    data = Dataset.load_from_df(df, Reader(rating_scale=(1, 5)))
+    ts = data.build_full_trainset()
+    assert (ts.n_users, ts.n_items, ts.n_ratings) == (3, 3, 4)
+    assert ts.to_inner_uid(2) == 1 and ts.global_mean == np.mean([4, 3, 5, 1])
+
+
+def test_load_builtin_never_downloads(monkeypatch, tmp_path):
+    monkeypatch.setenv("SURPRISE_DATA_FOLDER", str(tmp_path))
+    import importlib
+    import surprise_amd.reader as rd
+    importlib.reload(rd)
+    import surprise_amd.dataset as ds
+    importlib.reload(ds)
+    with pytest.raises(ValueError):
+        ds.Dataset.load_builtin("ml-1m")
+    importlib.reload(rd)
+    importlib.reload(ds)
+
+
+def test_accuracy_known_answers():
+    """test_accuracy.py:17-69 of the reference."""
+    preds = [Prediction(0, 0, 0, 0, None), Prediction(1, 1, 1, 1, None)]
+    assert accuracy.rmse(preds, verbose=False) == 0
+    preds = [Prediction(0, 0, 0, 0, None), Prediction(0, 0, 0, 2, None)]
+    assert accuracy.rmse(preds, verbose=False) == np.sqrt((0 + 4) / 2)
+    preds = [Prediction(0, 0, 2, 1, None), Prediction(0, 0, 3, 4, None)]
+    assert accuracy.rmse(preds, verbose=False) == np.sqrt((1 + 1) / 2)
+    preds = [Prediction(0, 0, 0, 0, None), Prediction(1, 1, 1, 1, None)]
+    assert accuracy.mae(preds, verbose=False) == 0
+    preds = [Prediction(0, 0, 0, 0, None), Prediction(0, 0, 0, 2, None)]
+    assert accuracy.mae(preds, verbose=False) == abs(0 - 2) / 2
+    preds = [Prediction(0, 0, 2, 1, None), Prediction(0, 0, 3, 4, None)]
+    assert accuracy.mae(preds, verbose=False) == (abs(2 - 1) + abs(3 - 4)) / 2
+    u0, u1, u2 = 0, 1, 2
+    preds = [Prediction(u0, 0, 1, 1, None), Prediction(u0, 0, 2, 2, None),
+             Prediction(u0, 0, 3, 3, None), Prediction(u1, 0, 1, 3, None),
+             Prediction(u1, 0, 2, 2, None), Prediction(u1, 0, 3, 1, None)]
+    assert accuracy.fcp(preds, verbose=False) == .5
+    preds.append(Prediction(u2, 0, 1, 2, None))
+    with pytest.raises(ValueError):
+        accuracy.fcp(preds[6:], verbose=False)
+    with pytest.raises(ValueError):
+        accuracy.rmse([], verbose=False)
+
+
+def test_constructor_kwargs_and_fallbacks():
+    a = SVD()
+    assert (a.n_factors, a.n_epochs, a.biased, a.init_mean, a.init_std_dev) == (100, 20, True, 0, .1)
+    assert a.lr_bu == a.lr_qi == .005 and a.reg_pu == .02
+    a = SVD(lr_all=.1, reg_all=.3, lr_bi=.2, reg_qi=.4)
+    assert (a.lr_bu, a.lr_bi, a.reg_pu, a.reg_qi) == (.1, .2, .3, .4)
+    p = SVDpp()
+    assert (p.n_factors, p.lr_yj, p.reg_yj) == (20, .007, .02)
+    p = SVDpp(lr_yj=.5, reg_yj=.6)
+    assert (p.lr_yj, p.reg_yj) == (.5, .6)
+    # exactly the reference's parameter names are accepted (test_SVD.py passes them by name)
+    SVD(n_factors=1, n_epochs=1, biased=False, init_mean=0, init_std_dev=.1, lr_all=5, reg_all=5,
+        lr_bu=5, lr_bi=5, lr_pu=5, lr_qi=5, reg_bu=5, reg_bi=5, reg_pu=5, reg_qi=5,
+        random_state=1, verbose=False)
+
+
+def test_unfitted_algo_pickles_without_gpu():
+    a = pickle.loads(pickle.dumps(SVD(n_factors=7)))
+    assert a.n_factors == 7 and a._engine is None
+
+
+def test_estimate_and_predict_semantics_host(golden):
+    """AlgoBase.predict / SVD.estimate on host factors: unknown ids, offset, clip and the
+    PredictionImpossible fallback (algo_base.py:101-176), checked against the reference's
+    values for custom_dataset (factors trained by the oracle, fp64)."""
+    import oracle as orc
+    meta, _ = golden
+    reader = Reader(line_format="user item rating", sep=" ", skip_lines=3, rating_scale=(1, 5))
+    ts = Dataset.load_from_file(os.path.join(GOLDEN, "custom_dataset"), reader).build_full_trainset()
+    for key, rows in meta["unknown"].items():
+        svdpp = key.startswith("SVDpp")
+        biased = key != "SVD_unbiased"
+        algo = (SVDpp if svdpp else SVD)(random_state=0, **({} if svdpp else dict(biased=biased)))
+        AlgoBase.fit(algo, ts)
+        rng = get_rng(0)
+        pu, qi, yj = orc.init_factors(rng, ts.n_users, ts.n_items, algo.n_factors,
+                                      with_yj=svdpp)
+        rp, it, rt = ts.csr()
+        hp = orc.svd_hyper(algo)
+        if svdpp:
+            algo.pu, algo.qi, algo.yj, algo.bu, algo.bi = orc.svdpp_sgd(
+                rp, it, rt, ts.n_items, algo.n_factors, algo.n_epochs, ts.global_mean, hp, pu,
+                qi, yj)
+        else:
+            algo.pu, algo.qi, algo.bu, algo.bi = orc.svd_sgd(
+                rp, it, rt, ts.n_items, algo.n_factors, algo.n_epochs, biased, ts.global_mean,
+                hp, pu, qi)
+        for uid, iid, est, details in rows:
+            p = algo.predict(uid, iid, None)
+            assert abs(p.est - est) < 1e-12, (key, uid, iid)
+            assert p.details == details
+
+
+def test_train_is_deprecated_alias():
+    class Old(AlgoBase):
+        def train(self, trainset):
+            AlgoBase.train(self, trainset)
+    with pytest.warns(UserWarning):
+        Old()
+
+
+def test_predictions_str():
+    s = str(Prediction("u", "i", 3.0, 2.5, {"was_impossible": False}))
+    assert "r_ui = 3.00" in s and "est = 2.50" in s
+    assert issubclass(PredictionImpossible, Exception)
+
+
+def test_synthetic_shapes_are_planted():
+    u, i, r = synthetic.shape("ml-100k")
+    assert len(r) == 100_000 and u.max() == 942 and i.max() <= 1681
+    assert np.bincount(u).min() >= 20
+    key = u.astype(np.int64) * 1682 + i
+    assert len(np.unique(key)) == len(key)
+    assert set(np.unique(r)) <= {1, 2, 3, 4, 5}
+    u2, i2, r2 = synthetic.shape("ml-100k")
+    np.testing.assert_array_equal(r, r2)
+
+
+def test_fit_without_gpu_fails_loudly(u1):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from surprise_amd._lib import SurpriseAMDError
+    ts, _ = u1
+    with pytest.raises(SurpriseAMDError):
+        SVD(n_factors=2, n_epochs=1).fit(ts)

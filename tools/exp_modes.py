@@ -55,8 +55,8 @@ def main():
     for dname, (ts, test), cases in sets:
         for algo, params in cases:
             ref = oracle_rmse(algo, params, ts, test, affine=(algo == "SVDpp"))
-            for mode in ("replica", "atomic", "plain"):
-                for nw in (0, 4096, 1024, 256, 64, 16):
+            for mode in ("replica", "atomic", "plain", "coherent"):
+                for nw in (0, 1024, 256, 64):
                     if nw and nw > ts.n_users:
                         continue
                     klass = SVD if algo == "SVD" else SVDpp
