@@ -236,6 +236,9 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
     const rsrc_t q_rs = make_rsrc(q_base, (uint32_t)n_items * qrow);
     const rsrc_t y_rs = PP ? make_rsrc(y_base, (uint32_t)n_items * yrow) : q_rs;
     constexpr int kStAux = MODE == kCoherent ? kSc1 : 0;
+    // Hogwild schedules read item rows around the CU's L1 (sc1); MF_MODE_PLAIN is the
+    // single-table mode the deterministic one-wave path uses: plain (L1-cached) loads
+    constexpr int kLdAux = MODE == kPlain ? 0 : kSc1;
 
     // per-lane column constants (column c = lane + 64 v)
     uint32_t cq[V], cu[V];
@@ -286,7 +289,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                     const int j = x + a < n ? x + a : n - 1;
                     const uint32_t ro = (uint32_t)it[j] * yrow + (x + a < n ? 0u : kOOB);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kSc1>(y_rs, ro + cu[v]);
+                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kLdAux>(y_rs, ro + cu[v]);
                 }
 #pragma unroll
                 for (int a = 0; a < 8; ++a)
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                 s_off[d] = (uint32_t)readlane(gi_a, d) * qrow + (d < n ? 0u : kOOB);
                 s_r[d] = readlane(gr_a, d);
 #pragma unroll
-                for (int v = 0; v < V; ++v) s_q[d][v] = Buf<T>::template ld<kSc1>(q_rs, s_off[d] + cq[v]);
+                for (int v = 0; v < V; ++v) s_q[d][v] = Buf<T>::template ld<kLdAux>(q_rs, s_off[d] + cq[v]);
                 __builtin_amdgcn_sched_barrier(0);  // keep slot order: slot 0's row lands first
             }
         }
@@ -370,7 +373,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                 s_r[d] = readlane(gr_b, d);
 #pragma unroll
                 for (int v = 0; v < V; ++v)
-                    s_q[d][v] = Buf<T>::template ld<kSc1>(q_rs, s_off[d] + cq[v]);
+                    s_q[d][v] = Buf<T>::template ld<kLdAux>(q_rs, s_off[d] + cq[v]);
                 if (DUPS && off != kOOB) {  // same item again within the window: forward the row
 #pragma unroll
                     for (int dd = 0; dd < kPF; ++dd)
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                     const int j = x + a < n ? x + a : n - 1;
                     ro[a] = (uint32_t)it[j] * yrow + (x + a < n ? 0u : kOOB);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kSc1>(y_rs, ro[a] + cu[v]);
+                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kLdAux>(y_rs, ro[a] + cu[v]);
                 }
 #pragma unroll
                 for (int a = 0; a < 8; ++a)
