@@ -18,7 +18,7 @@
  *     dimension ldu >= n_factors; item rows have ldq >= n_factors + 1 and hold the item bias in
  *     column n_factors: qb[i] = [q_i | b_i | 0 ...].  Padding columns must be zero and stay zero;
  *   - item tables (qb, yj) come in n_replicas consecutive copies (n_items rows each) and must
- *     be < 2 GiB per copy (32-bit buffer offsets);
+ *     be < 715 MB per copy (32-bit buffer offsets, three of which must add below 2^31);
  *   - `dtype` selects the arithmetic type of every floating array: MF_F32 or MF_F64.
  */
 #ifndef SURPRISE_AMD_H

@@ -148,13 +148,15 @@ __device__ __forceinline__ int xcc_id() {
 //
 // Every load/store/atomic of the SGD pipeline goes through a buffer descriptor.  A lane that
 // must not touch memory (a factor column beyond the row, an item row of a masked "tail"
-// rating) gets a byte offset >= kOOB: the hardware range check turns its load into 0 and drops
+// rating) gets a byte offset >= the table's size: the hardware range check turns its load into 0 and drops
 // its store, so the instruction stream has no exec-masked branches and every loop iteration
 // issues the same number of memory instructions -- which lets the compiler keep the row
 // prefetches of the next kPF ratings in flight behind counted vmcnt waits.
 
 using rsrc_t = __amdgpu_buffer_rsrc_t;
-constexpr uint32_t kOOB = 0x80000000u;  // > every table's num_records (tables are < 2 GiB)
+// Offsets stay below 2^31 (the check misbehaves on offsets with bit 31 set, measured): a masked
+// offset is a real offset plus the table size, so tables must be < 2^31 / 3 bytes (kMaxTable).
+constexpr uint64_t kMaxTable = 0x7FFFFFFFull / 3;
 constexpr int kSc1 = 16;                // gfx950 cache policy: sc1 (bypass the CU's L1)
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void *p, uint32_t bytes) {
@@ -233,8 +235,9 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), yrow = (uint32_t)ldu * sizeof(T);
     T *q_base = qb + (int64_t)rep * n_items * ldq;
     T *y_base = PP ? yj + (int64_t)rep * n_items * ldu : nullptr;
-    const rsrc_t q_rs = make_rsrc(q_base, (uint32_t)n_items * qrow);
-    const rsrc_t y_rs = PP ? make_rsrc(y_base, (uint32_t)n_items * yrow) : q_rs;
+    const uint32_t q_oob = (uint32_t)n_items * qrow, y_oob = (uint32_t)n_items * yrow;
+    const rsrc_t q_rs = make_rsrc(q_base, q_oob);
+    const rsrc_t y_rs = PP ? make_rsrc(y_base, y_oob) : q_rs;
     constexpr int kStAux = MODE == kCoherent ? kSc1 : 0;
     // Hogwild schedules read item rows around the CU's L1 (sc1); MF_MODE_PLAIN is the
     // single-table mode the deterministic one-wave path uses: plain (L1-cached) loads
@@ -246,8 +249,8 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const int c = lane + kWave * v;
-        cq[v] = c < ldq ? (uint32_t)c * sizeof(T) : kOOB;
-        cu[v] = c < ldu ? (uint32_t)c * sizeof(T) : kOOB;
+        cq[v] = c < ldq ? (uint32_t)c * sizeof(T) : q_oob;
+        cu[v] = c < ldu ? (uint32_t)c * sizeof(T) : (PP ? y_oob : yrow);  // >= pu record too
         const bool fac = c < K, bias = biased && c == K;
         one[v] = bias ? T(1) : T(0);
         lrq[v] = fac ? hp.lr_qi : (bias ? hp.lr_bi : T(0));
@@ -287,7 +290,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
 #pragma unroll
                 for (int a = 0; a < 8; ++a) {
                     const int j = x + a < n ? x + a : n - 1;
-                    const uint32_t ro = (uint32_t)it[j] * yrow + (x + a < n ? 0u : kOOB);
+                    const uint32_t ro = (uint32_t)it[j] * yrow + (x + a < n ? 0u : y_oob);
 #pragma unroll
                     for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kLdAux>(y_rs, ro + cu[v]);
                 }
@@ -319,11 +322,11 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
             grp_load(0, gi_a, gr_a);
             grp_load(kPF, gi_b, gr_b);
             __builtin_amdgcn_sched_barrier(0);
-            // (an out-of-range rating adds kOOB to a real row offset instead of selecting kOOB,
+            // (an out-of-range rating adds q_oob to a real row offset instead of selecting it,
             // so the item id is used unconditionally and no branch is generated)
 #pragma unroll
             for (int d = 0; d < kPF; ++d) {
-                s_off[d] = (uint32_t)readlane(gi_a, d) * qrow + (d < n ? 0u : kOOB);
+                s_off[d] = (uint32_t)readlane(gi_a, d) * qrow + (d < n ? 0u : q_oob);
                 s_r[d] = readlane(gr_a, d);
 #pragma unroll
                 for (int v = 0; v < V; ++v) s_q[d][v] = Buf<T>::template ld<kLdAux>(q_rs, s_off[d] + cq[v]);
@@ -369,12 +372,12 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                 // keep the next gather below the last use of the slot's old row: hoisting it would
                 // need a second register set and a copy (and a wait) at the loop latch
                 __builtin_amdgcn_sched_barrier(0);
-                s_off[d] = (uint32_t)readlane(gi_b, d) * qrow + (j0 + kPF + d < n ? 0u : kOOB);
+                s_off[d] = (uint32_t)readlane(gi_b, d) * qrow + (j0 + kPF + d < n ? 0u : q_oob);
                 s_r[d] = readlane(gr_b, d);
 #pragma unroll
                 for (int v = 0; v < V; ++v)
                     s_q[d][v] = Buf<T>::template ld<kLdAux>(q_rs, s_off[d] + cq[v]);
-                if (DUPS && off != kOOB) {  // same item again within the window: forward the row
+                if (DUPS && off < q_oob) {  // same item again within the window: forward the row
 #pragma unroll
                     for (int dd = 0; dd < kPF; ++dd)
                         if (s_off[dd] == off)
@@ -387,7 +390,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
         }
 #pragma unroll
         for (int v = 0; v < V; ++v) Buf<T>::template st<0>(p_rs, cu[v], p[v]);
-        Buf<T>::template st<0>(b_rs, lane == 0 ? 0u : kOOB, bu_u);
+        Buf<T>::template st<0>(b_rs, lane == 0 ? 0u : (uint32_t)sizeof(T), bu_u);
 
         // SVD++ (3): y_j <- A y_j + c for every j in I_u
         if (PP) {
@@ -397,7 +400,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
 #pragma unroll
                 for (int a = 0; a < 8; ++a) {
                     const int j = x + a < n ? x + a : n - 1;
-                    ro[a] = (uint32_t)it[j] * yrow + (x + a < n ? 0u : kOOB);
+                    ro[a] = (uint32_t)it[j] * yrow + (x + a < n ? 0u : y_oob);
 #pragma unroll
                     for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kLdAux>(y_rs, ro[a] + cu[v]);
                 }
@@ -611,9 +614,9 @@ int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const v
     if (mode < MF_MODE_PLAIN || mode > MF_MODE_COHERENT) return set_err(MF_E_ARG, "bad mode");
     if (n_rep < 1 || n_rep > 16) return set_err(MF_E_ARG, "n_replicas must be in [1, 16]");
     const size_t esz = dtype == MF_F32 ? 4 : 8;
-    if ((size_t)c->n_items * (size_t)ldq * esz >= (size_t)kOOB)
-        return set_err(MF_E_UNSUPPORTED, "item table >= 2 GiB per replica");
-    if ((size_t)K * esz >= (size_t)kOOB) return set_err(MF_E_UNSUPPORTED, "row too long");
+    if ((uint64_t)c->n_items * (uint64_t)ldq * esz >= kMaxTable ||
+        (uint64_t)c->n_items * (uint64_t)ldu * esz >= kMaxTable)
+        return set_err(MF_E_UNSUPPORTED, "item table >= 715 MB per replica (32-bit buffer offsets)");
     return 0;
 }
 
