@@ -36,8 +36,9 @@ extern "C" {
 /* Item-side update schedule of the Hogwild kernels. */
 #define MF_MODE_PLAIN   0 /* one shared item table, plain load/store (lock-free Hogwild)          */
 #define MF_MODE_ATOMIC  1 /* one shared item table, item deltas applied with float atomics         */
-#define MF_MODE_REPLICA 2 /* n_replicas item tables, replica = XCD id % n_replicas; merged by
-                             mf_replica_merge (sum of deltas) once per epoch-chunk                */
+#define MF_MODE_REPLICA 2 /* n_replicas item tables, one user queue per replica, drained first by
+                             the waves of XCD (replica id); merged by mf_item_merge once per
+                             epoch-chunk                                                          */
 #define MF_MODE_COHERENT 3 /* one shared item table, write-through (sc1) stores                    */
 
 #define MF_E_ARG          1001 /* invalid argument (shape, mode, dtype, n_factors too large)      */
@@ -75,14 +76,17 @@ typedef struct mf_csr {
  *   pu [n_users][ldu], bu [n_users], qb [n_replicas][n_items][ldq]
  *   biased    : 0 reproduces SVD(biased=False) (hp->global_mean must then be 0)
  *   mode      : MF_MODE_*; n_replicas is used by MF_MODE_REPLICA only (else pass 1)
+ *   rep_ptr   : (MF_MODE_REPLICA) device int32[n_replicas+1]: replica r's user queue is
+ *               sched[rep_ptr[r] .. rep_ptr[r+1]); heads: device int32[n_replicas] scratch
+ *               (zeroed by the call).  Other modes: NULL, and the waves stride over sched.
  *   n_waves   : wavefronts to launch (<= 0: library default = fill the GPU);
  *               1 gives the exact sequential reference order when sched = 0..n_users-1.
  *   dup_items : non-zero if some user lists the same item twice (enables in-register forwarding).
  */
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int32_t n_waves,
-                 int32_t dup_items, int32_t dtype, void *stream);
+                 const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, const int32_t *rep_ptr,
+                 int32_t *heads, int32_t n_waves, int32_t dup_items, int32_t dtype, void *stream);
 
 /*
  * One epoch-chunk of SVD++ SGD (SVDpp.sgd epoch body, matrix_factorization.pyx:463-498) in the
@@ -92,26 +96,32 @@ int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
  */
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
-                   const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int32_t n_waves,
-                   int32_t dup_items, int32_t dtype, void *stream);
+                   const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, const int32_t *rep_ptr,
+                   int32_t *heads, int32_t n_waves, int32_t dup_items, int32_t dtype,
+                   void *stream);
 
 /*
- * Item-side merge of an epoch-chunk: for each of the `n_seg` segments
- * (seg_ptr[s] = device pointer to replica 0 of that table, seg_len[s] elements, replicas
- * spaced by seg_stride[s] elements, snapshot at seg_snap[s]) compute
- *     delta = sum_r (rep_r - snap)                 into delta_out (packed, segment after segment)
- * and, if apply != 0, also  snap += delta; rep_r = snap  for every r.
- * With apply == 0 the caller all-reduces delta_out (RCCL SUM) and then calls mf_apply_delta.
- * The descriptor arrays are HOST arrays (<= 8 segments).
+ * Item-side merge of an epoch-chunk for one item table `tab`
+ * ([n_replicas][n_items][ld], snapshot `snap` [n_items][ld]):
+ *     delta[i] = sum_r w_r(i) (tab_r[i] - snap[i])
+ * With counts == NULL, w = 1 (plain SUM).  With counts ([n_replicas][n_items]: ratings of item i
+ * trained in replica r this chunk) and totals ([n_items]: the same summed over every replica of
+ * every rank), w_r(i) = (n_r/N)(1-(1-eta)^N)/(1-(1-eta)^{n_r}) -- SUM while eta N << 1, the
+ * count-weighted MEAN once the steps saturate -- with eta = lr_bi (1 + reg_bi) in column
+ * bias_col (-1: none) and eta = lr_qi (<pu^2> + reg_qi) in columns < n_factors, <pu^2> being the
+ * mean squared factor of pu ([n_users][ldu], reduced into the device scratch `work`, 1 double).
+ * apply != 0: snap += delta and every replica := snap.  apply == 0: only delta_out is written
+ * (the caller all-reduces it with RCCL SUM, then calls mf_item_apply).
  */
-int mf_replica_merge(int32_t n_seg, void *const *seg_ptr, void *const *seg_snap,
-                     const int64_t *seg_len, const int64_t *seg_stride, int32_t n_replicas,
-                     void *delta_out, int32_t apply, int32_t dtype, void *stream);
+int mf_item_merge(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_factors,
+                  int32_t bias_col, int32_t n_replicas, const int32_t *counts,
+                  const int32_t *totals, const mf_hyper_t *hp, const void *pu, int32_t n_users,
+                  int32_t ldu, void *work, void *delta_out, int32_t apply, int32_t dtype,
+                  void *stream);
 
-/* snap += delta; rep_r = snap for every replica (second half of mf_replica_merge). */
-int mf_apply_delta(int32_t n_seg, void *const *seg_ptr, void *const *seg_snap,
-                   const int64_t *seg_len, const int64_t *seg_stride, int32_t n_replicas,
-                   const void *delta, int32_t dtype, void *stream);
+/* snap += delta; every replica := snap (second half of a multi-rank merge). */
+int mf_item_apply(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_replicas,
+                  const void *delta, int32_t dtype, void *stream);
 
 /*
  * Batched SVD.estimate (matrix_factorization.pyx:269-299): for x < n, with u[x] < 0 / i[x] < 0

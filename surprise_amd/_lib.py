@@ -42,13 +42,12 @@ _vp, _i32, _i64, _dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.
 # name -> argtypes (all return int except mf_last_error)
 SIGNATURES = {
     "mf_svd_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32, _i32,
-                     ctypes.POINTER(MfHyper), _i32, _i32, _i32, _i32, _i32, _vp],
+                     ctypes.POINTER(MfHyper), _i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_svdpp_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp, _i32,
-                       ctypes.POINTER(MfHyper), _i32, _i32, _i32, _i32, _i32, _vp],
-    "mf_replica_merge": [_i32, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64),
-                         ctypes.POINTER(_i64), _i32, _vp, _i32, _i32, _vp],
-    "mf_apply_delta": [_i32, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64),
-                       ctypes.POINTER(_i64), _i32, _vp, _i32, _vp],
+                       ctypes.POINTER(MfHyper), _i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp],
+    "mf_item_merge": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, ctypes.POINTER(MfHyper),
+                      _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp],
+    "mf_item_apply": [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp],
     "mf_predict": [_i64, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _dbl, _vp, _vp,
                    _i32, _vp],
     "mf_svdpp_user_implicit": [ctypes.POINTER(MfCsr), _vp, _i32, _vp, _i32, _i32, _vp],

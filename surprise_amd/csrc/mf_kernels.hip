@@ -219,7 +219,8 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, int K, int biased,
-    Hyper<T> hp, int n_rep, int n_items, int64_t n_waves_req)
+    Hyper<T> hp, int n_rep, int n_items, int64_t n_waves_req, const int32_t *__restrict__ rep_ptr,
+    int32_t *heads)
 {
     const int lane = threadIdx.x & (kWave - 1);
     // wave id through readfirstlane: the compiler then knows it (and every user index, CSR
@@ -231,13 +232,8 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
     const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
     if (wave >= n_waves) return;  // whole wave exits (a 1-wave launch still uses a 4-wave block)
 
-    const int rep = MODE == kReplica ? xcc_id() % n_rep : 0;
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), yrow = (uint32_t)ldu * sizeof(T);
-    T *q_base = qb + (int64_t)rep * n_items * ldq;
-    T *y_base = PP ? yj + (int64_t)rep * n_items * ldu : nullptr;
     const uint32_t q_oob = (uint32_t)n_items * qrow, y_oob = (uint32_t)n_items * yrow;
-    const rsrc_t q_rs = make_rsrc(q_base, q_oob);
-    const rsrc_t y_rs = PP ? make_rsrc(y_base, y_oob) : q_rs;
     constexpr int kStAux = MODE == kCoherent ? kSc1 : 0;
     // Hogwild schedules read item rows around the CU's L1 (sc1); MF_MODE_PLAIN is the
     // single-table mode the deterministic one-wave path uses: plain (L1-cached) loads
@@ -262,11 +258,14 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
     const T lr_bu = biased ? hp.lr_bu : T(0);
     const T decay = T(1) - hp.lr_yj * hp.reg_yj;
 
-    for (int64_t w = wave; w < n_sched; w += n_waves) {
-        const int u = sched[w];
+    // one user block: the reference's per-rating order for user u against item tables
+    // (q_base, y_base) -- replica 0 or the replica whose queue the user came from
+    auto do_user = [&](const int u, T *q_base, T *y_base) {
+        const rsrc_t q_rs = make_rsrc(q_base, q_oob);
+        const rsrc_t y_rs = PP ? make_rsrc(y_base, y_oob) : q_rs;
         const int64_t s = row_ptr[u];
         const int n = (int)(row_ptr[u + 1] - s);  // |I_u| (< 2^31)
-        if (n <= 0) continue;
+        if (n <= 0) return;
         // the user's (item, rating) stream, read with scalar loads (uniform addresses ->
         // s_load, counted by lgkmcnt, out of the vector-memory queue the row gathers use)
         const int32_t *__restrict__ it = items + s;
@@ -416,60 +415,113 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                     }
             }
         }
+    };
+
+    if (MODE == kReplica) {
+        // per-XCD user queues: a wave drains the queue of its own XCD's replica first (the
+        // replica then lives in that XCD's L2), then helps with the others; every user is
+        // always trained against the replica of the queue it was assigned to, so the merge's
+        // per-replica item counts stay exact whatever the dispatch placement.
+        const int r0 = xcc_id() % n_rep;
+        for (int qq = 0; qq < n_rep; ++qq) {
+            const int r = r0 + qq < n_rep ? r0 + qq : r0 + qq - n_rep;
+            const int beg = rep_ptr[r], len = rep_ptr[r + 1] - beg;
+            T *q_r = qb + (int64_t)r * n_items * ldq;
+            T *y_r = PP ? yj + (int64_t)r * n_items * ldu : nullptr;
+            for (;;) {
+                int idx = 0;
+                if (lane == 0) idx = atomicAdd(heads + r, 1);
+                idx = __builtin_amdgcn_readfirstlane(idx);
+                if (idx >= len) break;
+                do_user(sched[beg + idx], q_r, y_r);
+            }
+        }
+    } else {
+        for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w], qb, yj);
     }
 }
 
-// ---------------------------------------------------------------- merge / apply (elementwise)
-
-struct SegDesc {
-    void *ptr[8];
-    void *snap[8];
-    int64_t len[8];
-    int64_t stride[8];
-    int64_t off[9];  // packed offsets into delta
-    int n_seg;
-};
+// ---------------------------------------------------------------- item-table merge (epoch-chunk)
+//
+// After an epoch-chunk, replica r of an item table holds snapshot + d_r.  Plain SUM of the d_r
+// is right while every replica made only a few small steps on a row, and overshoots by up to a
+// factor n_replicas once the steps saturate (a popular item's bias converges within one chunk
+// in every replica).  The count-aware merge weights each replica's delta per row by
+//     w_r = (n_r / N) (1 - (1-eta)^N) / (1 - (1-eta)^{n_r}),    N = sum_r n_r  (all ranks),
+// the exact combination for a scalar SGD recursion x <- x + eta (t - x) with n_r steps per
+// replica: -> 1 (SUM) while eta N << 1, -> n_r / N (count-weighted MEAN) when saturated.
+// eta per column: lr_bi (1 + reg_bi) for the bias column, lr_qi (<p^2> + reg_qi) for factor
+// columns (<p^2> = mean squared user factor, measured on the device at merge time).
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void merge_kernel(SegDesc d, int n_rep, T *delta, int apply)
+__global__ __launch_bounds__(kBlock) void sumsq_kernel(const T *__restrict__ x, int64_t n_rows,
+                                                       int K, int ld, double *out)
 {
-    const int64_t total = d.off[d.n_seg];
-    const int64_t step = (int64_t)gridDim.x * kBlock;
-    for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < total; x += step) {
-        int sg = 0;
-        while (sg + 1 < d.n_seg && x >= d.off[sg + 1]) ++sg;
-        const int64_t j = x - d.off[sg];
-        T *base = (T *)d.ptr[sg];
-        T *snap = (T *)d.snap[sg];
-        const T s0 = snap[j];
+    __shared__ double part[kBlock / kWave];
+    double acc = 0;
+    const int64_t total = n_rows * K;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * kBlock) {
+        const double v = (double)x[(e / K) * ld + e % K];
+        acc += v * v;
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & (kWave - 1)) == 0) part[threadIdx.x / kWave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) t += part[w];
+        atomicAdd(out, t);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void item_merge_kernel(
+    T *tab, T *snap, int n_items, int ld, int n_fac, int bias_col, int n_rep,
+    const int32_t *__restrict__ counts, const int32_t *__restrict__ totals, double l1m_bias,
+    double lr_fac, double reg_fac, const double *__restrict__ p2sum, double p2_den,
+    T *__restrict__ delta, int apply)
+{
+    const int64_t total = (int64_t)n_items * ld, stride = total;
+    double l1m_fac = 0;
+    if (counts) l1m_fac = log1p(-lr_fac * (*p2sum / p2_den + reg_fac));
+    for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * kBlock) {
+        const int i = (int)(x / ld), c = (int)(x - (int64_t)i * ld);
+        const double l = !counts ? 0.0 : (c == bias_col ? l1m_bias : (c < n_fac ? l1m_fac : 0.0));
+        const T s0 = snap[x];
         T acc = T(0);
-        for (int r = 0; r < n_rep; ++r) acc += base[r * d.stride[sg] + j] - s0;
+        const double N = counts ? (double)totals[i] : 0.0;
+        const double gN = l != 0.0 ? -expm1(N * l) : 0.0;
+        for (int r = 0; r < n_rep; ++r) {
+            const T d = tab[r * stride + x] - s0;
+            double w = 1.0;
+            if (l != 0.0) {
+                const double n = (double)counts[(int64_t)r * n_items + i];
+                w = n > 0 ? (n / N) * gN / -expm1(n * l) : 0.0;
+            }
+            acc += (T)w * d;
+        }
         if (apply) {
             const T nv = s0 + acc;
-            snap[j] = nv;
-            for (int r = 0; r < n_rep; ++r) base[r * d.stride[sg] + j] = nv;
+            snap[x] = nv;
+            for (int r = 0; r < n_rep; ++r) tab[r * stride + x] = nv;
         }
         if (delta) delta[x] = acc;
     }
 }
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void apply_kernel(SegDesc d, int n_rep, const T *delta)
+__global__ __launch_bounds__(kBlock) void item_apply_kernel(T *tab, T *snap, int64_t total,
+                                                            int n_rep, const T *__restrict__ delta)
 {
-    const int64_t total = d.off[d.n_seg];
-    const int64_t step = (int64_t)gridDim.x * kBlock;
-    for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < total; x += step) {
-        int sg = 0;
-        while (sg + 1 < d.n_seg && x >= d.off[sg + 1]) ++sg;
-        const int64_t j = x - d.off[sg];
-        T *base = (T *)d.ptr[sg];
-        T *snap = (T *)d.snap[sg];
-        const T nv = snap[j] + delta[x];
-        snap[j] = nv;
-        for (int r = 0; r < n_rep; ++r) base[r * d.stride[sg] + j] = nv;
+    for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * kBlock) {
+        const T nv = snap[x] + delta[x];
+        snap[x] = nv;
+        for (int r = 0; r < n_rep; ++r) tab[r * total + x] = nv;
     }
 }
-
 
 // ---------------------------------------------------------------- inference
 
@@ -623,14 +675,20 @@ int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const v
 template <bool PP>
 int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t K, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, int32_t n_rep, int32_t n_waves,
-                 int32_t dups, int32_t dtype, void *stream)
+                 const mf_hyper_t *hp, int32_t mode, int32_t n_rep, const int32_t *rep_ptr,
+                 int32_t *heads, int32_t n_waves, int32_t dups, int32_t dtype, void *stream)
 {
     if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, n_rep, dtype)) return rc;
     if (PP && !yj) return set_err(MF_E_ARG, "null yj");
+    if (mode == MF_MODE_REPLICA && (!rep_ptr || !heads))
+        return set_err(MF_E_ARG, "replica mode needs rep_ptr and heads");
     if (n_sched <= 0) return 0;
     const int64_t waves = n_waves > 0 ? n_waves : default_waves(n_sched);
     hipStream_t st = (hipStream_t)stream;
+    if (mode == MF_MODE_REPLICA) {
+        hipError_t e = hipMemsetAsync(heads, 0, sizeof(int32_t) * n_rep, st);
+        if (e != hipSuccess) return set_err((int)e, "hipMemsetAsync(heads)");
+    }
     auto run = [&](auto tag_t, auto mode_c) -> int {
         using T = decltype(tag_t);
         constexpr int M = decltype(mode_c)::value;
@@ -640,7 +698,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
             hipLaunchKernelGGL(kern, dim3(grid_for_waves(waves)), dim3(kBlock), 0, st,
                                csr->row_ptr, csr->items, (const T *)csr->ratings, sched, n_sched,
                                (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, K, biased,
-                               cast_hyper<T>(hp), n_rep, csr->n_items, waves);
+                               cast_hyper<T>(hp), n_rep, csr->n_items, waves, rep_ptr, heads);
             return check_launch(PP ? "mf_epoch_kernel<svdpp>" : "mf_epoch_kernel<svd>");
         });
     };
@@ -655,28 +713,6 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
     return dtype == MF_F32 ? by_mode(float{}) : by_mode(double{});
 }
 
-int build_segs(SegDesc &d, int n_seg, void *const *ptr, void *const *snap, const int64_t *len,
-               const int64_t *stride)
-{
-    if (n_seg < 1 || n_seg > 8 || !ptr || !snap || !len || !stride)
-        return set_err(MF_E_ARG, "n_seg must be in [1, 8] with non-null descriptors");
-    d.n_seg = n_seg;
-    d.off[0] = 0;
-    for (int s = 0; s < n_seg; ++s) {
-        d.ptr[s] = ptr[s];
-        d.snap[s] = snap[s];
-        d.len[s] = len[s];
-        d.stride[s] = stride[s];
-        d.off[s + 1] = d.off[s] + len[s];
-    }
-    for (int s = n_seg; s < 8; ++s) {
-        d.ptr[s] = d.snap[s] = nullptr;
-        d.len[s] = d.stride[s] = 0;
-        d.off[s + 1] = d.off[s];
-    }
-    return 0;
-}
-
 int elementwise_grid(int64_t total) {
     int64_t b = (total + kBlock - 1) / kBlock;
     if (b > 8192) b = 8192;
@@ -688,67 +724,91 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 200; }
+int mf_version(void) { return 300; }
 
 const char *mf_last_error(void) { return g_err; }
 
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int32_t n_waves,
-                 int32_t dup_items, int32_t dtype, void *stream)
+                 const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, const int32_t *rep_ptr,
+                 int32_t *heads, int32_t n_waves, int32_t dup_items, int32_t dtype, void *stream)
 {
     return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, nullptr, n_factors,
-                               biased, hp, mode, n_replicas, n_waves, dup_items, dtype, stream);
+                               biased, hp, mode, n_replicas, rep_ptr, heads, n_waves, dup_items,
+                               dtype, stream);
 }
 
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
-                   const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, int32_t n_waves,
-                   int32_t dup_items, int32_t dtype, void *stream)
+                   const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, const int32_t *rep_ptr,
+                   int32_t *heads, int32_t n_waves, int32_t dup_items, int32_t dtype,
+                   void *stream)
 {
     return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, n_factors, 1, hp,
-                              mode, n_replicas, n_waves, dup_items, dtype, stream);
+                              mode, n_replicas, rep_ptr, heads, n_waves, dup_items, dtype, stream);
 }
 
-int mf_replica_merge(int32_t n_seg, void *const *seg_ptr, void *const *seg_snap,
-                     const int64_t *seg_len, const int64_t *seg_stride, int32_t n_replicas,
-                     void *delta_out, int32_t apply, int32_t dtype, void *stream)
+int mf_item_merge(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_factors,
+                  int32_t bias_col, int32_t n_replicas, const int32_t *counts,
+                  const int32_t *totals, const mf_hyper_t *hp, const void *pu, int32_t n_users,
+                  int32_t ldu, void *work, void *delta_out, int32_t apply, int32_t dtype,
+                  void *stream)
 {
-    SegDesc d;
-    if (int rc = build_segs(d, n_seg, seg_ptr, seg_snap, seg_len, seg_stride)) return rc;
-    if (n_replicas < 1) return set_err(MF_E_ARG, "n_replicas < 1");
+    if (!tab || !snap || n_items < 0 || ld < 1 || n_replicas < 1)
+        return set_err(MF_E_ARG, "bad item table");
+    if (counts && (!totals || !hp || !pu || !work || n_users < 1 || ldu < n_factors))
+        return set_err(MF_E_ARG, "count-aware merge needs totals, hp, pu, work");
+    if (dtype != MF_F32 && dtype != MF_F64) return set_err(MF_E_ARG, "bad dtype");
     if (!delta_out && !apply) return 0;
-    const int g = elementwise_grid(d.off[n_seg]);
     hipStream_t st = (hipStream_t)stream;
+    const int64_t total = (int64_t)n_items * ld;
+    double l1m_bias = 0, lr_fac = 0, reg_fac = 0, den = 1;
+    if (counts) {
+        l1m_bias = bias_col >= 0 ? log1p(-hp->lr_bi * (1.0 + hp->reg_bi)) : 0.0;
+        lr_fac = hp->lr_qi;
+        reg_fac = hp->reg_qi;
+        den = (double)n_users * n_factors;
+        hipError_t e = hipMemsetAsync(work, 0, sizeof(double), st);
+        if (e != hipSuccess) return set_err((int)e, "hipMemsetAsync(work)");
+        const int g = elementwise_grid((int64_t)n_users * n_factors);
+        if (dtype == MF_F32)
+            hipLaunchKernelGGL(sumsq_kernel<float>, dim3(g), dim3(kBlock), 0, st, (const float *)pu,
+                               (int64_t)n_users, n_factors, ldu, (double *)work);
+        else
+            hipLaunchKernelGGL(sumsq_kernel<double>, dim3(g), dim3(kBlock), 0, st,
+                               (const double *)pu, (int64_t)n_users, n_factors, ldu, (double *)work);
+        if (int rc = check_launch("sumsq_kernel")) return rc;
+    }
+    const int g = elementwise_grid(total);
     if (dtype == MF_F32)
-        hipLaunchKernelGGL(merge_kernel<float>, dim3(g), dim3(kBlock), 0, st, d, n_replicas,
+        hipLaunchKernelGGL(item_merge_kernel<float>, dim3(g), dim3(kBlock), 0, st, (float *)tab,
+                           (float *)snap, n_items, ld, n_factors, bias_col, n_replicas, counts,
+                           totals, l1m_bias, lr_fac, reg_fac, (const double *)work, den,
                            (float *)delta_out, apply);
-    else if (dtype == MF_F64)
-        hipLaunchKernelGGL(merge_kernel<double>, dim3(g), dim3(kBlock), 0, st, d, n_replicas,
-                           (double *)delta_out, apply);
     else
-        return set_err(MF_E_ARG, "bad dtype");
-    return check_launch("merge_kernel");
+        hipLaunchKernelGGL(item_merge_kernel<double>, dim3(g), dim3(kBlock), 0, st, (double *)tab,
+                           (double *)snap, n_items, ld, n_factors, bias_col, n_replicas, counts,
+                           totals, l1m_bias, lr_fac, reg_fac, (const double *)work, den,
+                           (double *)delta_out, apply);
+    return check_launch("item_merge_kernel");
 }
 
-int mf_apply_delta(int32_t n_seg, void *const *seg_ptr, void *const *seg_snap,
-                   const int64_t *seg_len, const int64_t *seg_stride, int32_t n_replicas,
-                   const void *delta, int32_t dtype, void *stream)
+int mf_item_apply(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_replicas,
+                  const void *delta, int32_t dtype, void *stream)
 {
-    SegDesc d;
-    if (int rc = build_segs(d, n_seg, seg_ptr, seg_snap, seg_len, seg_stride)) return rc;
-    if (!delta || n_replicas < 1) return set_err(MF_E_ARG, "null delta / n_replicas < 1");
-    const int g = elementwise_grid(d.off[n_seg]);
+    if (!tab || !snap || !delta || n_replicas < 1) return set_err(MF_E_ARG, "bad argument");
+    const int64_t total = (int64_t)n_items * ld;
+    const int g = elementwise_grid(total);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == MF_F32)
-        hipLaunchKernelGGL(apply_kernel<float>, dim3(g), dim3(kBlock), 0, st, d, n_replicas,
-                           (const float *)delta);
+        hipLaunchKernelGGL(item_apply_kernel<float>, dim3(g), dim3(kBlock), 0, st, (float *)tab,
+                           (float *)snap, total, n_replicas, (const float *)delta);
     else if (dtype == MF_F64)
-        hipLaunchKernelGGL(apply_kernel<double>, dim3(g), dim3(kBlock), 0, st, d, n_replicas,
-                           (const double *)delta);
+        hipLaunchKernelGGL(item_apply_kernel<double>, dim3(g), dim3(kBlock), 0, st, (double *)tab,
+                           (double *)snap, total, n_replicas, (const double *)delta);
     else
         return set_err(MF_E_ARG, "bad dtype");
-    return check_launch("apply_kernel");
+    return check_launch("item_apply_kernel");
 }
 
 int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, const void *bu,

@@ -21,7 +21,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from .dist import ItemSync, chunk_users
+from .dist import ItemSync, chunk_users, item_counts, replica_queues
 
 
 def _pad64(n: int, dtype: int) -> int:
@@ -45,7 +45,7 @@ class MFEngine(ItemSync):
     def __init__(self, csr, n_items, n_factors, *, algo="svd", hyper=None, biased=True,
                  dtype="float32", mode="replica", n_replicas=8, n_chunks=1, users=None,
                  deterministic=False, user_order=None, n_waves=0, device=None, ld=None,
-                 world=1):
+                 world=1, merge="count"):
         torch = _lib.require_gpu()
         self.torch = torch
         self.algo = algo
@@ -87,7 +87,23 @@ class MFEngine(ItemSync):
             chunks = [order]
         else:
             chunks = chunk_users(self.users, row_ptr, self.n_chunks)
-        self.sched = [torch.from_numpy(np.ascontiguousarray(c, np.int32)).to(dev) for c in chunks]
+        # per chunk: the user schedule (replica mode: R queues back to back, rep_ptr[R+1]) and
+        # counts[R, I] = ratings of item i trained in replica r (the count-aware merge's n_r)
+        R = self.n_replicas
+        self.sched, self.rep_ptr, self.counts, self._totals_local = [], [], [], []
+        for c in chunks:
+            qs = replica_queues(c, row_ptr, R)
+            self.sched.append(torch.from_numpy(np.ascontiguousarray(np.concatenate(qs), np.int32)).to(dev))
+            ptr = np.zeros(R + 1, np.int32)
+            np.cumsum([len(q) for q in qs], out=ptr[1:])
+            self.rep_ptr.append(torch.from_numpy(ptr).to(dev))
+            cnt = np.stack([item_counts(q, row_ptr, items, self.n_items) for q in qs])
+            self.counts.append(torch.from_numpy(cnt.astype(np.int32)).to(dev))
+            self._totals_local.append(cnt.sum(0).astype(np.int32))
+        self.totals = None  # set by _prepare(): summed over every rank
+        self.heads = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.work = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.merge_rule = merge
         self.dup_items = int(_has_duplicate_items(row_ptr, items))
 
         # ---- factor tables
@@ -147,33 +163,56 @@ class MFEngine(ItemSync):
     def run_chunk(self, c: int):
         s = self.sched[c]
         st = ctypes.c_void_p(self.stream.cuda_stream)
+        rp = self._ptr(self.rep_ptr[c]) if self.mode == _lib.MF_MODE_REPLICA else None
+        hd = self._ptr(self.heads) if self.mode == _lib.MF_MODE_REPLICA else None
         if self.algo == "svd":
             _lib.call("mf_svd_epoch", ctypes.byref(self._csr), self._ptr(s), s.numel(),
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
                       self.ldq, self.K, int(self.biased), ctypes.byref(self._hyper), self.mode,
-                      self.n_replicas, self.n_waves, self.dup_items, self.dtype, st)
+                      self.n_replicas, rp, hd, self.n_waves, self.dup_items, self.dtype, st)
         else:
             _lib.call("mf_svdpp_epoch", ctypes.byref(self._csr), self._ptr(s), s.numel(),
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
                       self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper),
-                      self.mode, self.n_replicas, self.n_waves, self.dup_items, self.dtype, st)
+                      self.mode, self.n_replicas, rp, hd, self.n_waves, self.dup_items,
+                      self.dtype, st)
+        self._chunk = c
 
-    def _segs(self):
-        I, ld = self.n_items, self.ld
-        segs = [(self.qb, self.qb_s, I * self.ldq)]
+    def _prepare(self, ctx):
+        """Global per-item rating counts of every chunk (all ranks) for the count-aware merge."""
+        self.totals = []
+        for t in self._totals_local:
+            tt = self.torch.from_numpy(t).to(self.dev)
+            if ctx is not None and ctx.world > 1:
+                ctx.all_reduce_sum(tt)
+            self.totals.append(tt)
+
+    def _merge(self, delta_out, apply):
+        st = ctypes.c_void_p(self.stream.cuda_stream)
+        c = getattr(self, "_chunk", 0)
+        count_aware = self.merge_rule == "count"
+        if count_aware and self.totals is None:
+            self._prepare(None)
+        I = self.n_items
+        tabs = [(self.qb, self.qb_s, self.ldq, self.K)]
         if self.yj is not None:
-            segs.append((self.yj, self.yj_s, I * ld))
-        n = len(segs)
-        ptr = (ctypes.c_void_p * n)(*[s[0].data_ptr() for s in segs])
-        snap = (ctypes.c_void_p * n)(*[s[1].data_ptr() for s in segs])
-        ln = (ctypes.c_int64 * n)(*[s[2] for s in segs])
-        stride = (ctypes.c_int64 * n)(*[s[2] for s in segs])
-        return n, ptr, snap, ln, stride
+            tabs.append((self.yj, self.yj_s, self.ld, -1))
+        off = 0
+        for tab, snap, ld, bias_col in tabs:
+            # the implicit table yj is merged by plain SUM (its per-user steps stay small)
+            use_counts = count_aware and bias_col >= 0
+            dptr = None
+            if delta_out is not None:
+                dptr = ctypes.c_void_p(delta_out.data_ptr() + off * delta_out.element_size())
+            _lib.call("mf_item_merge", self._ptr(tab), self._ptr(snap), I, ld, self.K, bias_col,
+                      self.n_replicas, self._ptr(self.counts[c]) if use_counts else None,
+                      self._ptr(self.totals[c]) if use_counts else None,
+                      ctypes.byref(self._hyper), self._ptr(self.pu), self.n_users, self.ld,
+                      self._ptr(self.work), dptr, int(apply), self.dtype, st)
+            off += I * ld
 
     def _merge_local(self):
-        n, ptr, snap, ln, stride = self._segs()
-        _lib.call("mf_replica_merge", n, ptr, snap, ln, stride, self.n_replicas, None, 1,
-                  self.dtype, ctypes.c_void_p(self.stream.cuda_stream))
+        self._merge(None, True)
 
     def _delta_buffer(self):
         if self._delta is None:
@@ -184,14 +223,19 @@ class MFEngine(ItemSync):
         return self._delta
 
     def _delta_into(self, buf):
-        n, ptr, snap, ln, stride = self._segs()
-        _lib.call("mf_replica_merge", n, ptr, snap, ln, stride, self.n_replicas,
-                  self._ptr(buf), 0, self.dtype, ctypes.c_void_p(self.stream.cuda_stream))
+        self._merge(buf, False)
 
     def _apply(self, buf):
-        n, ptr, snap, ln, stride = self._segs()
-        _lib.call("mf_apply_delta", n, ptr, snap, ln, stride, self.n_replicas, self._ptr(buf),
-                  self.dtype, ctypes.c_void_p(self.stream.cuda_stream))
+        st = ctypes.c_void_p(self.stream.cuda_stream)
+        I = self.n_items
+        tabs = [(self.qb, self.qb_s, self.ldq)]
+        if self.yj is not None:
+            tabs.append((self.yj, self.yj_s, self.ld))
+        off = 0
+        for tab, snap, ld in tabs:
+            _lib.call("mf_item_apply", self._ptr(tab), self._ptr(snap), I, ld, self.n_replicas,
+                      ctypes.c_void_p(buf.data_ptr() + off * buf.element_size()), self.dtype, st)
+            off += I * ld
 
     def _gather_users(self, ctx):
         """After the last epoch: every rank keeps only its own users' rows, then a SUM

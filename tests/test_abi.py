@@ -27,14 +27,15 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_without_device(lib):
-    assert lib.mf_version() == 200
+    assert lib.mf_version() == 300
     # argument validation happens before any device call
-    rc = lib.mf_replica_merge(0, None, None, None, None, 1, None, 1, 0, None)
+    rc = lib.mf_item_merge(None, None, 10, 16, 10, 10, 1, None, None, None, None, 0, 16, None,
+                           None, 1, 0, None)
     assert rc == 1001
-    assert b"n_seg" in lib.mf_last_error()
+    assert b"bad item table" in lib.mf_last_error()
     csr = _lib.MfCsr(0, 0, 0, 0, 0)
     rc = lib.mf_svd_epoch(ctypes.byref(csr), None, 1, None, None, 16, None, 16, 10, 1, None,
-                          0, 1, 0, 0, 0, None)
+                          0, 1, None, None, 0, 0, 0, None)
     assert rc == 1001 and b"null csr" in lib.mf_last_error()
 
 

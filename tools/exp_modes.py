@@ -55,19 +55,20 @@ def main():
     for dname, (ts, test), cases in sets:
         for algo, params in cases:
             ref = oracle_rmse(algo, params, ts, test, affine=(algo == "SVDpp"))
-            for mode in ("replica", "atomic", "plain", "coherent"):
-                for nw in (0, 1024, 256, 64):
+            for mode, nw, ch in (("replica", 0, 1), ("replica", 0, 4), ("replica", 256, 1),
+                                 ("atomic", 0, 1), ("atomic", 256, 1), ("coherent", 0, 1),
+                                 ("plain", 0, 1)):
                     if nw and nw > ts.n_users:
                         continue
                     klass = SVD if algo == "SVD" else SVDpp
-                    m = klass(**params, mode=mode, n_waves=nw)
+                    m = klass(**params, mode=mode, n_waves=nw, chunks_per_epoch=ch)
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
                     m.fit(ts)
                     torch.cuda.synchronize()
                     dt = time.perf_counter() - t0
                     got = accuracy.rmse(m.test(test), verbose=False)
-                    rec = dict(data=dname, algo=algo, params=params, mode=mode, n_waves=nw,
+                    rec = dict(data=dname, algo=algo, params=params, mode=mode, n_waves=nw, chunks=ch,
                                rmse=got, ref=ref, delta=got - ref, fit_s=dt)
                     rows.append(rec)
                     print(json.dumps(rec), flush=True)
