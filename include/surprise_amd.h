@@ -40,6 +40,7 @@ extern "C" {
                              the waves of XCD (replica id); merged by mf_item_merge once per
                              epoch-chunk                                                          */
 #define MF_MODE_COHERENT 3 /* one shared item table, write-through (sc1) stores                    */
+#define MF_MODE_REPLICA_ATOMIC 4 /* MF_MODE_REPLICA with item updates applied as float atomics    */
 
 #define MF_E_ARG          1001 /* invalid argument (shape, mode, dtype, n_factors too large)      */
 #define MF_E_UNSUPPORTED  1002 /* combination not compiled                                       */
@@ -100,21 +101,29 @@ int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, v
                    int32_t *heads, int32_t n_waves, int32_t dup_items, int32_t dtype,
                    void *stream);
 
+/* Merge rules of mf_item_merge. */
+#define MF_MERGE_SUM   0 /* delta = sum_r d_r                                                      */
+#define MF_MERGE_COUNT 1 /* count-aware: SUM while a row's steps are small, count-weighted MEAN
+                            once they saturate (item factors and biases)                           */
+#define MF_MERGE_MEAN  2 /* count-weighted MEAN: sum_r (n_r / N) d_r (SVD++ implicit factors)      */
+
 /*
  * Item-side merge of an epoch-chunk for one item table `tab`
  * ([n_replicas][n_items][ld], snapshot `snap` [n_items][ld]):
  *     delta[i] = sum_r w_r(i) (tab_r[i] - snap[i])
- * With counts == NULL, w = 1 (plain SUM).  With counts ([n_replicas][n_items]: ratings of item i
- * trained in replica r this chunk) and totals ([n_items]: the same summed over every replica of
- * every rank), w_r(i) = (n_r/N)(1-(1-eta)^N)/(1-(1-eta)^{n_r}) -- SUM while eta N << 1, the
- * count-weighted MEAN once the steps saturate -- with eta = lr_bi (1 + reg_bi) in column
- * bias_col (-1: none) and eta = lr_qi (<pu^2> + reg_qi) in columns < n_factors, <pu^2> being the
- * mean squared factor of pu ([n_users][ldu], reduced into the device scratch `work`, 1 double).
+ * counts ([n_replicas][n_items]: ratings of item i trained in replica r this chunk) and totals
+ * ([n_items]: the same summed over every replica of every rank) give n_r and N.
+ *   MF_MERGE_SUM:   w = 1 (counts may be NULL);
+ *   MF_MERGE_COUNT: w_r(i) = (n_r/N)(1-(1-eta)^N)/(1-(1-eta)^{n_r}) with eta = lr_bi (1 + reg_bi)
+ *                   in column bias_col (-1: none) and eta = lr_qi (<pu^2> + reg_qi) in columns
+ *                   < n_factors, <pu^2> being the mean squared entry of pu[:, :n_factors]
+ *                   ([n_users][ldu], reduced on the device into `work`, 1 double of scratch);
+ *   MF_MERGE_MEAN:  w_r(i) = n_r / N.
  * apply != 0: snap += delta and every replica := snap.  apply == 0: only delta_out is written
  * (the caller all-reduces it with RCCL SUM, then calls mf_item_apply).
  */
 int mf_item_merge(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_factors,
-                  int32_t bias_col, int32_t n_replicas, const int32_t *counts,
+                  int32_t bias_col, int32_t n_replicas, int32_t rule, const int32_t *counts,
                   const int32_t *totals, const mf_hyper_t *hp, const void *pu, int32_t n_users,
                   int32_t ldu, void *work, void *delta_out, int32_t apply, int32_t dtype,
                   void *stream);
@@ -140,6 +149,9 @@ int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, co
  * yj is replica 0, imp is [n_users][ldu]. */
 int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, int32_t ldu, void *imp,
                            int32_t n_factors, int32_t dtype, void *stream);
+
+/* Self-test of the XCD id register: out[b] = HW_REG_XCC_ID of workgroup b, b < n_blocks. */
+int mf_selftest_xcc(int32_t *out, int32_t n_blocks, void *stream);
 
 /* Self-test of the wavefront reduction: out[w] = sum of in[64w .. 64w+63], w < n_waves. */
 int mf_selftest_wave_sum(const void *in, void *out, int32_t n_waves, int32_t dtype, void *stream);

@@ -16,8 +16,11 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "surprise_amd.h")
 
 MF_F32, MF_F64 = 0, 1
 MF_MODE_PLAIN, MF_MODE_ATOMIC, MF_MODE_REPLICA, MF_MODE_COHERENT = 0, 1, 2, 3
+MF_MODE_REPLICA_ATOMIC = 4
 MODES = {"plain": MF_MODE_PLAIN, "atomic": MF_MODE_ATOMIC, "replica": MF_MODE_REPLICA,
-         "coherent": MF_MODE_COHERENT}
+         "coherent": MF_MODE_COHERENT, "replica_atomic": MF_MODE_REPLICA_ATOMIC}
+REPLICA_MODES = (MF_MODE_REPLICA, MF_MODE_REPLICA_ATOMIC)
+MF_MERGE_SUM, MF_MERGE_COUNT, MF_MERGE_MEAN = 0, 1, 2
 MAX_FACTORS = {MF_F32: 512, MF_F64: 256}
 
 
@@ -45,13 +48,14 @@ SIGNATURES = {
                      ctypes.POINTER(MfHyper), _i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_svdpp_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp, _i32,
                        ctypes.POINTER(MfHyper), _i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp],
-    "mf_item_merge": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, ctypes.POINTER(MfHyper),
-                      _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp],
+    "mf_item_merge": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
+                      ctypes.POINTER(MfHyper), _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp],
     "mf_item_apply": [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp],
     "mf_predict": [_i64, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _dbl, _vp, _vp,
                    _i32, _vp],
     "mf_svdpp_user_implicit": [ctypes.POINTER(MfCsr), _vp, _i32, _vp, _i32, _i32, _vp],
     "mf_selftest_wave_sum": [_vp, _vp, _i32, _i32, _vp],
+    "mf_selftest_xcc": [_vp, _i32, _vp],
     "mf_version": [],
     "mf_last_error": [],
 }

@@ -208,7 +208,7 @@ struct Buf<double> {
 // ---------------------------------------------------------------- SGD epoch kernel (SVD, SVD++)
 
 enum { kPlain = MF_MODE_PLAIN, kAtomic = MF_MODE_ATOMIC, kReplica = MF_MODE_REPLICA,
-       kCoherent = MF_MODE_COHERENT };
+       kCoherent = MF_MODE_COHERENT, kReplicaAtomic = MF_MODE_REPLICA_ATOMIC };
 
 // Item table row (ldq elements): [q_0 .. q_{K-1} | b_i | 0 ...].  The user row is extended in
 // registers with a constant 1 in column K, so <q_aug, p_aug> = <q_i, p_u> + b_i and the item
@@ -234,6 +234,8 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
 
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), yrow = (uint32_t)ldu * sizeof(T);
     const uint32_t q_oob = (uint32_t)n_items * qrow, y_oob = (uint32_t)n_items * yrow;
+    constexpr bool REP = MODE == kReplica || MODE == kReplicaAtomic;  // per-XCD replica queues
+    constexpr bool ATOM = MODE == kAtomic || MODE == kReplicaAtomic;  // item updates as atomics
     constexpr int kStAux = MODE == kCoherent ? kSc1 : 0;
     // Hogwild schedules read item rows around the CU's L1 (sc1); MF_MODE_PLAIN is the
     // single-table mode the deterministic one-wave path uses: plain (L1-cached) loads
@@ -363,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                 const uint32_t off = s_off[d];
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
-                    if (MODE == kAtomic)
+                    if (ATOM)
                         Buf<T>::add(q_rs, q_base, (uint32_t)n_items * qrow, off + cq[v], qn[v] - s_q[d][v]);
                     else
                         Buf<T>::template st<kStAux>(q_rs, off + cq[v], qn[v]);
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                 for (int a = 0; a < 8; ++a)
 #pragma unroll
                     for (int v = 0; v < V; ++v) {
-                        if (MODE == kAtomic)
+                        if (ATOM)
                             Buf<T>::add(y_rs, y_base, (uint32_t)n_items * yrow, ro[a] + cu[v],
                                         (A - T(1)) * g[a][v] + cacc[v]);
                         else
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
         }
     };
 
-    if (MODE == kReplica) {
+    if (REP) {
         // per-XCD user queues: a wave drains the queue of its own XCD's replica first (the
         // replica then lives in that XCD's L2), then helps with the others; every user is
         // always trained against the replica of the queue it was assigned to, so the merge's
@@ -478,17 +480,20 @@ __global__ __launch_bounds__(kBlock) void sumsq_kernel(const T *__restrict__ x, 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void item_merge_kernel(
     T *tab, T *snap, int n_items, int ld, int n_fac, int bias_col, int n_rep,
-    const int32_t *__restrict__ counts, const int32_t *__restrict__ totals, double l1m_bias,
-    double lr_fac, double reg_fac, const double *__restrict__ p2sum, double p2_den,
-    T *__restrict__ delta, int apply)
+    const int32_t *__restrict__ counts, const int32_t *__restrict__ totals, int mean,
+    double l1m_bias, double lr_fac, double reg_fac, const double *__restrict__ p2sum,
+    double p2_den, T *__restrict__ delta, int apply)
 {
     const int64_t total = (int64_t)n_items * ld, stride = total;
     double l1m_fac = 0;
-    if (counts) l1m_fac = log1p(-lr_fac * (*p2sum / p2_den + reg_fac));
+    if (counts && !mean) l1m_fac = log1p(-lr_fac * (*p2sum / p2_den + reg_fac));
     for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * kBlock) {
         const int i = (int)(x / ld), c = (int)(x - (int64_t)i * ld);
-        const double l = !counts ? 0.0 : (c == bias_col ? l1m_bias : (c < n_fac ? l1m_fac : 0.0));
+        // l = log(1 - eta); -inf selects the count-weighted mean (rule MF_MERGE_MEAN)
+        const double l = !counts ? 0.0
+                         : (mean ? -INFINITY
+                                 : (c == bias_col ? l1m_bias : (c < n_fac ? l1m_fac : 0.0)));
         const T s0 = snap[x];
         T acc = T(0);
         const double N = counts ? (double)totals[i] : 0.0;
@@ -498,7 +503,7 @@ __global__ __launch_bounds__(kBlock) void item_merge_kernel(
             double w = 1.0;
             if (l != 0.0) {
                 const double n = (double)counts[(int64_t)r * n_items + i];
-                w = n > 0 ? (n / N) * gN / -expm1(n * l) : 0.0;
+                w = n > 0 ? (mean ? n / N : (n / N) * gN / -expm1(n * l)) : 0.0;
             }
             acc += (T)w * d;
         }
@@ -599,6 +604,11 @@ __global__ __launch_bounds__(kBlock) void user_implicit_kernel(
     }
 }
 
+__global__ void xcc_selftest_kernel(int32_t *out, int n_blocks)
+{
+    if (threadIdx.x == 0 && (int)blockIdx.x < n_blocks) out[blockIdx.x] = xcc_id();
+}
+
 template <typename T>
 __global__ void wave_sum_selftest_kernel(const T *in, T *out, int n_waves)
 {
@@ -663,7 +673,7 @@ int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const v
     const int maxk = dtype == MF_F32 ? MF_MAX_FACTORS_F32 : MF_MAX_FACTORS_F64;
     if (K < 1 || K > maxk) return set_err(MF_E_ARG, "n_factors out of range");
     if (ldu < K || ldq < K + 1) return set_err(MF_E_ARG, "need ldu >= n_factors, ldq >= n_factors+1");
-    if (mode < MF_MODE_PLAIN || mode > MF_MODE_COHERENT) return set_err(MF_E_ARG, "bad mode");
+    if (mode < MF_MODE_PLAIN || mode > MF_MODE_REPLICA_ATOMIC) return set_err(MF_E_ARG, "bad mode");
     if (n_rep < 1 || n_rep > 16) return set_err(MF_E_ARG, "n_replicas must be in [1, 16]");
     const size_t esz = dtype == MF_F32 ? 4 : 8;
     if ((uint64_t)c->n_items * (uint64_t)ldq * esz >= kMaxTable ||
@@ -680,12 +690,13 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
 {
     if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, n_rep, dtype)) return rc;
     if (PP && !yj) return set_err(MF_E_ARG, "null yj");
-    if (mode == MF_MODE_REPLICA && (!rep_ptr || !heads))
-        return set_err(MF_E_ARG, "replica mode needs rep_ptr and heads");
+    const bool rep_mode = mode == MF_MODE_REPLICA || mode == MF_MODE_REPLICA_ATOMIC;
+    if (rep_mode && (!rep_ptr || !heads))
+        return set_err(MF_E_ARG, "replica modes need rep_ptr and heads");
     if (n_sched <= 0) return 0;
     const int64_t waves = n_waves > 0 ? n_waves : default_waves(n_sched);
     hipStream_t st = (hipStream_t)stream;
-    if (mode == MF_MODE_REPLICA) {
+    if (rep_mode) {
         hipError_t e = hipMemsetAsync(heads, 0, sizeof(int32_t) * n_rep, st);
         if (e != hipSuccess) return set_err((int)e, "hipMemsetAsync(heads)");
     }
@@ -707,6 +718,8 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
             case MF_MODE_PLAIN: return run(tag_t, std::integral_constant<int, kPlain>{});
             case MF_MODE_ATOMIC: return run(tag_t, std::integral_constant<int, kAtomic>{});
             case MF_MODE_REPLICA: return run(tag_t, std::integral_constant<int, kReplica>{});
+            case MF_MODE_REPLICA_ATOMIC:
+                return run(tag_t, std::integral_constant<int, kReplicaAtomic>{});
             default: return run(tag_t, std::integral_constant<int, kCoherent>{});
         }
     };
@@ -749,21 +762,26 @@ int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, v
 }
 
 int mf_item_merge(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_factors,
-                  int32_t bias_col, int32_t n_replicas, const int32_t *counts,
+                  int32_t bias_col, int32_t n_replicas, int32_t rule, const int32_t *counts,
                   const int32_t *totals, const mf_hyper_t *hp, const void *pu, int32_t n_users,
                   int32_t ldu, void *work, void *delta_out, int32_t apply, int32_t dtype,
                   void *stream)
 {
     if (!tab || !snap || n_items < 0 || ld < 1 || n_replicas < 1)
         return set_err(MF_E_ARG, "bad item table");
-    if (counts && (!totals || !hp || !pu || !work || n_users < 1 || ldu < n_factors))
-        return set_err(MF_E_ARG, "count-aware merge needs totals, hp, pu, work");
+    if (rule < MF_MERGE_SUM || rule > MF_MERGE_MEAN) return set_err(MF_E_ARG, "bad merge rule");
+    if (rule == MF_MERGE_SUM) counts = nullptr;
+    const int mean = rule == MF_MERGE_MEAN;
+    if (counts && !totals) return set_err(MF_E_ARG, "counted merge needs totals");
+    if (counts && !mean && (!hp || !pu || !work || n_users < 1 || ldu < n_factors))
+        return set_err(MF_E_ARG, "count-aware merge needs hp, pu, work");
+    if (rule != MF_MERGE_SUM && !counts) return set_err(MF_E_ARG, "counted merge needs counts");
     if (dtype != MF_F32 && dtype != MF_F64) return set_err(MF_E_ARG, "bad dtype");
     if (!delta_out && !apply) return 0;
     hipStream_t st = (hipStream_t)stream;
     const int64_t total = (int64_t)n_items * ld;
     double l1m_bias = 0, lr_fac = 0, reg_fac = 0, den = 1;
-    if (counts) {
+    if (counts && !mean) {
         l1m_bias = bias_col >= 0 ? log1p(-hp->lr_bi * (1.0 + hp->reg_bi)) : 0.0;
         lr_fac = hp->lr_qi;
         reg_fac = hp->reg_qi;
@@ -783,12 +801,12 @@ int mf_item_merge(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
     if (dtype == MF_F32)
         hipLaunchKernelGGL(item_merge_kernel<float>, dim3(g), dim3(kBlock), 0, st, (float *)tab,
                            (float *)snap, n_items, ld, n_factors, bias_col, n_replicas, counts,
-                           totals, l1m_bias, lr_fac, reg_fac, (const double *)work, den,
+                           totals, mean, l1m_bias, lr_fac, reg_fac, (const double *)work, den,
                            (float *)delta_out, apply);
     else
         hipLaunchKernelGGL(item_merge_kernel<double>, dim3(g), dim3(kBlock), 0, st, (double *)tab,
                            (double *)snap, n_items, ld, n_factors, bias_col, n_replicas, counts,
-                           totals, l1m_bias, lr_fac, reg_fac, (const double *)work, den,
+                           totals, mean, l1m_bias, lr_fac, reg_fac, (const double *)work, den,
                            (double *)delta_out, apply);
     return check_launch("item_merge_kernel");
 }
@@ -858,6 +876,14 @@ int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, int32_t ldu, voi
     if (dtype == MF_F32) return run(float{});
     if (dtype == MF_F64) return run(double{});
     return set_err(MF_E_ARG, "bad dtype");
+}
+
+int mf_selftest_xcc(int32_t *out, int32_t n_blocks, void *stream)
+{
+    if (!out || n_blocks < 1) return set_err(MF_E_ARG, "bad argument");
+    hipLaunchKernelGGL(xcc_selftest_kernel, dim3(n_blocks), dim3(kWave), 0, (hipStream_t)stream, out,
+                       n_blocks);
+    return check_launch("xcc_selftest_kernel");
 }
 
 int mf_selftest_wave_sum(const void *in, void *out, int32_t n_waves, int32_t dtype, void *stream)

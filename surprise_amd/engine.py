@@ -67,7 +67,7 @@ class MFEngine(ItemSync):
         if self.deterministic:
             mode, n_replicas, n_chunks, n_waves = "plain", 1, 1, 1
         self.mode = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
-        self.n_replicas = int(n_replicas) if self.mode == _lib.MF_MODE_REPLICA else 1
+        self.n_replicas = int(n_replicas) if self.mode in _lib.REPLICA_MODES else 1
         self.n_chunks = max(1, int(n_chunks))
         self.n_waves = int(n_waves)
         self.world = int(world)
@@ -163,8 +163,9 @@ class MFEngine(ItemSync):
     def run_chunk(self, c: int):
         s = self.sched[c]
         st = ctypes.c_void_p(self.stream.cuda_stream)
-        rp = self._ptr(self.rep_ptr[c]) if self.mode == _lib.MF_MODE_REPLICA else None
-        hd = self._ptr(self.heads) if self.mode == _lib.MF_MODE_REPLICA else None
+        rep = self.mode in _lib.REPLICA_MODES
+        rp = self._ptr(self.rep_ptr[c]) if rep else None
+        hd = self._ptr(self.heads) if rep else None
         if self.algo == "svd":
             _lib.call("mf_svd_epoch", ctypes.byref(self._csr), self._ptr(s), s.numel(),
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
@@ -199,13 +200,16 @@ class MFEngine(ItemSync):
             tabs.append((self.yj, self.yj_s, self.ld, -1))
         off = 0
         for tab, snap, ld, bias_col in tabs:
-            # the implicit table yj is merged by plain SUM (its per-user steps stay small)
-            use_counts = count_aware and bias_col >= 0
+            # item factors / biases: count-aware; SVD++ implicit factors: count-weighted mean
+            # (every user of a group moves all its y_j together, which saturates fast)
+            rule = (_lib.MF_MERGE_SUM if not count_aware else
+                    _lib.MF_MERGE_COUNT if bias_col >= 0 else _lib.MF_MERGE_MEAN)
+            use_counts = rule != _lib.MF_MERGE_SUM
             dptr = None
             if delta_out is not None:
                 dptr = ctypes.c_void_p(delta_out.data_ptr() + off * delta_out.element_size())
             _lib.call("mf_item_merge", self._ptr(tab), self._ptr(snap), I, ld, self.K, bias_col,
-                      self.n_replicas, self._ptr(self.counts[c]) if use_counts else None,
+                      self.n_replicas, rule, self._ptr(self.counts[c]) if use_counts else None,
                       self._ptr(self.totals[c]) if use_counts else None,
                       ctypes.byref(self._hyper), self._ptr(self.pu), self.n_users, self.ld,
                       self._ptr(self.work), dptr, int(apply), self.dtype, st)

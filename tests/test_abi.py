@@ -29,8 +29,8 @@ def test_library_exports_every_header_symbol(lib):
 def test_version_and_error_without_device(lib):
     assert lib.mf_version() == 300
     # argument validation happens before any device call
-    rc = lib.mf_item_merge(None, None, 10, 16, 10, 10, 1, None, None, None, None, 0, 16, None,
-                           None, 1, 0, None)
+    rc = lib.mf_item_merge(None, None, 10, 16, 10, 10, 1, 0, None, None, None, None, 0, 16,
+                           None, None, 1, 0, None)
     assert rc == 1001
     assert b"bad item table" in lib.mf_last_error()
     csr = _lib.MfCsr(0, 0, 0, 0, 0)
@@ -42,6 +42,6 @@ def test_version_and_error_without_device(lib):
 def test_header_constants_match_python():
     text = open(_lib.HEADER_PATH).read()
     for name, val in (("MF_F32", 0), ("MF_F64", 1), ("MF_MODE_PLAIN", 0), ("MF_MODE_ATOMIC", 1),
-                      ("MF_MODE_REPLICA", 2), ("MF_MODE_COHERENT", 3), ("MF_MAX_FACTORS_F32", 512),
+                      ("MF_MODE_REPLICA", 2), ("MF_MODE_COHERENT", 3), ("MF_MODE_REPLICA_ATOMIC", 4), ("MF_MAX_FACTORS_F32", 512),
                       ("MF_MAX_FACTORS_F64", 256)):
         assert "#define %s" % name in text and str(val) in text.split("#define %s" % name)[1].split("\n")[0]

@@ -37,8 +37,20 @@ def oracle_rmse(algo, params, ts, test, affine=False):
     return _oracle_test_rmse(P, f, algo, ts, list(test))[1]
 
 
+def xcc_histogram(n_blocks=4096):
+    import ctypes
+    from surprise_amd import _lib
+    out = torch.zeros(n_blocks, dtype=torch.int32, device="cuda")
+    _lib.call("mf_selftest_xcc", ctypes.c_void_p(out.data_ptr()), n_blocks, None)
+    torch.cuda.synchronize()
+    ids = out.cpu().numpy()
+    print("xcc ids of blocks 0..15:", ids[:16].tolist(), "histogram:",
+          np.bincount(ids, minlength=8).tolist(), flush=True)
+
+
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    xcc_histogram()
     rows = []
     sets = []
     if which in ("all", "u1"):
@@ -55,9 +67,8 @@ def main():
     for dname, (ts, test), cases in sets:
         for algo, params in cases:
             ref = oracle_rmse(algo, params, ts, test, affine=(algo == "SVDpp"))
-            for mode, nw, ch in (("replica", 0, 1), ("replica", 0, 4), ("replica", 256, 1),
-                                 ("atomic", 0, 1), ("atomic", 256, 1), ("coherent", 0, 1),
-                                 ("plain", 0, 1)):
+            for mode, nw, ch in (("replica", 0, 1), ("replica_atomic", 0, 1),
+                                 ("replica_atomic", 0, 4), ("atomic", 0, 1), ("atomic", 256, 1)):
                     if nw and nw > ts.n_users:
                         continue
                     klass = SVD if algo == "SVD" else SVDpp
