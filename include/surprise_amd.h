@@ -17,8 +17,8 @@
  *   - factor tables are row-major.  User rows pu[u] and implicit rows yj[j] have leading
  *     dimension ldu >= n_factors; item rows have ldq >= n_factors + 1 and hold the item bias in
  *     column n_factors: qb[i] = [q_i | b_i | 0 ...].  Padding columns must be zero and stay zero;
- *   - item tables (qb, yj) come in n_replicas consecutive copies (n_items rows each) and must
- *     be < 715 MB per copy (32-bit buffer offsets, three of which must add below 2^31);
+ *   - item tables (qb, yj) must be < 715 MB (32-bit buffer offsets, three of which must add
+ *     below 2^31);
  *   - `dtype` selects the arithmetic type of every floating array: MF_F32 or MF_F64.
  */
 #ifndef SURPRISE_AMD_H
@@ -33,14 +33,13 @@ extern "C" {
 #define MF_F32 0
 #define MF_F64 1
 
-/* Item-side update schedule of the Hogwild kernels. */
-#define MF_MODE_PLAIN   0 /* one shared item table, plain load/store (lock-free Hogwild)          */
-#define MF_MODE_ATOMIC  1 /* one shared item table, item deltas applied with float atomics         */
-#define MF_MODE_REPLICA 2 /* n_replicas item tables, one user queue per replica, drained first by
-                             the waves of XCD (replica id); merged by mf_item_merge once per
-                             epoch-chunk                                                          */
-#define MF_MODE_COHERENT 3 /* one shared item table, write-through (sc1) stores                    */
-#define MF_MODE_REPLICA_ATOMIC 4 /* MF_MODE_REPLICA with item updates applied as float atomics    */
+/* Item-side update schedule of the epoch kernels. */
+#define MF_MODE_PLAIN  0 /* shared item table, plain load/store (lock-free Hogwild!; with one wave
+                            the exact sequential order of the reference)                           */
+#define MF_MODE_ATOMIC 1 /* shared item table, item deltas applied with float atomics              */
+#define MF_MODE_LOG    2 /* item table read-only for the epoch-chunk, every rating's item delta
+                            written to a delta log (row = CSR position), folded into the table by
+                            mf_log_reduce + mf_log_apply: race-free, independent of scheduling     */
 
 #define MF_E_ARG          1001 /* invalid argument (shape, mode, dtype, n_factors too large)      */
 #define MF_E_UNSUPPORTED  1002 /* combination not compiled                                       */
@@ -72,34 +71,63 @@ typedef struct mf_csr {
  * One epoch-chunk of SVD SGD over the users listed in sched[0..n_sched).
  * Replaces the body of SVD.sgd's epoch loop (matrix_factorization.pyx:241-262):
  * each wavefront owns a user (pu[u], bu[u] live in registers, updated in the
- * reference's per-rating order) and applies lock-free Hogwild! updates to the
- * shared item rows qb[i] = [q_i | b_i].
- *   pu [n_users][ldu], bu [n_users], qb [n_replicas][n_items][ldq]
+ * reference's per-rating order); the item rows qb[i] = [q_i | b_i] are updated per `mode`.
+ *   pu [n_users][ldu], bu [n_users], qb [n_items][ldq]
  *   biased    : 0 reproduces SVD(biased=False) (hp->global_mean must then be 0)
- *   mode      : MF_MODE_*; n_replicas is used by MF_MODE_REPLICA only (else pass 1)
- *   rep_ptr   : (MF_MODE_REPLICA) device int32[n_replicas+1]: replica r's user queue is
- *               sched[rep_ptr[r] .. rep_ptr[r+1]); heads: device int32[n_replicas] scratch
- *               (zeroed by the call).  Other modes: NULL, and the waves stride over sched.
+ *   mode      : MF_MODE_*
+ *   qlog      : MF_MODE_LOG: device [nnz][ldq] delta log, row k = rating k of the CSR (columns
+ *               0..n_factors written, the rest untouched); each user's segment must be < 2^30
+ *               bytes (|I_u| * ldq * sizeof(dtype)).  Other modes: NULL.
  *   n_waves   : wavefronts to launch (<= 0: library default = fill the GPU);
- *               1 gives the exact sequential reference order when sched = 0..n_users-1.
- *   dup_items : non-zero if some user lists the same item twice (enables in-register forwarding).
+ *               1 with MF_MODE_PLAIN gives the exact sequential reference order when
+ *               sched = 0..n_users-1.
+ *   dup_items : non-zero if some user lists the same item twice (enables in-register forwarding
+ *               in MF_MODE_PLAIN / MF_MODE_ATOMIC; MF_MODE_LOG reads the snapshot row).
  */
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, const int32_t *rep_ptr,
-                 int32_t *heads, int32_t n_waves, int32_t dup_items, int32_t dtype, void *stream);
+                 const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves, int32_t dup_items,
+                 int32_t dtype, void *stream);
 
 /*
  * One epoch-chunk of SVD++ SGD (SVDpp.sgd epoch body, matrix_factorization.pyx:463-498) in the
  * exact per-user affine form: per user, one gather of y_j (j in I_u), the sequential rating
- * loop with u_impl maintained incrementally, and one affine write-back y_j <- A y_j + c.
- * yj [n_replicas][n_items][ldu] is replicated like qb.  Always biased (SVDpp has no option).
+ * loop with u_impl maintained incrementally, and one affine write-back y_j <- A y_j + c
+ * (stores in MF_MODE_PLAIN, float atomics of (A-1) y_j + c otherwise).  yj [n_items][ldu].
+ * Always biased (SVDpp has no option).
  */
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
-                   const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, const int32_t *rep_ptr,
-                   int32_t *heads, int32_t n_waves, int32_t dup_items, int32_t dtype,
-                   void *stream);
+                   const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves,
+                   int32_t dup_items, int32_t dtype, void *stream);
+
+/* out[0] += sum of x[r][c]^2 over r < n_rows, c < n_cols (x is [n_rows][ld]; out is one device
+ * double).  The <pu^2> statistic of the count-aware merge rules. */
+int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *out, int32_t dtype,
+             void *stream);
+
+/*
+ * Delta-log merge, step 1 (MF_MODE_LOG): sums[p][c] = sum_{x in [piece_beg[p], piece_beg[p+1])}
+ * qlog[perm[x]][c] for c < n_cols (zero for n_cols <= c < ld), summed in x order.  perm lists the
+ * chunk's log rows grouped by item; an item's rows are cut into consecutive pieces.
+ */
+int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *perm,
+                  const int32_t *piece_beg, int64_t n_pieces, void *sums, int32_t dtype,
+                  void *stream);
+
+/*
+ * Delta-log merge, step 2: S_i = sum of sums[p] over p in [item_piece_ptr[i], item_piece_ptr[i+1])
+ * (item_piece_ptr NULL: S_i = sums[i], e.g. after an all-reduce).  delta_out (nullable,
+ * [n_items][ld]) receives S; apply != 0 adds w * S_i to qb[i] in columns < n_factors and bias_col:
+ *   MF_MERGE_SUM:   w = 1;
+ *   MF_MERGE_COUNT: w = (1 - (1-eta)^N) / (N eta), N = totals[i] (ratings of item i in the chunk,
+ *                   all ranks), eta = lr_bi (1 + reg_bi) in bias_col and lr_qi (<p^2> + reg_qi)
+ *                   in factor columns, <p^2> = p2sum[0] / p2_den (p2sum a device double).
+ */
+int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
+                 const void *sums, const int32_t *item_piece_ptr, const int32_t *totals,
+                 const mf_hyper_t *hp, const double *p2sum, double p2_den, int32_t rule,
+                 void *delta_out, int32_t apply, int32_t dtype, void *stream);
 
 /* Merge rules of mf_item_merge. */
 #define MF_MERGE_SUM   0 /* delta = sum_r d_r                                                      */
@@ -108,8 +136,9 @@ int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, v
 #define MF_MERGE_MEAN  2 /* count-weighted MEAN: sum_r (n_r / N) d_r (SVD++ implicit factors)      */
 
 /*
- * Item-side merge of an epoch-chunk for one item table `tab`
- * ([n_replicas][n_items][ld], snapshot `snap` [n_items][ld]):
+ * Item-side merge of an epoch-chunk across ranks for MF_MODE_PLAIN /
+ * MF_MODE_ATOMIC tables and SVD++'s yj: `tab` ([n_replicas][n_items][ld]; one copy per rank in
+ * the library's own engine) against the chunk-start snapshot `snap` [n_items][ld]:
  *     delta[i] = sum_r w_r(i) (tab_r[i] - snap[i])
  * counts ([n_replicas][n_items]: ratings of item i trained in replica r this chunk) and totals
  * ([n_items]: the same summed over every replica of every rank) give n_r and N.

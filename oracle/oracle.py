@@ -139,6 +139,49 @@ def svd_sgd_groups(row_ptr, items, ratings, n_items, K, n_epochs, biased, global
     return pu, qi, bu, bi
 
 
+def svd_sgd_deltalog(row_ptr, items, ratings, n_items, K, n_epochs, biased, global_mean, hp,
+                     pu, qi, chunk_of_user=None, n_chunks=1, merge=2, bu=None, bi=None):
+    """Delta-log schedule (the GPU's MF_MODE_LOG): every user against the chunk-start item
+    snapshot, item deltas merged per item with the count-aware weight (merge=2) or summed (0)."""
+    row_ptr, items, ratings = _csr_args(row_ptr, items, ratings)
+    n_users = len(row_ptr) - 1
+    pu = np.ascontiguousarray(pu, dtype=np.float64)
+    qi = np.ascontiguousarray(qi, dtype=np.float64)
+    bu = np.zeros(n_users) if bu is None else np.ascontiguousarray(bu, dtype=np.float64)
+    bi = np.zeros(n_items) if bi is None else np.ascontiguousarray(bi, dtype=np.float64)
+    c = (np.zeros(n_users, np.int32) if chunk_of_user is None
+         else np.ascontiguousarray(chunk_of_user, dtype=np.int32))
+    lib().oracle_svd_sgd_deltalog(ctypes.c_int64(n_users), ctypes.c_int64(n_items), _p(row_ptr),
+                                  _p(items), _p(ratings), ctypes.c_int32(K),
+                                  ctypes.c_int32(n_epochs), ctypes.c_int32(int(biased)),
+                                  ctypes.c_double(global_mean), ctypes.byref(hp), _p(c),
+                                  ctypes.c_int32(n_chunks), ctypes.c_int32(merge),
+                                  _p(pu), _p(qi), _p(bu), _p(bi))
+    return pu, qi, bu, bi
+
+
+def svdpp_sgd_deltalog(row_ptr, items, ratings, n_items, K, n_epochs, global_mean, hp, pu, qi,
+                       yj, chunk_of_user=None, n_chunks=1, merge=2, merge_y=0, bu=None, bi=None):
+    """SVD++ delta-log schedule: q/b as svd_sgd_deltalog, y_j shared and updated at the end of
+    each user (merge_y=0, the GPU's semantics) or logged and merged by their mean (1)."""
+    row_ptr, items, ratings = _csr_args(row_ptr, items, ratings)
+    n_users = len(row_ptr) - 1
+    pu = np.ascontiguousarray(pu, dtype=np.float64)
+    qi = np.ascontiguousarray(qi, dtype=np.float64)
+    yj = np.ascontiguousarray(yj, dtype=np.float64)
+    bu = np.zeros(n_users) if bu is None else np.ascontiguousarray(bu, dtype=np.float64)
+    bi = np.zeros(n_items) if bi is None else np.ascontiguousarray(bi, dtype=np.float64)
+    c = (np.zeros(n_users, np.int32) if chunk_of_user is None
+         else np.ascontiguousarray(chunk_of_user, dtype=np.int32))
+    lib().oracle_svdpp_sgd_deltalog(ctypes.c_int64(n_users), ctypes.c_int64(n_items), _p(row_ptr),
+                                    _p(items), _p(ratings), ctypes.c_int32(K),
+                                    ctypes.c_int32(n_epochs), ctypes.c_double(global_mean),
+                                    ctypes.byref(hp), _p(c), ctypes.c_int32(n_chunks),
+                                    ctypes.c_int32(merge), ctypes.c_int32(merge_y),
+                                    _p(pu), _p(qi), _p(yj), _p(bu), _p(bi))
+    return pu, qi, yj, bu, bi
+
+
 def svd_predict(u, i, K, biased, global_mean, pu, qi, bu, bi):
     """SVD.estimate on inner ids (-1 = unknown). Returns (est, impossible)."""
     u = np.ascontiguousarray(u, dtype=np.int32)

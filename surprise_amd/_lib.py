@@ -15,11 +15,8 @@ LIB_PATH = os.path.join(_HERE, "libsurprise_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "surprise_amd.h")
 
 MF_F32, MF_F64 = 0, 1
-MF_MODE_PLAIN, MF_MODE_ATOMIC, MF_MODE_REPLICA, MF_MODE_COHERENT = 0, 1, 2, 3
-MF_MODE_REPLICA_ATOMIC = 4
-MODES = {"plain": MF_MODE_PLAIN, "atomic": MF_MODE_ATOMIC, "replica": MF_MODE_REPLICA,
-         "coherent": MF_MODE_COHERENT, "replica_atomic": MF_MODE_REPLICA_ATOMIC}
-REPLICA_MODES = (MF_MODE_REPLICA, MF_MODE_REPLICA_ATOMIC)
+MF_MODE_PLAIN, MF_MODE_ATOMIC, MF_MODE_LOG = 0, 1, 2
+MODES = {"plain": MF_MODE_PLAIN, "atomic": MF_MODE_ATOMIC, "log": MF_MODE_LOG}
 MF_MERGE_SUM, MF_MERGE_COUNT, MF_MERGE_MEAN = 0, 1, 2
 MAX_FACTORS = {MF_F32: 512, MF_F64: 256}
 
@@ -45,9 +42,13 @@ _vp, _i32, _i64, _dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.
 # name -> argtypes (all return int except mf_last_error)
 SIGNATURES = {
     "mf_svd_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32, _i32,
-                     ctypes.POINTER(MfHyper), _i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp],
+                     ctypes.POINTER(MfHyper), _i32, _vp, _i32, _i32, _i32, _vp],
     "mf_svdpp_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp, _i32,
-                       ctypes.POINTER(MfHyper), _i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp],
+                       ctypes.POINTER(MfHyper), _i32, _vp, _i32, _i32, _i32, _vp],
+    "mf_sumsq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
+    "mf_log_reduce": [_vp, _i32, _i32, _vp, _vp, _i64, _vp, _i32, _vp],
+    "mf_log_apply": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, ctypes.POINTER(MfHyper), _vp,
+                     _dbl, _i32, _vp, _i32, _i32, _vp],
     "mf_item_merge": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
                       ctypes.POINTER(MfHyper), _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp],
     "mf_item_apply": [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp],

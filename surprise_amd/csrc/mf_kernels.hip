@@ -139,8 +139,8 @@ __device__ __forceinline__ double readlane(double v, int l) {
 }
 
 __device__ __forceinline__ int xcc_id() {
-    // HW_REG_XCC_ID (hwreg 20), bits [3:0]: the XCD this wave runs on. Used only to pick an
-    // item-table replica (a speed/locality choice; any placement is correct).
+    // HW_REG_XCC_ID (hwreg 20), bits [3:0]: the XCD this wave runs on (mf_selftest_xcc: blocks
+    // are dealt to the 8 XCDs round-robin).
     return (int)(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 0xF);
 }
 
@@ -207,20 +207,30 @@ struct Buf<double> {
 
 // ---------------------------------------------------------------- SGD epoch kernel (SVD, SVD++)
 
-enum { kPlain = MF_MODE_PLAIN, kAtomic = MF_MODE_ATOMIC, kReplica = MF_MODE_REPLICA,
-       kCoherent = MF_MODE_COHERENT, kReplicaAtomic = MF_MODE_REPLICA_ATOMIC };
+enum { kPlain = MF_MODE_PLAIN, kAtomic = MF_MODE_ATOMIC, kLog = MF_MODE_LOG };
+
+// Log rows: a lane whose column is past the bias column stores to this offset (beyond any user's
+// log segment, which is < 2^30 bytes) and is dropped by the range check.
+constexpr uint32_t kLogOob = 0x40000000u;
 
 // Item table row (ldq elements): [q_0 .. q_{K-1} | b_i | 0 ...].  The user row is extended in
 // registers with a constant 1 in column K, so <q_aug, p_aug> = <q_i, p_u> + b_i and the item
 // bias rides in the same gather / scatter as the item factors; its update
 // b_i += lr_bi (err * 1 - reg_bi b_i) is the factor rule with the per-column (lr, reg) swapped.
+//
+// MODE decides what happens to the item row after a rating:
+//   kPlain  store q_i + d (lock-free Hogwild!; with one wave: the exact sequential reference);
+//   kAtomic memory-side float add of d;
+//   kLog    the item table is a read-only snapshot for the whole epoch-chunk and d goes to row k
+//           of the delta log (k = the rating's CSR position); mf_log_reduce / mf_log_apply fold
+//           the log into the table afterwards.  Race-free and independent of wave scheduling.
+// SVD++'s y_j rows are shared state in every mode (kPlain: stores, kAtomic / kLog: float adds).
 template <typename T, int V, int MODE, bool PP, bool DUPS>
 __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
-    T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, int K, int biased,
-    Hyper<T> hp, int n_rep, int n_items, int64_t n_waves_req, const int32_t *__restrict__ rep_ptr,
-    int32_t *heads)
+    T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, int K,
+    int biased, Hyper<T> hp, int n_items, int64_t n_waves_req)
 {
     const int lane = threadIdx.x & (kWave - 1);
     // wave id through readfirstlane: the compiler then knows it (and every user index, CSR
@@ -234,20 +244,22 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
 
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), yrow = (uint32_t)ldu * sizeof(T);
     const uint32_t q_oob = (uint32_t)n_items * qrow, y_oob = (uint32_t)n_items * yrow;
-    constexpr bool REP = MODE == kReplica || MODE == kReplicaAtomic;  // per-XCD replica queues
-    constexpr bool ATOM = MODE == kAtomic || MODE == kReplicaAtomic;  // item updates as atomics
-    constexpr int kStAux = MODE == kCoherent ? kSc1 : 0;
-    // Hogwild schedules read item rows around the CU's L1 (sc1); MF_MODE_PLAIN is the
-    // single-table mode the deterministic one-wave path uses: plain (L1-cached) loads
-    constexpr int kLdAux = MODE == kPlain ? 0 : kSc1;
+    constexpr bool ATOM = MODE == kAtomic;  // item updates as float atomics
+    constexpr bool LOG = MODE == kLog;      // item updates to the delta log
+    constexpr bool YATOM = MODE != kPlain;  // SVD++ y_j updates as float atomics
+    // Rows other waves are updating are read around the CU's L1 (sc1).  kPlain (the
+    // deterministic one-wave path) and the kLog snapshot use plain, L1-cached loads.
+    constexpr int kLdAux = MODE == kAtomic ? kSc1 : 0;
+    constexpr int kYLdAux = MODE == kPlain ? 0 : kSc1;
 
     // per-lane column constants (column c = lane + 64 v)
-    uint32_t cq[V], cu[V];
+    uint32_t cq[V], cu[V], cl[V];
     T one[V], lrq[V], regq[V], lrp[V], regp[V], lry[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const int c = lane + kWave * v;
         cq[v] = c < ldq ? (uint32_t)c * sizeof(T) : q_oob;
+        cl[v] = c <= K ? (uint32_t)c * sizeof(T) : kLogOob;
         cu[v] = c < ldu ? (uint32_t)c * sizeof(T) : (PP ? y_oob : yrow);  // >= pu record too
         const bool fac = c < K, bias = biased && c == K;
         one[v] = bias ? T(1) : T(0);
@@ -260,14 +272,16 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
     const T lr_bu = biased ? hp.lr_bu : T(0);
     const T decay = T(1) - hp.lr_yj * hp.reg_yj;
 
-    // one user block: the reference's per-rating order for user u against item tables
-    // (q_base, y_base) -- replica 0 or the replica whose queue the user came from
-    auto do_user = [&](const int u, T *q_base, T *y_base) {
-        const rsrc_t q_rs = make_rsrc(q_base, q_oob);
-        const rsrc_t y_rs = PP ? make_rsrc(y_base, y_oob) : q_rs;
+    const rsrc_t q_rs = make_rsrc(qb, q_oob);
+    const rsrc_t y_rs = PP ? make_rsrc(yj, y_oob) : q_rs;
+
+    // one user block: the reference's per-rating order for user u
+    auto do_user = [&](const int u) {
         const int64_t s = row_ptr[u];
         const int n = (int)(row_ptr[u + 1] - s);  // |I_u| (< 2^31)
         if (n <= 0) return;
+        // kLog: this user's log segment, rows s .. s+n-1 (n * qrow < 2^30 bytes)
+        const rsrc_t l_rs = LOG ? make_rsrc(qlog + s * ldq, (uint32_t)n * qrow) : q_rs;
         // the user's (item, rating) stream, read with scalar loads (uniform addresses ->
         // s_load, counted by lgkmcnt, out of the vector-memory queue the row gathers use)
         const int32_t *__restrict__ it = items + s;
@@ -293,7 +307,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                     const int j = x + a < n ? x + a : n - 1;
                     const uint32_t ro = (uint32_t)it[j] * yrow + (x + a < n ? 0u : y_oob);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kLdAux>(y_rs, ro + cu[v]);
+                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kYLdAux>(y_rs, ro + cu[v]);
                 }
 #pragma unroll
                 for (int a = 0; a < 8; ++a)
@@ -344,12 +358,13 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                 for (int v = 0; v < V; ++v) part += s_q[d][v] * (PP ? p[v] + imp[v] : p[v]);
                 const T dot = wave_sum(part);                 // <q_i, p_u (+imp)> + b_i
                 const T err = s_r[d] - (hp.gm + bu_u + dot);  // mf.pyx:250 / :483
-                T qn[V];
+                T qd[V], qn[V];
 #pragma unroll
                 for (int v = 0; v < V; ++v) {  // mf.pyx:258-262 / :490-498, old puf and qif
                     const T q = s_q[d][v], pv = p[v];
                     const T pe = PP ? pv + imp[v] : pv;
-                    qn[v] = q + lrq[v] * (err * pe - regq[v] * q);
+                    qd[v] = lrq[v] * (err * pe - regq[v] * q);
+                    qn[v] = q + qd[v];
                     const T pn = pv + lrp[v] * (err * q - regp[v] * pv);
                     p[v] = valid ? pn : pv;
                     if (PP) {
@@ -365,10 +380,12 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                 const uint32_t off = s_off[d];
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
-                    if (ATOM)
-                        Buf<T>::add(q_rs, q_base, (uint32_t)n_items * qrow, off + cq[v], qn[v] - s_q[d][v]);
+                    if (LOG)  // (a tail slot's row offset n * qrow and beyond is dropped)
+                        Buf<T>::template st<0>(l_rs, (uint32_t)(j0 + d) * qrow + cl[v], qd[v]);
+                    else if (ATOM)
+                        Buf<T>::add(q_rs, qb, q_oob, off + cq[v], qd[v]);
                     else
-                        Buf<T>::template st<kStAux>(q_rs, off + cq[v], qn[v]);
+                        Buf<T>::template st<0>(q_rs, off + cq[v], qn[v]);
                 }
                 // keep the next gather below the last use of the slot's old row: hoisting it would
                 // need a second register set and a copy (and a wait) at the loop latch
@@ -403,49 +420,27 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
                     const int j = x + a < n ? x + a : n - 1;
                     ro[a] = (uint32_t)it[j] * yrow + (x + a < n ? 0u : y_oob);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kLdAux>(y_rs, ro[a] + cu[v]);
+                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kYLdAux>(y_rs, ro[a] + cu[v]);
                 }
 #pragma unroll
                 for (int a = 0; a < 8; ++a)
 #pragma unroll
                     for (int v = 0; v < V; ++v) {
-                        if (ATOM)
-                            Buf<T>::add(y_rs, y_base, (uint32_t)n_items * yrow, ro[a] + cu[v],
-                                        (A - T(1)) * g[a][v] + cacc[v]);
+                        if (YATOM)
+                            Buf<T>::add(y_rs, yj, y_oob, ro[a] + cu[v], (A - T(1)) * g[a][v] + cacc[v]);
                         else
-                            Buf<T>::template st<kStAux>(y_rs, ro[a] + cu[v], A * g[a][v] + cacc[v]);
+                            Buf<T>::template st<0>(y_rs, ro[a] + cu[v], A * g[a][v] + cacc[v]);
                     }
             }
         }
     };
 
-    if (REP) {
-        // per-XCD user queues: a wave drains the queue of its own XCD's replica first (the
-        // replica then lives in that XCD's L2), then helps with the others; every user is
-        // always trained against the replica of the queue it was assigned to, so the merge's
-        // per-replica item counts stay exact whatever the dispatch placement.
-        const int r0 = xcc_id() % n_rep;
-        for (int qq = 0; qq < n_rep; ++qq) {
-            const int r = r0 + qq < n_rep ? r0 + qq : r0 + qq - n_rep;
-            const int beg = rep_ptr[r], len = rep_ptr[r + 1] - beg;
-            T *q_r = qb + (int64_t)r * n_items * ldq;
-            T *y_r = PP ? yj + (int64_t)r * n_items * ldu : nullptr;
-            for (;;) {
-                int idx = 0;
-                if (lane == 0) idx = atomicAdd(heads + r, 1);
-                idx = __builtin_amdgcn_readfirstlane(idx);
-                if (idx >= len) break;
-                do_user(sched[beg + idx], q_r, y_r);
-            }
-        }
-    } else {
-        for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w], qb, yj);
-    }
+    for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w]);
 }
 
 // ---------------------------------------------------------------- item-table merge (epoch-chunk)
 //
-// After an epoch-chunk, replica r of an item table holds snapshot + d_r.  Plain SUM of the d_r
+// After an epoch-chunk, copy r of an item table (one per rank) holds snapshot + d_r.  Plain SUM of the d_r
 // is right while every replica made only a few small steps on a row, and overshoots by up to a
 // factor n_replicas once the steps saturate (a popular item's bias converges within one chunk
 // in every replica).  The count-aware merge weights each replica's delta per row by
@@ -525,6 +520,100 @@ __global__ __launch_bounds__(kBlock) void item_apply_kernel(T *tab, T *snap, int
         const T nv = snap[x] + delta[x];
         snap[x] = nv;
         for (int r = 0; r < n_rep; ++r) tab[r * total + x] = nv;
+    }
+}
+
+// ---------------------------------------------------------------- delta-log merge (MF_MODE_LOG)
+//
+// After an epoch-chunk in kLog mode, log row k holds the item-row delta d_k of rating k.  The
+// merge is a segmented sum in item order: perm lists the chunk's log rows grouped by item (rows
+// of an item in increasing k, i.e. the reference's user order), cut into pieces of <= 64 rows
+// so the most popular item does not serialise one wave.  Fixed order throughout: the result is
+// bit-reproducible.  Then per item, with N = ratings of the item in the chunk (all ranks):
+//     q_i += w(N) * sum_k d_k,   w(N) = (1 - (1-eta)^N) / (N eta),
+// the count-aware weight for N single steps (every user is its own group): 1 for rare items,
+// 1/(N eta) for items whose row would have converged within the chunk (plain SUM
+// diverges on ML-1M).  eta as in mf_item_merge.
+
+template <typename T, int V>
+__global__ __launch_bounds__(kBlock) void log_reduce_kernel(
+    const T *__restrict__ qlog, int ld, int n_cols, const int32_t *__restrict__ perm,
+    const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
+        const int beg = piece_beg[pc], end = piece_beg[pc + 1];
+        T acc[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = T(0);
+        constexpr int kU = 8;
+        for (int x = beg; x < end; x += kU) {
+            T g[kU][V];
+#pragma unroll
+            for (int a = 0; a < kU; ++a) {
+                const bool ok = x + a < end;
+                const T *row = qlog + (int64_t)perm[ok ? x + a : beg] * ld + lane;
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    g[a][v] = (ok && lane + kWave * v < n_cols) ? row[kWave * v] : T(0);
+            }
+#pragma unroll
+            for (int a = 0; a < kU; ++a)
+#pragma unroll
+                for (int v = 0; v < V; ++v) acc[v] += g[a][v];
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+            if (lane + kWave * v < ld) sums[pc * ld + lane + kWave * v] = acc[v];
+    }
+}
+
+template <typename T, int V>
+__global__ __launch_bounds__(kBlock) void log_apply_kernel(
+    T *__restrict__ qb, int n_items, int ld, int n_fac, int bias_col, const T *__restrict__ sums,
+    const int32_t *__restrict__ item_piece_ptr, const int32_t *__restrict__ totals, int count_rule,
+    double eta_bias, double lr_fac, double reg_fac, const double *__restrict__ p2sum,
+    double p2_den, T *__restrict__ delta_out, int apply)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    double eta_fac = 0, l_fac = 0, l_bias = 0;
+    if (count_rule) {
+        eta_fac = lr_fac * (*p2sum / p2_den + reg_fac);
+        l_fac = log1p(-eta_fac);
+        l_bias = log1p(-eta_bias);
+    }
+    for (int64_t i = wave; i < n_items; i += n_waves) {
+        const int p0 = item_piece_ptr ? item_piece_ptr[i] : (int)i;
+        const int p1 = item_piece_ptr ? item_piece_ptr[i + 1] : (int)i + 1;
+        T acc[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = T(0);
+        for (int pc = p0; pc < p1; ++pc)
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if (lane + kWave * v < ld) acc[v] += sums[(int64_t)pc * ld + lane + kWave * v];
+        const double N = totals ? (double)totals[i] : 0.0;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const int c = lane + kWave * v;
+            if (c >= ld) continue;
+            const int64_t x = i * ld + c;
+            if (delta_out) delta_out[x] = acc[v];
+            if (apply && (c < n_fac || c == bias_col)) {
+                double w = 1.0;
+                if (count_rule && N > 1.0) {
+                    const bool b = c == bias_col;
+                    w = -expm1(N * (b ? l_bias : l_fac)) / (N * (b ? eta_bias : eta_fac));
+                }
+                qb[x] += (T)w * acc[v];
+            }
+        }
     }
 }
 
@@ -665,7 +754,7 @@ int dispatch_v(int ld, F &&f)
 
 int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const void *bu,
                 const void *qb, const mf_hyper_t *hp, int K, int ldu, int ldq, int mode,
-                int n_rep, int dtype)
+                const void *qlog, int dtype)
 {
     if (!c || !c->row_ptr || !c->items || !c->ratings) return set_err(MF_E_ARG, "null csr");
     if (!sched || !pu || !bu || !qb || !hp) return set_err(MF_E_ARG, "null argument");
@@ -673,43 +762,38 @@ int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const v
     const int maxk = dtype == MF_F32 ? MF_MAX_FACTORS_F32 : MF_MAX_FACTORS_F64;
     if (K < 1 || K > maxk) return set_err(MF_E_ARG, "n_factors out of range");
     if (ldu < K || ldq < K + 1) return set_err(MF_E_ARG, "need ldu >= n_factors, ldq >= n_factors+1");
-    if (mode < MF_MODE_PLAIN || mode > MF_MODE_REPLICA_ATOMIC) return set_err(MF_E_ARG, "bad mode");
-    if (n_rep < 1 || n_rep > 16) return set_err(MF_E_ARG, "n_replicas must be in [1, 16]");
+    if (mode < MF_MODE_PLAIN || mode > MF_MODE_LOG) return set_err(MF_E_ARG, "bad mode");
+    if (mode == MF_MODE_LOG && !qlog) return set_err(MF_E_ARG, "MF_MODE_LOG needs qlog");
     const size_t esz = dtype == MF_F32 ? 4 : 8;
     if ((uint64_t)c->n_items * (uint64_t)ldq * esz >= kMaxTable ||
         (uint64_t)c->n_items * (uint64_t)ldu * esz >= kMaxTable)
-        return set_err(MF_E_UNSUPPORTED, "item table >= 715 MB per replica (32-bit buffer offsets)");
+        return set_err(MF_E_UNSUPPORTED, "item table >= 715 MB (32-bit buffer offsets)");
     return 0;
 }
 
 template <bool PP>
 int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
-                 int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t K, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, int32_t n_rep, const int32_t *rep_ptr,
-                 int32_t *heads, int32_t n_waves, int32_t dups, int32_t dtype, void *stream)
+                 int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, int32_t K,
+                 int32_t biased, const mf_hyper_t *hp, int32_t mode, int32_t n_waves, int32_t dups,
+                 int32_t dtype, void *stream)
 {
-    if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, n_rep, dtype)) return rc;
+    if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, qlog, dtype)) return rc;
     if (PP && !yj) return set_err(MF_E_ARG, "null yj");
-    const bool rep_mode = mode == MF_MODE_REPLICA || mode == MF_MODE_REPLICA_ATOMIC;
-    if (rep_mode && (!rep_ptr || !heads))
-        return set_err(MF_E_ARG, "replica modes need rep_ptr and heads");
     if (n_sched <= 0) return 0;
     const int64_t waves = n_waves > 0 ? n_waves : default_waves(n_sched);
     hipStream_t st = (hipStream_t)stream;
-    if (rep_mode) {
-        hipError_t e = hipMemsetAsync(heads, 0, sizeof(int32_t) * n_rep, st);
-        if (e != hipSuccess) return set_err((int)e, "hipMemsetAsync(heads)");
-    }
     auto run = [&](auto tag_t, auto mode_c) -> int {
         using T = decltype(tag_t);
         constexpr int M = decltype(mode_c)::value;
         return dispatch_v<T>(ldq, [&](auto vc) -> int {
             constexpr int V = decltype(vc)::value;
-            auto kern = dups ? mf_epoch_kernel<T, V, M, PP, true> : mf_epoch_kernel<T, V, M, PP, false>;
+            // (kLog reads a snapshot: a repeated item sees the chunk-start row, no forwarding)
+            auto kern = (dups && M != kLog) ? mf_epoch_kernel<T, V, M, PP, true>
+                                            : mf_epoch_kernel<T, V, M, PP, false>;
             hipLaunchKernelGGL(kern, dim3(grid_for_waves(waves)), dim3(kBlock), 0, st,
                                csr->row_ptr, csr->items, (const T *)csr->ratings, sched, n_sched,
-                               (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, K, biased,
-                               cast_hyper<T>(hp), n_rep, csr->n_items, waves, rep_ptr, heads);
+                               (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, (T *)qlog, K, biased,
+                               cast_hyper<T>(hp), csr->n_items, waves);
             return check_launch(PP ? "mf_epoch_kernel<svdpp>" : "mf_epoch_kernel<svd>");
         });
     };
@@ -717,10 +801,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         switch (mode) {
             case MF_MODE_PLAIN: return run(tag_t, std::integral_constant<int, kPlain>{});
             case MF_MODE_ATOMIC: return run(tag_t, std::integral_constant<int, kAtomic>{});
-            case MF_MODE_REPLICA: return run(tag_t, std::integral_constant<int, kReplica>{});
-            case MF_MODE_REPLICA_ATOMIC:
-                return run(tag_t, std::integral_constant<int, kReplicaAtomic>{});
-            default: return run(tag_t, std::integral_constant<int, kCoherent>{});
+            default: return run(tag_t, std::integral_constant<int, kLog>{});
         }
     };
     return dtype == MF_F32 ? by_mode(float{}) : by_mode(double{});
@@ -737,28 +818,99 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 300; }
+int mf_version(void) { return 400; }
 
 const char *mf_last_error(void) { return g_err; }
 
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, const int32_t *rep_ptr,
-                 int32_t *heads, int32_t n_waves, int32_t dup_items, int32_t dtype, void *stream)
+                 const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves, int32_t dup_items,
+                 int32_t dtype, void *stream)
 {
-    return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, nullptr, n_factors,
-                               biased, hp, mode, n_replicas, rep_ptr, heads, n_waves, dup_items,
-                               dtype, stream);
+    return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, nullptr, qlog, n_factors,
+                               biased, hp, mode, n_waves, dup_items, dtype, stream);
 }
 
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
-                   const mf_hyper_t *hp, int32_t mode, int32_t n_replicas, const int32_t *rep_ptr,
-                   int32_t *heads, int32_t n_waves, int32_t dup_items, int32_t dtype,
-                   void *stream)
+                   const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves,
+                   int32_t dup_items, int32_t dtype, void *stream)
 {
-    return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, n_factors, 1, hp,
-                              mode, n_replicas, rep_ptr, heads, n_waves, dup_items, dtype, stream);
+    return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, n_factors, 1, hp,
+                              mode, n_waves, dup_items, dtype, stream);
+}
+
+int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *out, int32_t dtype,
+             void *stream)
+{
+    if (!out || n_rows < 0 || n_cols < 0 || ld < n_cols) return set_err(MF_E_ARG, "bad argument");
+    if (n_rows == 0 || n_cols == 0) return 0;
+    if (!x) return set_err(MF_E_ARG, "null x");
+    const int g = elementwise_grid(n_rows * n_cols);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MF_F32)
+        hipLaunchKernelGGL(sumsq_kernel<float>, dim3(g), dim3(kBlock), 0, st, (const float *)x,
+                           n_rows, n_cols, ld, out);
+    else if (dtype == MF_F64)
+        hipLaunchKernelGGL(sumsq_kernel<double>, dim3(g), dim3(kBlock), 0, st, (const double *)x,
+                           n_rows, n_cols, ld, out);
+    else
+        return set_err(MF_E_ARG, "bad dtype");
+    return check_launch("sumsq_kernel");
+}
+
+int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *perm,
+                  const int32_t *piece_beg, int64_t n_pieces, void *sums, int32_t dtype,
+                  void *stream)
+{
+    if (n_pieces < 0 || ld < 1 || n_cols < 0 || n_cols > ld) return set_err(MF_E_ARG, "bad shape");
+    if (n_pieces == 0) return 0;
+    if (!qlog || !perm || !piece_beg || !sums) return set_err(MF_E_ARG, "null argument");
+    const int g = grid_for_waves(default_waves(n_pieces));
+    hipStream_t st = (hipStream_t)stream;
+    auto run = [&](auto tag_t) -> int {
+        using T = decltype(tag_t);
+        return dispatch_v<T>(ld, [&](auto vc) -> int {
+            hipLaunchKernelGGL((log_reduce_kernel<T, decltype(vc)::value>), dim3(g), dim3(kBlock), 0,
+                               st, (const T *)qlog, ld, n_cols, perm, piece_beg, n_pieces, (T *)sums);
+            return check_launch("log_reduce_kernel");
+        });
+    };
+    if (dtype == MF_F32) return run(float{});
+    if (dtype == MF_F64) return run(double{});
+    return set_err(MF_E_ARG, "bad dtype");
+}
+
+int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
+                 const void *sums, const int32_t *item_piece_ptr, const int32_t *totals,
+                 const mf_hyper_t *hp, const double *p2sum, double p2_den, int32_t rule,
+                 void *delta_out, int32_t apply, int32_t dtype, void *stream)
+{
+    if (n_items < 0 || ld < 1 || n_factors < 0 || n_factors > ld || bias_col >= ld)
+        return set_err(MF_E_ARG, "bad shape");
+    if (rule != MF_MERGE_SUM && rule != MF_MERGE_COUNT) return set_err(MF_E_ARG, "bad merge rule");
+    const int count_rule = rule == MF_MERGE_COUNT;
+    if (count_rule && (!totals || !hp || !p2sum || !(p2_den > 0)))
+        return set_err(MF_E_ARG, "count-aware rule needs totals, hp, p2sum, p2_den > 0");
+    if (n_items == 0 || (!apply && !delta_out)) return 0;
+    if (!sums || (apply && !qb)) return set_err(MF_E_ARG, "null argument");
+    const int g = grid_for_waves(default_waves(n_items));
+    hipStream_t st = (hipStream_t)stream;
+    const double eta_b = count_rule ? hp->lr_bi * (1.0 + hp->reg_bi) : 0.0;
+    const double lr_f = count_rule ? hp->lr_qi : 0.0, reg_f = count_rule ? hp->reg_qi : 0.0;
+    auto run = [&](auto tag_t) -> int {
+        using T = decltype(tag_t);
+        return dispatch_v<T>(ld, [&](auto vc) -> int {
+            hipLaunchKernelGGL((log_apply_kernel<T, decltype(vc)::value>), dim3(g), dim3(kBlock), 0,
+                               st, (T *)qb, n_items, ld, n_factors, bias_col, (const T *)sums,
+                               item_piece_ptr, totals, count_rule, eta_b, lr_f, reg_f, p2sum,
+                               p2_den, (T *)delta_out, apply);
+            return check_launch("log_apply_kernel");
+        });
+    };
+    if (dtype == MF_F32) return run(float{});
+    if (dtype == MF_F64) return run(double{});
+    return set_err(MF_E_ARG, "bad dtype");
 }
 
 int mf_item_merge(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_factors,

@@ -1,22 +1,21 @@
-"""Multi-GPU schedule: users sharded by row across ranks, item-side deltas
+"""Multi-GPU schedule: users sharded by row across ranks, item-side updates
 SUM-all-reduced once per epoch-chunk.
 
 One process per GPU (torchrun / torch.distributed; backend "nccl" is RCCL on
 ROCm, "gloo" for the CPU tests).  Each rank owns a contiguous range of users
-balanced by rating count, so pu/bu rows never cross ranks; qi/bi (and yj for
-SVD++) are replicated and every rank runs its epoch-chunk from the same
-snapshot.  After the chunk each rank contributes its (weighted) ``local -
-snapshot`` and the SUM of all contributions is added to the snapshot on every
-rank.  The weights are the count-aware rule of mf_item_merge
-(include/surprise_amd.h): plain SUM while a row made few small steps per group,
-count-weighted MEAN once they saturate.  Measured with the oracle on the
-ML-1M-shape fold (K=100, E=20): plain SUM diverges (+0.90 RMSE) once a popular
-item's bias converges inside every group, MEAN is 1.3e-2 to 2.7e-2 off, the
-count-aware rule stays within 6.3e-4 at 8 and 64 groups.
+balanced by rating count, so pu/bu rows never cross ranks; item tables are
+replicated and every rank runs its epoch-chunk from the same chunk-start state.
 
-The same delta/apply protocol merges the per-XCD item replicas inside one GPU
-(MF_MODE_REPLICA), so a rank's contribution is already the weighted sum over
-its replicas.
+  mode "log":  each rank folds its delta log into per-item sums S_i; the SUM
+               all-reduce of S (and of the <pu^2> partials) gives every rank the
+               same S, applied with the count-aware weight w(N_i) of the global
+               per-item count -- the identical result of one GPU processing every
+               rank's users (mf_log_apply, include/surprise_amd.h).
+  other modes: each rank contributes its weighted ``local - snapshot`` item delta
+               (mf_item_merge's count-aware rule, n_r = the rank's ratings of the
+               item), SUM all-reduced and added to the snapshot.
+SVD++'s y_j rows are per-rank shared state, merged across ranks by the
+count-weighted mean of the rank deltas.
 """
 from __future__ import annotations
 
@@ -51,21 +50,8 @@ def chunk_users(users, row_ptr, n_chunks: int):
     return [order[c::n_chunks].astype(np.int32) for c in range(n_chunks)]
 
 
-def replica_queues(users, row_ptr, n_replicas: int):
-    """Deal a chunk's users (heaviest first) to n_replicas queues in snake order
-    (0..R-1, R-1..0, ...): near-equal rating counts per queue, each queue heaviest-first."""
-    users = np.asarray(users, dtype=np.int64)
-    if n_replicas == 1:
-        return [users.astype(np.int32)]
-    deg = np.diff(np.asarray(row_ptr, dtype=np.int64))[users]
-    order = users[np.argsort(-deg, kind="stable")]
-    pos = np.arange(len(order)) % (2 * n_replicas)
-    lane = np.where(pos < n_replicas, pos, 2 * n_replicas - 1 - pos)
-    return [order[lane == r].astype(np.int32) for r in range(n_replicas)]
-
-
 def item_counts(users, row_ptr, items, n_items: int):
-    """Ratings per item among `users` (the per-replica n_r of the count-aware merge)."""
+    """Ratings per item among `users` (a rank's n_r in the count-aware merge)."""
     row_ptr = np.asarray(row_ptr, dtype=np.int64)
     users = np.asarray(users, dtype=np.int64)
     if len(users) == 0:
@@ -107,18 +93,16 @@ class DistContext:
 class ItemSync:
     """Epoch-chunk protocol shared by the HIP engine and the CPU test engine.
 
-    Subclasses provide ``n_replicas``, ``run_chunk(c)``, ``_merge_local()``
-    (replica merge + apply in one pass), ``_delta_into(buf)``, ``_apply(buf)``,
-    ``_delta_buffer()`` and ``_owned_user_rows()`` / ``_gather_users(ctx)``."""
+    Subclasses provide ``run_chunk(c)``, ``_merge_local()`` (single-rank fold, may
+    be a no-op), ``_delta_into(buf)``, ``_apply(buf)``, ``_delta_buffer()`` and
+    ``_gather_users(ctx)``."""
 
     n_chunks = 1
-    n_replicas = 1
 
     def sync_items(self, ctx: DistContext | None):
         world = 1 if ctx is None else ctx.world
         if world == 1:
-            if self.n_replicas > 1:
-                self._merge_local()
+            self._merge_local()
             return
         buf = self._delta_buffer()
         self._delta_into(buf)

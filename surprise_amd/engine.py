@@ -2,17 +2,18 @@
 
 HBM layout for one rank (T = float32 or float64; rows padded to 64-byte multiples):
   row_ptr int64[U+1], items int32[nnz], ratings T[nnz]     user-major CSR, all_ratings() order
-  sched   int32[...] per epoch-chunk                        users heaviest-first (Hogwild) or in
-                                                            ur order (deterministic mode)
+  sched   int32[...] per epoch-chunk                        users heaviest-first, or in ur order
+                                                            (deterministic mode)
   pu T[U, ldu], bu T[U]                                     user side, owned by one wave per user
-  qb T[R, I, ldq] = [q_i | b_i | 0..]                       item factors + item bias in one row,
-                                                            R = item replicas
-  yj T[R, I, ldu]                                           SVD++ implicit factors
-  qb_s, (yj_s)                                              chunk-start snapshot (R > 1 or world > 1)
-  delta T[I*ldq (+ I*ldu)]                                  packed item delta for the all-reduce
+  qb T[I, ldq] = [q_i | b_i | 0..]                          item factors + item bias in one row
+  yj T[I, ldu]                                              SVD++ implicit factors
+  qlog T[nnz_rank, ldq]                                     "log" mode: item delta per rating
+  perm int32[nnz_chunk], piece_beg, item_piece_ptr          "log" mode: per-chunk item grouping
+  sums T[pieces, ldq]                                       "log" mode: partial sums per piece
+  qb_s, yj_s                                                chunk-start snapshots (world > 1)
 
 Every compute step is a HIP kernel behind include/surprise_amd.h; torch only
-allocates device memory and supplies the stream.
+allocates device memory, supplies the stream and runs the RCCL all-reduce.
 """
 from __future__ import annotations
 
@@ -21,7 +22,9 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from .dist import ItemSync, chunk_users, item_counts, replica_queues
+from .dist import ItemSync, chunk_users, item_counts
+
+PIECE_ROWS = 64  # log rows summed by one wave of mf_log_reduce
 
 
 def _pad64(n: int, dtype: int) -> int:
@@ -39,13 +42,36 @@ def default_ldq(n_factors: int, dtype: int) -> int:
     return _pad64(n_factors + 1, dtype)
 
 
+def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS):
+    """Item grouping of one epoch-chunk's delta-log rows (MF_MODE_LOG).
+
+    Returns (perm, piece_beg, item_piece_ptr, counts): perm = CSR positions of the ratings of
+    `users`, grouped by item, increasing position within an item (the reference's user order);
+    an item's rows are cut into pieces of <= piece_rows; counts[i] = ratings of item i."""
+    row_ptr = np.asarray(row_ptr, np.int64)
+    users = np.sort(np.asarray(users, np.int64))
+    starts, ends = row_ptr[users], row_ptr[users + 1]
+    lens = ends - starts
+    tot = int(lens.sum())
+    ks = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(tot)
+    it = np.asarray(items)[ks]
+    perm = ks[np.argsort(it, kind="stable")].astype(np.int32)
+    counts = np.bincount(it, minlength=n_items).astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    npc = -(-counts // piece_rows)
+    item_piece_ptr = np.concatenate([[0], np.cumsum(npc)]).astype(np.int32)
+    piece_item = np.repeat(np.arange(n_items), npc)
+    local = np.arange(len(piece_item)) - item_piece_ptr[piece_item]
+    piece_beg = np.concatenate([offs[piece_item] + piece_rows * local, [tot]]).astype(np.int32)
+    return perm, piece_beg, item_piece_ptr, counts.astype(np.int32)
+
+
 class MFEngine(ItemSync):
     """SVD / SVD++ SGD on one GPU (one rank of a multi-GPU job)."""
 
     def __init__(self, csr, n_items, n_factors, *, algo="svd", hyper=None, biased=True,
-                 dtype="float32", mode="replica", n_replicas=8, n_chunks=1, users=None,
-                 deterministic=False, user_order=None, n_waves=0, device=None, ld=None,
-                 world=1, merge="count"):
+                 dtype="float32", mode="log", n_chunks=1, users=None, deterministic=False,
+                 user_order=None, n_waves=0, device=None, ld=None, world=1, merge="count"):
         torch = _lib.require_gpu()
         self.torch = torch
         self.algo = algo
@@ -60,22 +86,24 @@ class MFEngine(ItemSync):
         self.ld = int(ld) if ld else default_ld(self.K, self.dtype)
         self.ldq = default_ldq(self.K, self.dtype)
         row_ptr, items, ratings = csr
+        row_ptr = np.asarray(row_ptr, np.int64)
         self.n_users = len(row_ptr) - 1
         self.n_items = int(n_items)
         self.biased = bool(biased)
         self.deterministic = bool(deterministic)
         if self.deterministic:
-            mode, n_replicas, n_chunks, n_waves = "plain", 1, 1, 1
+            mode, n_chunks, n_waves = "plain", 1, 1
         self.mode = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
-        self.n_replicas = int(n_replicas) if self.mode in _lib.REPLICA_MODES else 1
         self.n_chunks = max(1, int(n_chunks))
         self.n_waves = int(n_waves)
         self.world = int(world)
+        self.merge_rule = merge
         self.stream = torch.cuda.current_stream(self.dev)
+        esz = 8 if self.dtype == _lib.MF_F64 else 4
 
         # ---- CSR + schedules
         dev = self.dev
-        self.row_ptr = torch.from_numpy(np.ascontiguousarray(row_ptr, np.int64)).to(dev)
+        self.row_ptr = torch.from_numpy(np.ascontiguousarray(row_ptr)).to(dev)
         self.items = torch.from_numpy(np.ascontiguousarray(items, np.int32)).to(dev)
         self.ratings = torch.from_numpy(np.ascontiguousarray(ratings, np.float64)).to(
             dev, self.tdt)
@@ -87,35 +115,45 @@ class MFEngine(ItemSync):
             chunks = [order]
         else:
             chunks = chunk_users(self.users, row_ptr, self.n_chunks)
-        # per chunk: the user schedule (replica mode: R queues back to back, rep_ptr[R+1]) and
-        # counts[R, I] = ratings of item i trained in replica r (the count-aware merge's n_r)
-        R = self.n_replicas
-        self.sched, self.rep_ptr, self.counts, self._totals_local = [], [], [], []
+        to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        self.sched = [to_dev(np.asarray(c, np.int32)) for c in chunks]
+        self._totals_local = []
+        self.logs = []  # "log" mode: per chunk (perm, piece_beg, item_piece_ptr, n_pieces)
         for c in chunks:
-            qs = replica_queues(c, row_ptr, R)
-            self.sched.append(torch.from_numpy(np.ascontiguousarray(np.concatenate(qs), np.int32)).to(dev))
-            ptr = np.zeros(R + 1, np.int32)
-            np.cumsum([len(q) for q in qs], out=ptr[1:])
-            self.rep_ptr.append(torch.from_numpy(ptr).to(dev))
-            cnt = np.stack([item_counts(q, row_ptr, items, self.n_items) for q in qs])
-            self.counts.append(torch.from_numpy(cnt.astype(np.int32)).to(dev))
-            self._totals_local.append(cnt.sum(0).astype(np.int32))
+            if self.mode == _lib.MF_MODE_LOG:
+                perm, pb, ipp, cnt = log_layout(row_ptr, items, c, self.n_items)
+                self.logs.append((to_dev(perm), to_dev(pb), to_dev(ipp), len(pb) - 1))
+            else:
+                cnt = item_counts(c, row_ptr, items, self.n_items).astype(np.int32)
+            self._totals_local.append(cnt)
+        self.counts = [to_dev(t) for t in self._totals_local]  # this rank's n_r per chunk
         self.totals = None  # set by _prepare(): summed over every rank
-        self.heads = torch.zeros(R, dtype=torch.int32, device=dev)
         self.work = torch.zeros(1, dtype=torch.float64, device=dev)
-        self.merge_rule = merge
         self.dup_items = int(_has_duplicate_items(row_ptr, items))
 
         # ---- factor tables
-        U, I, ld, ldq, R = self.n_users, self.n_items, self.ld, self.ldq, self.n_replicas
+        U, I, ld, ldq = self.n_users, self.n_items, self.ld, self.ldq
         z = lambda *shape: torch.zeros(*shape, dtype=self.tdt, device=dev)
         self.pu, self.bu = z(U, ld), z(U)
-        self.qb = z(R, I, ldq)
-        self.yj = z(R, I, ld) if algo == "svdpp" else None
-        self.need_snap = R > 1 or self.world > 1
-        if self.need_snap:
-            self.qb_s = z(I, ldq)
-            self.yj_s = z(I, ld) if algo == "svdpp" else None
+        self.qb = z(I, ldq)
+        self.yj = z(I, ld) if algo == "svdpp" else None
+        # the user rows this rank owns form one range [u_lo, u_hi) (shard_users)
+        self.u_lo = int(self.users.min()) if len(self.users) else 0
+        self.u_hi = int(self.users.max()) + 1 if len(self.users) else 0
+        self.qlog = None
+        if self.mode == _lib.MF_MODE_LOG:
+            k_lo, k_hi = int(row_ptr[self.u_lo]), int(row_ptr[self.u_hi])
+            deg = np.diff(row_ptr)
+            if len(deg) and int(deg.max()) * ldq * esz >= (1 << 30):
+                raise _lib.SurpriseAMDError("a user's delta-log segment would exceed 1 GiB; "
+                                            "use mode='atomic'")
+            self.qlog = z(max(k_hi - k_lo, 1), ldq)
+            # the kernels index the log by absolute CSR position k
+            self._qlog_base = self.qlog.data_ptr() - k_lo * ldq * esz
+            self.sums = z(max(lg[3] for lg in self.logs), ldq)
+        snap_q = self.world > 1 and self.mode != _lib.MF_MODE_LOG
+        self.qb_s = z(I, ldq) if snap_q else None
+        self.yj_s = z(I, ld) if (self.world > 1 and self.yj is not None) else None
         self._delta = None
         self._hyper = _lib.MfHyper(**(hyper or {}))
         if not self.biased:
@@ -123,7 +161,7 @@ class MFEngine(ItemSync):
 
     # ------------------------------------------------------------------ state in / out
     def set_factors(self, pu, qi, bu=None, bi=None, yj=None):
-        """Upload host fp64 arrays (n, K) into the padded device tables (all replicas)."""
+        """Upload host fp64 arrays (n, K) into the padded device tables."""
         t = self.torch
         K = self.K
 
@@ -135,52 +173,68 @@ class MFEngine(ItemSync):
         put(self.pu, pu)
         self.bu.copy_(t.from_numpy(np.zeros(self.n_users) if bu is None else
                                    np.asarray(bu, np.float64)).to(self.dev, self.tdt))
-        for r in range(self.n_replicas):
-            put(self.qb[r], qi)
-            self.qb[r][:, K].copy_(t.from_numpy(np.zeros(self.n_items) if bi is None else
-                                                np.asarray(bi, np.float64)).to(self.dev, self.tdt))
-            if self.yj is not None:
-                put(self.yj[r], yj)
-        if self.need_snap:
-            self.qb_s.copy_(self.qb[0])
-            if self.yj is not None:
-                self.yj_s.copy_(self.yj[0])
+        put(self.qb, qi)
+        self.qb[:, K].copy_(t.from_numpy(np.zeros(self.n_items) if bi is None else
+                                         np.asarray(bi, np.float64)).to(self.dev, self.tdt))
+        if self.yj is not None:
+            put(self.yj, yj)
+        if self.qb_s is not None:
+            self.qb_s.copy_(self.qb)
+        if self.yj_s is not None:
+            self.yj_s.copy_(self.yj)
 
     def get_factors(self):
         """Host fp64 copies (pu, qi, bu, bi, yj) with the padding columns dropped."""
         self.stream.synchronize()
         K = self.K
         h = lambda x: x.to(self.torch.float64).cpu().numpy()
-        out = dict(pu=h(self.pu[:, :K]), qi=h(self.qb[0][:, :K]), bu=h(self.bu),
-                   bi=h(self.qb[0][:, K]))
-        out["yj"] = h(self.yj[0][:, :K]) if self.yj is not None else None
+        out = dict(pu=h(self.pu[:, :K]), qi=h(self.qb[:, :K]), bu=h(self.bu),
+                   bi=h(self.qb[:, K]))
+        out["yj"] = h(self.yj[:, :K]) if self.yj is not None else None
         return out
 
     # ------------------------------------------------------------------ kernels
     def _ptr(self, t):
         return ctypes.c_void_p(t.data_ptr())
 
-    def run_chunk(self, c: int):
+    def _st(self):
+        return ctypes.c_void_p(self.stream.cuda_stream)
+
+    @property
+    def is_log(self):
+        return self.mode == _lib.MF_MODE_LOG
+
+    def run_chunk(self, c: int, events=None):
+        """Launch the epoch kernel for chunk c (log mode: preceded by the <pu^2> reduction the
+        merge's count-aware weights use, taken at the chunk start like the oracle).  events:
+        optional (start, end) torch.cuda.Event pair recorded around the epoch kernel alone."""
         s = self.sched[c]
-        st = ctypes.c_void_p(self.stream.cuda_stream)
-        rep = self.mode in _lib.REPLICA_MODES
-        rp = self._ptr(self.rep_ptr[c]) if rep else None
-        hd = self._ptr(self.heads) if rep else None
+        st = self._st()
+        qlog = None
+        if self.is_log:
+            qlog = ctypes.c_void_p(self._qlog_base)
+            self.work.zero_()
+            _lib.call("mf_sumsq", ctypes.c_void_p(self.pu.data_ptr() +
+                                                  self.u_lo * self.ld * self.pu.element_size()),
+                      self.u_hi - self.u_lo, self.K, self.ld, self._ptr(self.work), self.dtype, st)
+        if events is not None:
+            events[0].record(self.stream)
         if self.algo == "svd":
             _lib.call("mf_svd_epoch", ctypes.byref(self._csr), self._ptr(s), s.numel(),
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
                       self.ldq, self.K, int(self.biased), ctypes.byref(self._hyper), self.mode,
-                      self.n_replicas, rp, hd, self.n_waves, self.dup_items, self.dtype, st)
+                      qlog, self.n_waves, self.dup_items, self.dtype, st)
         else:
             _lib.call("mf_svdpp_epoch", ctypes.byref(self._csr), self._ptr(s), s.numel(),
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
                       self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper),
-                      self.mode, self.n_replicas, rp, hd, self.n_waves, self.dup_items,
-                      self.dtype, st)
+                      self.mode, qlog, self.n_waves, self.dup_items, self.dtype, st)
+        if events is not None:
+            events[1].record(self.stream)
         self._chunk = c
 
     def _prepare(self, ctx):
-        """Global per-item rating counts of every chunk (all ranks) for the count-aware merge."""
+        """Global per-item rating counts of every chunk (all ranks) for the count-aware rules."""
         self.totals = []
         for t in self._totals_local:
             tt = self.torch.from_numpy(t).to(self.dev)
@@ -188,58 +242,103 @@ class MFEngine(ItemSync):
                 ctx.all_reduce_sum(tt)
             self.totals.append(tt)
 
-    def _merge(self, delta_out, apply):
-        st = ctypes.c_void_p(self.stream.cuda_stream)
-        c = getattr(self, "_chunk", 0)
-        count_aware = self.merge_rule == "count"
-        if count_aware and self.totals is None:
+    def _count_rule(self):
+        if self.merge_rule == "count" and self.totals is None:
             self._prepare(None)
-        I = self.n_items
-        tabs = [(self.qb, self.qb_s, self.ldq, self.K)]
-        if self.yj is not None:
-            tabs.append((self.yj, self.yj_s, self.ld, -1))
-        off = 0
-        for tab, snap, ld, bias_col in tabs:
-            # item factors / biases: count-aware; SVD++ implicit factors: count-weighted mean
-            # (every user of a group moves all its y_j together, which saturates fast)
-            rule = (_lib.MF_MERGE_SUM if not count_aware else
-                    _lib.MF_MERGE_COUNT if bias_col >= 0 else _lib.MF_MERGE_MEAN)
-            use_counts = rule != _lib.MF_MERGE_SUM
-            dptr = None
-            if delta_out is not None:
-                dptr = ctypes.c_void_p(delta_out.data_ptr() + off * delta_out.element_size())
-            _lib.call("mf_item_merge", self._ptr(tab), self._ptr(snap), I, ld, self.K, bias_col,
-                      self.n_replicas, rule, self._ptr(self.counts[c]) if use_counts else None,
-                      self._ptr(self.totals[c]) if use_counts else None,
-                      ctypes.byref(self._hyper), self._ptr(self.pu), self.n_users, self.ld,
-                      self._ptr(self.work), dptr, int(apply), self.dtype, st)
-            off += I * ld
+        return self.merge_rule == "count"
+
+    def _log_fold(self, delta_out, apply):
+        """mf_log_reduce + mf_log_apply of the current chunk."""
+        c = getattr(self, "_chunk", 0)
+        perm, pb, ipp, n_pieces = self.logs[c]
+        st = self._st()
+        _lib.call("mf_log_reduce", ctypes.c_void_p(self._qlog_base), self.ldq, self.K + 1,
+                  self._ptr(perm), self._ptr(pb), n_pieces, self._ptr(self.sums), self.dtype, st)
+        count = self._count_rule()
+        _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K, self.K,
+                  self._ptr(self.sums), self._ptr(ipp),
+                  self._ptr(self.totals[c]) if count else None, ctypes.byref(self._hyper),
+                  self._ptr(self.work), float(self.n_users * self.K),
+                  _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM,
+                  None if delta_out is None else self._ptr(delta_out), int(apply), self.dtype, st)
+
+    def _snap_tables(self):
+        """(table, snapshot, ld, bias_col, rule) of the tables merged by snapshot deltas."""
+        count = self._count_rule()
+        tabs = []
+        if self.qb_s is not None:
+            tabs.append((self.qb, self.qb_s, self.ldq, self.K,
+                         _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM))
+        if self.yj_s is not None:
+            # SVD++ implicit factors: count-weighted mean over ranks (every user of a rank moves
+            # all its y_j together, which saturates fast; DESIGN.md)
+            tabs.append((self.yj, self.yj_s, self.ld, -1,
+                         _lib.MF_MERGE_MEAN if count else _lib.MF_MERGE_SUM))
+        return tabs
 
     def _merge_local(self):
-        self._merge(None, True)
+        if self.is_log:
+            self._log_fold(None, True)
+
+    def sync_items(self, ctx):
+        if ctx is None or ctx.world == 1:
+            self._merge_local()
+            return
+        bufs = self._delta_buffer()
+        self._delta_into(bufs)
+        for b in bufs:
+            ctx.all_reduce_sum(b)
+        self._apply(bufs)
 
     def _delta_buffer(self):
+        """[log sums (log mode)] + [one delta per snapshot table] + [<pu^2> partial (log mode)]"""
         if self._delta is None:
-            n = self.n_items * self.ldq
-            if self.yj is not None:
-                n += self.n_items * self.ld
-            self._delta = self.torch.zeros(n, dtype=self.tdt, device=self.dev)
+            z = lambda n: self.torch.zeros(n, dtype=self.tdt, device=self.dev)
+            bufs = []
+            if self.is_log:
+                bufs.append(z(self.n_items * self.ldq))
+            for tab, snap, ld, _, _ in self._snap_tables():
+                bufs.append(z(self.n_items * ld))
+            if self.is_log:
+                bufs.append(self.work)
+            self._delta = bufs
         return self._delta
 
-    def _delta_into(self, buf):
-        self._merge(buf, False)
+    def _delta_into(self, bufs):
+        c = getattr(self, "_chunk", 0)
+        st = self._st()
+        x = 0
+        if self.is_log:
+            self._log_fold(bufs[0], False)
+            x = 1
+        for tab, snap, ld, bias_col, rule in self._snap_tables():
+            use_counts = rule != _lib.MF_MERGE_SUM
+            _lib.call("mf_item_merge", self._ptr(tab), self._ptr(snap), self.n_items, ld, self.K,
+                      bias_col, 1, rule, self._ptr(self.counts[c]) if use_counts else None,
+                      self._ptr(self.totals[c]) if use_counts else None,
+                      ctypes.byref(self._hyper),
+                      ctypes.c_void_p(self.pu.data_ptr() +
+                                      self.u_lo * self.ld * self.pu.element_size()),
+                      max(self.u_hi - self.u_lo, 1), self.ld, self._ptr(self.work),
+                      self._ptr(bufs[x]), 0, self.dtype, st)
+            x += 1
 
-    def _apply(self, buf):
-        st = ctypes.c_void_p(self.stream.cuda_stream)
-        I = self.n_items
-        tabs = [(self.qb, self.qb_s, self.ldq)]
-        if self.yj is not None:
-            tabs.append((self.yj, self.yj_s, self.ld))
-        off = 0
-        for tab, snap, ld in tabs:
-            _lib.call("mf_item_apply", self._ptr(tab), self._ptr(snap), I, ld, self.n_replicas,
-                      ctypes.c_void_p(buf.data_ptr() + off * buf.element_size()), self.dtype, st)
-            off += I * ld
+    def _apply(self, bufs):
+        c = getattr(self, "_chunk", 0)
+        st = self._st()
+        x = 0
+        if self.is_log:  # bufs[-1] is the all-reduced sum of squares of pu
+            count = self._count_rule()
+            _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K, self.K,
+                      self._ptr(bufs[0]), None, self._ptr(self.totals[c]) if count else None,
+                      ctypes.byref(self._hyper), self._ptr(bufs[-1]),
+                      float(self.n_users * self.K),
+                      _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM, None, 1, self.dtype, st)
+            x = 1
+        for tab, snap, ld, _, _ in self._snap_tables():
+            _lib.call("mf_item_apply", self._ptr(tab), self._ptr(snap), self.n_items, ld, 1,
+                      self._ptr(bufs[x]), self.dtype, st)
+            x += 1
 
     def _gather_users(self, ctx):
         """After the last epoch: every rank keeps only its own users' rows, then a SUM
@@ -255,7 +354,7 @@ class MFEngine(ItemSync):
     def user_implicit(self):
         """imp[u] = sum_{j in I_u} yj[j] / sqrt|I_u| on device (SVDpp.estimate :518-520)."""
         imp = self.torch.zeros(self.n_users, self.ld, dtype=self.tdt, device=self.dev)
-        _lib.call("mf_svdpp_user_implicit", ctypes.byref(self._csr), self._ptr(self.yj[0]),
+        _lib.call("mf_svdpp_user_implicit", ctypes.byref(self._csr), self._ptr(self.yj),
                   self.ld, self._ptr(imp), self.K, self.dtype,
                   ctypes.c_void_p(self.stream.cuda_stream))
         return imp
@@ -269,7 +368,7 @@ class MFEngine(ItemSync):
         est = t.zeros(n, dtype=self.tdt, device=self.dev)
         bad = t.zeros(n, dtype=t.int32, device=self.dev)
         _lib.call("mf_predict", n, self._ptr(du), self._ptr(di), self._ptr(self.pu),
-                  self._ptr(self.bu), self.ld, self._ptr(self.qb[0]), self.ldq,
+                  self._ptr(self.bu), self.ld, self._ptr(self.qb), self.ldq,
                   None if imp is None else self._ptr(imp), self.K, int(self.biased),
                   float(global_mean), self._ptr(est), self._ptr(bad), self.dtype,
                   ctypes.c_void_p(self.stream.cuda_stream))

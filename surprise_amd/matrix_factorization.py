@@ -12,9 +12,10 @@ libsurprise_amd.so and raises if the library or the GPU is missing -- there is
 no CPU fallback.  Extra, keyword-only device options:
 
   dtype              "float32" (default) or "float64" arithmetic on the device
-  mode               item-side Hogwild schedule: "replica" (per-XCD item tables merged by a
-                     sum of deltas once per epoch-chunk), "atomic", "plain" or "auto"
-  n_replicas         item replicas in "replica" mode (8 = one per XCD)
+  mode               item-side schedule: "log" (default; item rows read from the chunk-start
+                     snapshot, per-rating item deltas logged and folded in once per
+                     epoch-chunk -- race-free, bit-reproducible), "atomic" (shared rows,
+                     float atomics), "plain" (shared rows, plain stores) or "auto" (= "log")
   chunks_per_epoch   epoch-chunks (item merges / all-reduces per epoch)
   deterministic      one wavefront, users in Trainset order: the reference's exact sequence
   n_waves            wavefronts per launch (0 = fill the GPU)
@@ -33,17 +34,16 @@ from .predictions import Prediction, PredictionImpossible
 from .trainset import Trainset
 from .utils import get_rng
 
-_REPLICA_BUDGET_BYTES = 4 << 30
-
 
 class _MFBase(AlgoBase):
     _algo = "svd"
 
-    def _device_options(self, dtype, mode, n_replicas, chunks_per_epoch, deterministic, n_waves,
+    def _device_options(self, dtype, mode, chunks_per_epoch, deterministic, n_waves,
                         distributed):
+        if mode not in ("auto",) + tuple(_lib.MODES):
+            raise ValueError(f"mode must be 'auto' or one of {sorted(_lib.MODES)}, got {mode!r}")
         self.dtype = dtype
         self.mode = mode
-        self.n_replicas = n_replicas
         self.chunks_per_epoch = chunks_per_epoch
         self.deterministic = deterministic
         self.n_waves = n_waves
@@ -57,12 +57,8 @@ class _MFBase(AlgoBase):
         state["_imp"] = None
         return state
 
-    def _resolve_mode(self, n_items, ld):
-        if self.mode != "auto":
-            return self.mode
-        per = n_items * ld * (2 if self._algo == "svdpp" else 1) * \
-            (8 if self.dtype in ("float64", "f64") else 4)
-        return "replica" if per * self.n_replicas <= _REPLICA_BUDGET_BYTES else "atomic"
+    def _resolve_mode(self):
+        return "log" if self.mode == "auto" else self.mode
 
     def _hyper(self, global_mean):
         return dict(lr_bu=self.lr_bu, lr_bi=self.lr_bi, lr_pu=self.lr_pu, lr_qi=self.lr_qi,
@@ -77,7 +73,7 @@ class _MFBase(AlgoBase):
         return self.fit(ts)
 
     def _run_sgd(self, trainset, with_yj):
-        from .engine import MFEngine, default_ld
+        from .engine import MFEngine
         from .dist import DistContext, shard_users
 
         torch = _lib.require_gpu()
@@ -101,11 +97,9 @@ class _MFBase(AlgoBase):
         if ctx is not None and ctx.world > 1:
             b = shard_users(csr[0], ctx.world)
             users = np.arange(b[ctx.rank], b[ctx.rank + 1])
-        dt = _lib.MF_F64 if self.dtype in ("float64", "f64") else _lib.MF_F32
-        mode = self._resolve_mode(n_items, default_ld(K, dt))
         eng = MFEngine(csr, n_items, K, algo=self._algo, hyper=self._hyper(global_mean),
-                       biased=getattr(self, "biased", True), dtype=self.dtype, mode=mode,
-                       n_replicas=self.n_replicas, n_chunks=self.chunks_per_epoch, users=users,
+                       biased=getattr(self, "biased", True), dtype=self.dtype,
+                       mode=self._resolve_mode(), n_chunks=self.chunks_per_epoch, users=users,
                        deterministic=self.deterministic, user_order=user_order,
                        n_waves=self.n_waves, world=1 if ctx is None else ctx.world)
         eng.set_factors(pu, qi, yj=yj)
@@ -161,14 +155,14 @@ class _MFBase(AlgoBase):
 
 
 class SVD(_MFBase):
-    """Biased MF / PMF trained by Hogwild! SGD on the GPU (matrix_factorization.pyx:19-299)."""
+    """Biased MF / PMF trained by parallel SGD on the GPU (matrix_factorization.pyx:19-299)."""
 
     _algo = "svd"
 
     def __init__(self, n_factors=100, n_epochs=20, biased=True, init_mean=0, init_std_dev=.1,
                  lr_all=.005, reg_all=.02, lr_bu=None, lr_bi=None, lr_pu=None, lr_qi=None,
                  reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, random_state=None,
-                 verbose=False, *, dtype="float32", mode="auto", n_replicas=8,
+                 verbose=False, *, dtype="float32", mode="auto",
                  chunks_per_epoch=1, deterministic=False, n_waves=0, distributed=True):
         self.n_factors = n_factors
         self.n_epochs = n_epochs
@@ -185,8 +179,7 @@ class SVD(_MFBase):
         self.reg_qi = reg_qi if reg_qi is not None else reg_all
         self.random_state = random_state
         self.verbose = verbose
-        self._device_options(dtype, mode, n_replicas, chunks_per_epoch, deterministic, n_waves,
-                             distributed)
+        self._device_options(dtype, mode, chunks_per_epoch, deterministic, n_waves, distributed)
         AlgoBase.__init__(self)
 
     def fit(self, trainset):
@@ -230,7 +223,7 @@ class SVDpp(_MFBase):
                  reg_all=.02, lr_bu=None, lr_bi=None, lr_pu=None, lr_qi=None, lr_yj=None,
                  reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, reg_yj=None,
                  random_state=None, verbose=False, *, dtype="float32", mode="auto",
-                 n_replicas=8, chunks_per_epoch=1, deterministic=False, n_waves=0,
+                 chunks_per_epoch=1, deterministic=False, n_waves=0,
                  distributed=True):
         self.n_factors = n_factors
         self.n_epochs = n_epochs
@@ -248,8 +241,7 @@ class SVDpp(_MFBase):
         self.reg_yj = reg_yj if reg_yj is not None else reg_all
         self.random_state = random_state
         self.verbose = verbose
-        self._device_options(dtype, mode, n_replicas, chunks_per_epoch, deterministic, n_waves,
-                             distributed)
+        self._device_options(dtype, mode, chunks_per_epoch, deterministic, n_waves, distributed)
         AlgoBase.__init__(self)
 
     def fit(self, trainset):

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_without_device(lib):
-    assert lib.mf_version() == 300
+    assert lib.mf_version() == 400
     # argument validation happens before any device call
     rc = lib.mf_item_merge(None, None, 10, 16, 10, 10, 1, 0, None, None, None, None, 0, 16,
                            None, None, 1, 0, None)
@@ -35,13 +35,21 @@ def test_version_and_error_without_device(lib):
     assert b"bad item table" in lib.mf_last_error()
     csr = _lib.MfCsr(0, 0, 0, 0, 0)
     rc = lib.mf_svd_epoch(ctypes.byref(csr), None, 1, None, None, 16, None, 16, 10, 1, None,
-                          0, 1, None, None, 0, 0, 0, None)
+                          0, None, 0, 0, 0, None)
     assert rc == 1001 and b"null csr" in lib.mf_last_error()
+    rc = lib.mf_log_apply(None, 10, 16, 10, 10, None, None, None, None, None, 1.0, 1, None, 1, 0,
+                          None)
+    assert rc == 1001 and b"count-aware rule needs" in lib.mf_last_error()
+    rc = lib.mf_log_reduce(None, 16, 11, None, None, 5, None, 0, None)
+    assert rc == 1001 and b"null argument" in lib.mf_last_error()
+    rc = lib.mf_sumsq(None, 4, 8, 4, None, 0, None)
+    assert rc == 1001
 
 
 def test_header_constants_match_python():
     text = open(_lib.HEADER_PATH).read()
     for name, val in (("MF_F32", 0), ("MF_F64", 1), ("MF_MODE_PLAIN", 0), ("MF_MODE_ATOMIC", 1),
-                      ("MF_MODE_REPLICA", 2), ("MF_MODE_COHERENT", 3), ("MF_MODE_REPLICA_ATOMIC", 4), ("MF_MAX_FACTORS_F32", 512),
+                      ("MF_MODE_LOG", 2), ("MF_MERGE_SUM", 0), ("MF_MERGE_COUNT", 1), ("MF_MERGE_MEAN", 2),
+                      ("MF_MAX_FACTORS_F32", 512),
                       ("MF_MAX_FACTORS_F64", 256)):
         assert "#define %s" % name in text and str(val) in text.split("#define %s" % name)[1].split("\n")[0]

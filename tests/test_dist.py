@@ -75,7 +75,7 @@ class OracleRankEngine(ItemSync):
         self.b[...] = self.b_snap
 
     def _merge_local(self):
-        raise AssertionError("single replica")
+        pass
 
     def _gather_users(self, ctx):
         keep = np.zeros(len(self.bu), bool)

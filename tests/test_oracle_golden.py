@@ -228,3 +228,63 @@ def test_synthetic_fold_matches_reference(golden, tmp_path):
     P, f = run_oracle("SVDpp", dict(n_factors=10, n_epochs=2, random_state=0), row_ptr, items,
                       ratings, ts.n_items, ts.global_mean)
     assert _sha(f["pu"], f["qi"], f["yj"]) == g["svdpp_k10_e2"]["sha_pu_qi_yj"]
+
+
+# ----------------------------------------------------------------------------- delta-log schedule
+
+def run_oracle_log(algo, params, row_ptr, items, ratings, n_items, global_mean, chunk_of_user=None,
+                   n_chunks=1, merge=2):
+    """The GPU's default schedule (MF_MODE_LOG) restated: oracle_*_sgd_deltalog."""
+    P = _Params(algo, params)
+    rng = get_rng(P.random_state)
+    n_users = len(row_ptr) - 1
+    pu, qi, yj = orc.init_factors(rng, n_users, n_items, P.n_factors, P.init_mean,
+                                  P.init_std_dev, with_yj=(algo == "SVDpp"))
+    hp = orc.svd_hyper(P)
+    if algo == "SVD":
+        pu, qi, bu, bi = orc.svd_sgd_deltalog(row_ptr, items, ratings, n_items, P.n_factors,
+                                              P.n_epochs, P.biased, global_mean, hp, pu, qi,
+                                              chunk_of_user, n_chunks, merge)
+        return P, dict(pu=pu, qi=qi, bu=bu, bi=bi)
+    pu, qi, yj, bu, bi = orc.svdpp_sgd_deltalog(row_ptr, items, ratings, n_items, P.n_factors,
+                                                P.n_epochs, global_mean, hp, pu, qi, yj,
+                                                chunk_of_user, n_chunks, merge)
+    return P, dict(pu=pu, qi=qi, yj=yj, bu=bu, bi=bi)
+
+
+@pytest.mark.parametrize("name", ["svd_k20_e5", "svd_k5_e2_unbiased", "svd_k10_e3_hyper"])
+def test_deltalog_one_user_per_chunk_is_the_reference(golden, u1, name):
+    """Pins the delta-log oracle to the reference: one user per chunk = SVD.sgd bit-for-bit."""
+    meta, _ = golden
+    case = meta["cases"][name]
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    P, f = run_oracle_log("SVD", case["params"], row_ptr, items, ratings, ts.n_items,
+                          ts.global_mean, np.arange(ts.n_users), ts.n_users)
+    assert _sha(f["pu"], f["qi"]) == case["sha_pu_qi"]
+    assert _sha(f["bu"], f["bi"]) == case["sha_bu_bi"]
+
+
+def test_deltalog_svdpp_one_user_per_chunk_is_the_affine_form(u1):
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    params = dict(n_factors=6, n_epochs=2, random_state=0)
+    _, a = run_oracle("SVDpp", params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
+                      affine=True)
+    _, b = run_oracle_log("SVDpp", params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
+                          np.arange(ts.n_users), ts.n_users)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+@pytest.mark.parametrize("name", ["svd_k20_e5", "svd_k100_e20", "svd_k10_e3_hyper"])
+def test_deltalog_one_chunk_within_1e3_of_reference(golden, u1, name):
+    """The schedule itself (all users of the epoch against one snapshot, count-aware merge)
+    stays within the north-star tolerance of the sequential reference on u1."""
+    meta, _ = golden
+    case = meta["cases"][name]
+    ts, test = u1
+    row_ptr, items, ratings = ts.csr()
+    P, f = run_oracle_log("SVD", case["params"], row_ptr, items, ratings, ts.n_items,
+                          ts.global_mean)
+    assert abs(_oracle_test_rmse(P, f, "SVD", ts, list(test))[1] - case["rmse"]) < 1e-3

@@ -67,8 +67,8 @@ def main():
     for dname, (ts, test), cases in sets:
         for algo, params in cases:
             ref = oracle_rmse(algo, params, ts, test, affine=(algo == "SVDpp"))
-            for mode, nw, ch in (("replica", 0, 1), ("replica_atomic", 0, 1),
-                                 ("replica_atomic", 0, 4), ("atomic", 0, 1), ("atomic", 256, 1)):
+            for mode, nw, ch in (("log", 0, 1), ("log", 0, 4), ("atomic", 0, 1),
+                                 ("plain", 0, 1)):
                     if nw and nw > ts.n_users:
                         continue
                     klass = SVD if algo == "SVD" else SVDpp
