@@ -77,7 +77,7 @@ def main():
     lr = .007 if svdpp else .005
     hyper = dict(lr_bu=lr, lr_bi=lr, lr_pu=lr, lr_qi=lr, lr_yj=lr, reg_bu=.02, reg_bi=.02,
                  reg_pu=.02, reg_qi=.02, reg_yj=.02, global_mean=float(ts.global_mean))
-    mode = "log" if args.mode == "auto" else args.mode
+    mode = args.mode if args.mode != "auto" else ("atomic" if svdpp else "log")
 
     def make_engine():
         rng = get_rng(0)

@@ -68,7 +68,8 @@ typedef struct mf_csr {
 } mf_csr_t;
 
 /*
- * One epoch-chunk of SVD SGD over the users listed in sched[0..n_sched).
+ * One epoch-chunk of SVD SGD over the users listed in sched[0..n_sched), heaviest first (the
+ * waves of users with more than 1/8 of sched[0]'s ratings get raised issue priority).
  * Replaces the body of SVD.sgd's epoch loop (matrix_factorization.pyx:241-262):
  * each wavefront owns a user (pu[u], bu[u] live in registers, updated in the
  * reference's per-rating order); the item rows qb[i] = [q_i | b_i] are updated per `mode`.

@@ -11,7 +11,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsurprise_amd.so")
+LIB_PATH = os.environ.get("SURPRISE_AMD_LIB") or os.path.join(_HERE, "libsurprise_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "surprise_amd.h")
 
 MF_F32, MF_F64 = 0, 1

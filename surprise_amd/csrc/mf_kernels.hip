@@ -32,7 +32,10 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kBlock = 256;  // 4 waves per workgroup
-constexpr int kPF = 8;       // item rows gathered ahead of use
+#ifndef MF_PF
+#define MF_PF 8
+#endif
+constexpr int kPF = MF_PF;   // item rows gathered ahead of use
 
 thread_local char g_err[256] = "";
 
@@ -274,12 +277,19 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
 
     const rsrc_t q_rs = make_rsrc(qb, q_oob);
     const rsrc_t y_rs = PP ? make_rsrc(yj, y_oob) : q_rs;
+    // sched lists users heaviest first: its head's degree scales the priority levels
+    const int prio_len = (int)(row_ptr[sched[0] + 1] - row_ptr[sched[0]]);
 
     // one user block: the reference's per-rating order for user u
     auto do_user = [&](const int u) {
         const int64_t s = row_ptr[u];
         const int n = (int)(row_ptr[u + 1] - s);  // |I_u| (< 2^31)
         if (n <= 0) return;
+        // The epoch ends when the longest user chain ends: the waves of the heaviest users
+        // take issue priority over the light users sharing their SIMD.
+        if (n * 2 > prio_len) __builtin_amdgcn_s_setprio(3);
+        else if (n * 4 > prio_len) __builtin_amdgcn_s_setprio(2);
+        else if (n * 8 > prio_len) __builtin_amdgcn_s_setprio(1);
         // kLog: this user's log segment, rows s .. s+n-1 (n * qrow < 2^30 bytes)
         const rsrc_t l_rs = LOG ? make_rsrc(qlog + s * ldq, (uint32_t)n * qrow) : q_rs;
         // the user's (item, rating) stream, read with scalar loads (uniform addresses ->
@@ -409,6 +419,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
 #pragma unroll
         for (int v = 0; v < V; ++v) Buf<T>::template st<0>(p_rs, cu[v], p[v]);
         Buf<T>::template st<0>(b_rs, lane == 0 ? 0u : (uint32_t)sizeof(T), bu_u);
+        __builtin_amdgcn_s_setprio(0);
 
         // SVD++ (3): y_j <- A y_j + c for every j in I_u
         if (PP) {
@@ -456,12 +467,13 @@ __global__ __launch_bounds__(kBlock) void sumsq_kernel(const T *__restrict__ x, 
 {
     __shared__ double part[kBlock / kWave];
     double acc = 0;
-    const int64_t total = n_rows * K;
-    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < total;
-         e += (int64_t)gridDim.x * kBlock) {
-        const double v = (double)x[(e / K) * ld + e % K];
-        acc += v * v;
-    }
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    for (int64_t r = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave; r < n_rows; r += n_waves)
+        for (int c = lane; c < K; c += kWave) {
+            const double v = (double)x[r * ld + c];
+            acc += v * v;
+        }
     acc = wave_sum(acc);
     if ((threadIdx.x & (kWave - 1)) == 0) part[threadIdx.x / kWave] = acc;
     __syncthreads();
@@ -594,10 +606,20 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
         T acc[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) acc[v] = T(0);
-        for (int pc = p0; pc < p1; ++pc)
+        constexpr int kU = 8;  // independent loads in flight
+        for (int pc = p0; pc < p1; pc += kU) {
+            T g[kU][V];
 #pragma unroll
-            for (int v = 0; v < V; ++v)
-                if (lane + kWave * v < ld) acc[v] += sums[(int64_t)pc * ld + lane + kWave * v];
+            for (int a = 0; a < kU; ++a)
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    g[a][v] = (pc + a < p1 && lane + kWave * v < ld)
+                                  ? sums[(int64_t)(pc + a) * ld + lane + kWave * v] : T(0);
+#pragma unroll
+            for (int a = 0; a < kU; ++a)
+#pragma unroll
+                for (int v = 0; v < V; ++v) acc[v] += g[a][v];
+        }
         const double N = totals ? (double)totals[i] : 0.0;
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -846,7 +868,7 @@ int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *
     if (!out || n_rows < 0 || n_cols < 0 || ld < n_cols) return set_err(MF_E_ARG, "bad argument");
     if (n_rows == 0 || n_cols == 0) return 0;
     if (!x) return set_err(MF_E_ARG, "null x");
-    const int g = elementwise_grid(n_rows * n_cols);
+    const int g = grid_for_waves(n_rows < 1024 ? n_rows : 1024);  // few blocks: one atomic each
     hipStream_t st = (hipStream_t)stream;
     if (dtype == MF_F32)
         hipLaunchKernelGGL(sumsq_kernel<float>, dim3(g), dim3(kBlock), 0, st, (const float *)x,
@@ -940,7 +962,7 @@ int mf_item_merge(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
         den = (double)n_users * n_factors;
         hipError_t e = hipMemsetAsync(work, 0, sizeof(double), st);
         if (e != hipSuccess) return set_err((int)e, "hipMemsetAsync(work)");
-        const int g = elementwise_grid((int64_t)n_users * n_factors);
+        const int g = grid_for_waves(n_users < 1024 ? n_users : 1024);
         if (dtype == MF_F32)
             hipLaunchKernelGGL(sumsq_kernel<float>, dim3(g), dim3(kBlock), 0, st, (const float *)pu,
                                (int64_t)n_users, n_factors, ldu, (double *)work);

@@ -1,0 +1,50 @@
+"""Probe: epoch-kernel time for subsets of the ML-1M-shape schedule (is the epoch bound by the
+heaviest users' dependent chains or by throughput?).  Prints one line per subset."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+from surprise_amd import Dataset, synthetic  # noqa: E402
+from surprise_amd.engine import MFEngine  # noqa: E402
+from surprise_amd.model_selection import KFold  # noqa: E402
+
+mode = sys.argv[1] if len(sys.argv) > 1 else "log"
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+u, i, r = synthetic.shape("ml-1m")
+ts, _ = next(KFold(5, random_state=0).split(Dataset.load_from_arrays(u, i, r)))
+rp, it, rt = ts.csr()
+hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02, reg_pu=.02,
+             reg_qi=.02, global_mean=float(ts.global_mean))
+eng = MFEngine((rp, it, rt), ts.n_items, K, hyper=hyper, mode=mode)
+rng = np.random.RandomState(0)
+eng.set_factors(rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K)))
+full = eng.sched[0].clone()
+deg = np.diff(rp)
+order = full.cpu().numpy()
+
+
+def t_sched(s, n_waves=0, reps=10):
+    eng.sched[0] = torch.from_numpy(np.ascontiguousarray(s, np.int32)).cuda()
+    eng.n_waves = n_waves
+    ts_ = []
+    for _ in range(reps + 2):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        eng.run_chunk(0, events=(a, b))
+        torch.cuda.synchronize()
+        ts_.append(a.elapsed_time(b))
+    return float(np.median(ts_[2:])) * 1e3
+
+
+print("mode", mode, "K", K, "max deg", deg.max(), "ratings", deg.sum())
+for name, s, nw in [("full", order, 0), ("top1", order[:1], 0), ("top16", order[:16], 0),
+                    ("top256", order[:256], 0), ("top1024", order[:1024], 0),
+                    ("drop-top64", order[64:], 0), ("drop-top256", order[256:], 0),
+                    ("full-2048waves", order, 2048), ("full-8192waves", order, 8192)]:
+    us = t_sched(s, nw)
+    n = int(deg[s].sum())
+    print("%-16s users %5d ratings %7d max %4d  %8.1f us  %.1f ns/rating(max chain)  %.2f Gupd/s"
+          % (name, len(s), n, deg[s].max(), us, us * 1e3 / deg[s].max(), n / us / 1e3), flush=True)
