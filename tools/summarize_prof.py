@@ -52,6 +52,24 @@ fetch = pmc("fetch", "FETCH_SIZE")
 write = pmc("write", "WRITE_SIZE")
 summary["FETCH_SIZE_kib"] = fetch
 summary["WRITE_SIZE_kib"] = write
+# HBM-side bytes per epoch-kernel launch, corrected as MI355X_MICROARCH.md (HBM) prescribes:
+# FETCH_SIZE tallies 128-B read requests at 64 B on gfx950 -> x2; WRITE_SIZE is exact.
+# Calibrated on our own access pattern: log_reduce_kernel reads a known 404 B/rating from
+# 448-B-strided rows (4 x 128-B lines each), and 2 x FETCH_SIZE matches that line count.
+bench_line = summary.get("bench_line_under_profiler")
+if fetch and write and bench_line and "mf_epoch_kernel" in fetch and "mf_epoch_kernel" in write:
+    fb = 2 * fetch["mf_epoch_kernel"]["mean_per_dispatch"] * 1024
+    wb = write["mf_epoch_kernel"]["mean_per_dispatch"] * 1024
+    cfg = bench_line["config"]
+    n_up = bench_line["roofline"]["updates_per_launch"]
+    traffic = {"kernel": "mf_epoch_kernel", "bytes_per_launch": fb + wb, "read_bytes": fb,
+               "write_bytes": wb, "bytes_per_update": (fb + wb) / n_up,
+               "algorithmic_bytes_per_update": bench_line["roofline"]["algorithmic_bytes_per_update"],
+               "source": "profiles/%s_summary.json (2 x FETCH_SIZE + WRITE_SIZE, separate passes)" % tag,
+               "workload": cfg["workload"]}
+    summary["traffic"] = traffic
+    with open(os.path.join(prof, "traffic_%s_k%d.json" % (cfg["algo"], cfg["n_factors"])), "w") as f:
+        json.dump(traffic, f, indent=1)
 with open(os.path.join(prof, "%s_summary.json" % tag), "w") as f:
     json.dump(summary, f, indent=1)
 print(json.dumps(summary, indent=1)[:4000])
