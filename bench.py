@@ -97,25 +97,26 @@ def main():
             eng.sync_items(ctx)
     torch.cuda.synchronize()
 
-    evs, mevs = [], []
+    recs = []
     if ctx is not None:
         ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         for c in range(eng.n_chunks):
-            a, b, m = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-            eng.run_chunk(c, events=(a, b))  # a / b bracket the epoch kernel on its stream
+            ev = {k: torch.cuda.Event(enable_timing=True) for k in ("start", "end", "step_end")}
+            eng.run_chunk(c, events=ev)  # HIP events on the streams the kernels run on
             eng.sync_items(ctx)
-            m.record(stream)
-            evs.append((a, b))
-            mevs.append((b, m))
+            ev["step_end"].record(stream)
+            recs.append((c, ev))
     torch.cuda.synchronize()
     if ctx is not None:
         ctx.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
-    merge_ms = [a.elapsed_time(b) for a, b in mevs]
+    # per chunk: the epoch kernel, and the rest of the step (log reduction + fold, or the
+    # multi-rank merge + all-reduce)
+    kern_ms = [ev["start"].elapsed_time(ev["end"]) for _, ev in recs]
+    merge_ms = [ev["end"].elapsed_time(ev["step_end"]) for _, ev in recs]
     if ctx is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -158,7 +159,8 @@ def main():
             traffic = json.load(f).get("bytes_per_launch")
     result["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                          "kernel": "%s_epoch_kernel" % args.algo, "launch_ms": launch_ms,
+                          "kernel": "mf_epoch_kernel (%s, mode=%s)" % (args.algo, mode),
+                          "launch_ms": launch_ms,
                           "algorithmic_bytes_per_update": K_bytes,
                           "updates_per_launch": per_launch_updates,
                           "merge_ms_per_chunk": float(np.mean(merge_ms))}

@@ -76,18 +76,19 @@ typedef struct mf_csr {
  *   pu [n_users][ldu], bu [n_users], qb [n_items][ldq]
  *   biased    : 0 reproduces SVD(biased=False) (hp->global_mean must then be 0)
  *   mode      : MF_MODE_*
- *   qlog      : MF_MODE_LOG: device [nnz][ldq] delta log, row k = rating k of the CSR (columns
- *               0..n_factors written, the rest untouched); each user's segment must be < 2^30
+ *   qlog      : MF_MODE_LOG: device [nnz][ldq] delta log, row k = rating k of the CSR (whole rows
+ *               written, zero padding included); each user's segment must be < 2^30
  *               bytes (|I_u| * ldq * sizeof(dtype)).  Other modes: NULL.
  *   n_waves   : wavefronts to launch (<= 0: library default = fill the GPU);
  *               1 with MF_MODE_PLAIN gives the exact sequential reference order when
  *               sched = 0..n_users-1.
- *   dup_items : non-zero if some user lists the same item twice (enables in-register forwarding
- *               in MF_MODE_PLAIN / MF_MODE_ATOMIC; MF_MODE_LOG reads the snapshot row).
+ *   flags     : MF_EPOCH_DUP_ITEMS if some user lists the same item twice (in-register
+ *               forwarding in MF_MODE_PLAIN / MF_MODE_ATOMIC; MF_MODE_LOG reads the snapshot row);
  */
+#define MF_EPOCH_DUP_ITEMS   1
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves, int32_t dup_items,
+                 const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves, int32_t flags,
                  int32_t dtype, void *stream);
 
 /*
@@ -100,7 +101,7 @@ int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
                    const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves,
-                   int32_t dup_items, int32_t dtype, void *stream);
+                   int32_t flags, int32_t dtype, void *stream);
 
 /* out[0] += sum of x[r][c]^2 over r < n_rows, c < n_cols (x is [n_rows][ld]; out is one device
  * double).  The <pu^2> statistic of the count-aware merge rules. */
@@ -110,7 +111,7 @@ int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *
 /*
  * Delta-log merge, step 1 (MF_MODE_LOG): sums[p][c] = sum_{x in [piece_beg[p], piece_beg[p+1])}
  * qlog[perm[x]][c] for c < n_cols (zero for n_cols <= c < ld), summed in x order.  perm lists the
- * chunk's log rows grouped by item; an item's rows are cut into consecutive pieces.
+ * chunk's log rows grouped by item; an item's rows are cut into consecutive pieces of 1..64 rows.
  */
 int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *perm,
                   const int32_t *piece_beg, int64_t n_pieces, void *sums, int32_t dtype,

@@ -18,6 +18,7 @@ MF_F32, MF_F64 = 0, 1
 MF_MODE_PLAIN, MF_MODE_ATOMIC, MF_MODE_LOG = 0, 1, 2
 MODES = {"plain": MF_MODE_PLAIN, "atomic": MF_MODE_ATOMIC, "log": MF_MODE_LOG}
 MF_MERGE_SUM, MF_MERGE_COUNT, MF_MERGE_MEAN = 0, 1, 2
+MF_EPOCH_DUP_ITEMS = 1
 MAX_FACTORS = {MF_F32: 512, MF_F64: 256}
 
 

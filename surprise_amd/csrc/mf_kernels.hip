@@ -37,6 +37,7 @@ constexpr int kBlock = 256;  // 4 waves per workgroup
 #endif
 constexpr int kPF = MF_PF;   // item rows gathered ahead of use
 
+
 thread_local char g_err[256] = "";
 
 int set_err(int code, const char *msg) {
@@ -216,6 +217,103 @@ enum { kPlain = MF_MODE_PLAIN, kAtomic = MF_MODE_ATOMIC, kLog = MF_MODE_LOG };
 // log segment, which is < 2^30 bytes) and is dropped by the range check.
 constexpr uint32_t kLogOob = 0x40000000u;
 
+// ---- 8-byte lane elements.  A lane owns 8 consecutive bytes of a row per group v: two fp32
+// columns (a float2: packed v_pk_fma_f32 / v_pk_mul_f32 math, one dwordx2 load per row) or one
+// fp64 column.  Lane l, group v holds columns (l + 64 v) * W .. + W-1; a row of ld elements
+// spans G = ceil(ld * sizeof(T) / 512) groups.
+template <typename T>
+struct Lane8;
+
+template <>
+struct Lane8<float> {
+    typedef float vec __attribute__((ext_vector_type(2)));
+    static constexpr int W = 2;
+    __device__ static __forceinline__ vec splat(float x) { return vec{x, x}; }
+    __device__ static __forceinline__ float hsum(vec v) { return v.x + v.y; }
+    __device__ static __forceinline__ float get(vec v, int e) { return e ? v.y : v.x; }
+    __device__ static __forceinline__ void set(vec &v, int e, float x) {
+        if (e) v.y = x; else v.x = x;
+    }
+    template <int AUX>
+    __device__ static __forceinline__ vec ld(rsrc_t r, uint32_t off) {
+        return __builtin_bit_cast(vec, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX));
+    }
+    template <int AUX>
+    __device__ static __forceinline__ void st(rsrc_t r, uint32_t off, vec v) {
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v), r,
+            off, 0, AUX);
+    }
+    __device__ static __forceinline__ void add(rsrc_t r, void *, uint32_t, uint32_t off, vec v) {
+        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v.x, r, off, 0, 0);  // memory-side adds
+        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v.y, r, off + 4, 0, 0);
+    }
+    // voffset + soffset forms (soffset: a wave-uniform row offset in an SGPR)
+    template <int AUX>
+    __device__ static __forceinline__ vec lds(rsrc_t r, uint32_t voff, uint32_t soff) {
+        return __builtin_bit_cast(vec, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, AUX));
+    }
+    template <int AUX>
+    __device__ static __forceinline__ void sts(rsrc_t r, uint32_t voff, uint32_t soff, vec v) {
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v), r,
+            voff, soff, AUX);
+    }
+    __device__ static __forceinline__ void adds(rsrc_t r, void *, uint32_t, uint32_t voff,
+                                                uint32_t soff, vec v) {
+        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v.x, r, voff, soff, 0);
+        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v.y, r, voff + 4, soff, 0);
+    }
+};
+
+template <>
+struct Lane8<double> {
+    typedef double vec;
+    static constexpr int W = 1;
+    __device__ static __forceinline__ vec splat(double x) { return x; }
+    __device__ static __forceinline__ double hsum(vec v) { return v; }
+    __device__ static __forceinline__ double get(vec v, int) { return v; }
+    __device__ static __forceinline__ void set(vec &v, int, double x) { v = x; }
+    template <int AUX>
+    __device__ static __forceinline__ vec ld(rsrc_t r, uint32_t off) { return Buf<double>::ld<AUX>(r, off); }
+    template <int AUX>
+    __device__ static __forceinline__ void st(rsrc_t r, uint32_t off, vec v) { Buf<double>::st<AUX>(r, off, v); }
+    __device__ static __forceinline__ void add(rsrc_t r, void *base, uint32_t bytes, uint32_t off,
+                                               vec v) {
+        Buf<double>::add(r, (double *)base, bytes, off, v);
+    }
+    template <int AUX>
+    __device__ static __forceinline__ vec lds(rsrc_t r, uint32_t voff, uint32_t soff) {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, AUX));
+    }
+    template <int AUX>
+    __device__ static __forceinline__ void sts(rsrc_t r, uint32_t voff, uint32_t soff, vec v) {
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v), r,
+            voff, soff, AUX);
+    }
+    __device__ static __forceinline__ void adds(rsrc_t r, void *base, uint32_t bytes, uint32_t voff,
+                                                uint32_t soff, vec v) {
+        Buf<double>::add(r, (double *)base, bytes, voff + soff, v);
+    }
+};
+
+// Full 64-lane sum returned as a wave-uniform value (scalar register): 4 DPP butterfly steps
+// leave every lane with its 16-lane row sum, two DPP row broadcasts fold rows 0..3 into lane 63,
+// one v_readlane.  (gfx9 DPP: row_bcast:15 = 0x142, row_bcast:31 = 0x143.)
+__device__ __forceinline__ float wave_sum_u(float v) {
+    v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp<0x141>(v);  // row_half_mirror
+    v += dpp<0x140>(v);  // row_mirror
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142,
+                                                               0xA, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x143,
+                                                               0xC, 0xF, false));
+    return readlane(v, 63);
+}
+__device__ __forceinline__ double wave_sum_u(double v) { return readlane(wave_sum(v), 0); }
+
 // Item table row (ldq elements): [q_0 .. q_{K-1} | b_i | 0 ...].  The user row is extended in
 // registers with a constant 1 in column K, so <q_aug, p_aug> = <q_i, p_u> + b_i and the item
 // bias rides in the same gather / scatter as the item factors; its update
@@ -228,13 +326,20 @@ constexpr uint32_t kLogOob = 0x40000000u;
 //           of the delta log (k = the rating's CSR position); mf_log_reduce / mf_log_apply fold
 //           the log into the table afterwards.  Race-free and independent of wave scheduling.
 // SVD++'s y_j rows are shared state in every mode (kPlain: stores, kAtomic / kLog: float adds).
-template <typename T, int V, int MODE, bool PP, bool DUPS>
-__global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
+//
+// Per rating the dependent chain is: p -> <q, p> partial (packed mul) -> wave sum -> err ->
+// (lr err) -> p' = (lr err) q + (1 - lr reg) p (one packed FMA); everything that does not need
+// err ((1 - lr reg) p, -lr reg q, the next row's address) is computed off that chain.
+template <typename T, int G, int MODE, bool PP, bool DUPS, int kPF>
+__device__ __forceinline__ void epoch_body(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, int K,
     int biased, Hyper<T> hp, int n_items, int64_t n_waves_req)
 {
+    using L = Lane8<T>;
+    using vec = typename L::vec;
+    constexpr int W = L::W;
     const int lane = threadIdx.x & (kWave - 1);
     // wave id through readfirstlane: the compiler then knows it (and every user index, CSR
     // bound and loop counter derived from it) is wave-uniform -> SGPRs, scalar loads, scalar
@@ -255,24 +360,38 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
     constexpr int kLdAux = MODE == kAtomic ? kSc1 : 0;
     constexpr int kYLdAux = MODE == kPlain ? 0 : kSc1;
 
-    // per-lane column constants (column c = lane + 64 v)
-    uint32_t cq[V], cu[V], cl[V];
-    T one[V], lrq[V], regq[V], lrp[V], regp[V], lry[V];
+    // per-lane constants of group v (byte offsets of the lane's 8 bytes; masked lanes get an
+    // offset past the table / log so their loads read 0 and their stores are dropped)
+    uint32_t cq[G], cu[G], cl[G];
+    vec one[G], lrq[G], nrq[G], lrp[G], ap[G], lry[G];
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-        const int c = lane + kWave * v;
-        cq[v] = c < ldq ? (uint32_t)c * sizeof(T) : q_oob;
-        cl[v] = c <= K ? (uint32_t)c * sizeof(T) : kLogOob;
-        cu[v] = c < ldu ? (uint32_t)c * sizeof(T) : (PP ? y_oob : yrow);  // >= pu record too
-        const bool fac = c < K, bias = biased && c == K;
-        one[v] = bias ? T(1) : T(0);
-        lrq[v] = fac ? hp.lr_qi : (bias ? hp.lr_bi : T(0));
-        regq[v] = fac ? hp.reg_qi : (bias ? hp.reg_bi : T(0));
-        lrp[v] = fac ? hp.lr_pu : T(0);
-        regp[v] = fac ? hp.reg_pu : T(0);
-        lry[v] = fac ? hp.lr_yj : T(0);
+    for (int v = 0; v < G; ++v) {
+        const int c0 = (lane + kWave * v) * W;  // first column of this lane's 8 bytes
+        const uint32_t b = (uint32_t)c0 * sizeof(T);
+        cq[v] = c0 < ldq ? b : q_oob;
+        cu[v] = c0 < ldu ? b : (PP ? y_oob : yrow);  // >= pu record too
+        // log rows are stored whole, zero padding included: a user's log segment is then one
+        // contiguous, fully written byte range (partially written lines cost a read-modify-write
+        // at the memory side: measured 2 TB/s effective with the padding left unwritten)
+        cl[v] = c0 < ldq ? b : kLogOob;
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            const int c = c0 + e;
+            const bool fac = c < K, bias = biased && c == K;
+            const T lq = fac ? hp.lr_qi : (bias ? hp.lr_bi : T(0));
+            const T rq = fac ? hp.reg_qi : (bias ? hp.reg_bi : T(0));
+            const T lp = fac ? hp.lr_pu : T(0);
+            const T rp = fac ? hp.reg_pu : T(0);
+            L::set(one[v], e, bias ? T(1) : T(0));
+            L::set(lrq[v], e, lq);
+            L::set(nrq[v], e, -lq * rq);      // d = (lr err) pe - lr reg q
+            L::set(lrp[v], e, lp);
+            L::set(ap[v], e, T(1) - lp * rp);  // p' = (lr err) q + (1 - lr reg) p
+            L::set(lry[v], e, fac ? hp.lr_yj : T(0));
+        }
     }
     const T lr_bu = biased ? hp.lr_bu : T(0);
+    const T abu = T(1) - lr_bu * hp.reg_bu;
     const T decay = T(1) - hp.lr_yj * hp.reg_yj;
 
     const rsrc_t q_rs = make_rsrc(qb, q_oob);
@@ -292,45 +411,43 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
         else if (n * 8 > prio_len) __builtin_amdgcn_s_setprio(1);
         // kLog: this user's log segment, rows s .. s+n-1 (n * qrow < 2^30 bytes)
         const rsrc_t l_rs = LOG ? make_rsrc(qlog + s * ldq, (uint32_t)n * qrow) : q_rs;
-        // the user's (item, rating) stream, read with scalar loads (uniform addresses ->
-        // s_load, counted by lgkmcnt, out of the vector-memory queue the row gathers use)
         const int32_t *__restrict__ it = items + s;
         const T *__restrict__ rt = ratings + s;
         const rsrc_t p_rs = make_rsrc(pu + (int64_t)u * ldu, (uint32_t)K * sizeof(T));
         const rsrc_t b_rs = make_rsrc(bu + u, sizeof(T));
 
-        T p[V];
+        vec p[G];
 #pragma unroll
-        for (int v = 0; v < V; ++v) p[v] = Buf<T>::template ld<0>(p_rs, cu[v]) + one[v];
+        for (int v = 0; v < G; ++v) p[v] = L::template ld<0>(p_rs, cu[v]) + one[v];
         T bu_u = Buf<T>::template ld<0>(b_rs, 0);
         const T sqrt_n = sqrt(T(n));  // mf.pyx:470
 
         // SVD++ (1): u_impl = sum_{j in I_u} y_j / sqrt|I_u|  (mf.pyx:473-476, per-term division)
-        T imp[V], cacc[V];
+        vec imp[G], cacc[G];
 #pragma unroll
-        for (int v = 0; v < V; ++v) imp[v] = cacc[v] = T(0);
+        for (int v = 0; v < G; ++v) imp[v] = cacc[v] = L::splat(T(0));
         if (PP) {
             for (int x = 0; x < n; x += 8) {
-                T g[8][V];
+                vec g[8][G];
 #pragma unroll
                 for (int a = 0; a < 8; ++a) {
                     const int j = x + a < n ? x + a : n - 1;
                     const uint32_t ro = (uint32_t)it[j] * yrow + (x + a < n ? 0u : y_oob);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kYLdAux>(y_rs, ro + cu[v]);
+                    for (int v = 0; v < G; ++v) g[a][v] = L::template ld<kYLdAux>(y_rs, ro + cu[v]);
                 }
 #pragma unroll
                 for (int a = 0; a < 8; ++a)
 #pragma unroll
-                    for (int v = 0; v < V; ++v) imp[v] += g[a][v] / sqrt_n;
+                    for (int v = 0; v < G; ++v) imp[v] += g[a][v] / sqrt_n;
             }
         }
         T A = T(1);
 
         // software pipeline: slot d holds the gathered row of rating j0 + d.  The item ids and
-        // ratings of a group travel one group ahead in VGPR lanes (lane l < kPF holds entry l),
-        // are loaded once per group by two unconditional vector loads, and are read with
-        // v_readlane when the group's rows are gathered.
+        // ratings of a group travel one group ahead in VGPR lanes (lane l < kPF holds entry l,
+        // clamped to the user's last rating, so every gathered row is a real row), are loaded
+        // once per group by two unconditional vector loads, and are read with v_readlane.
         auto grp_load = [&](int j0, int &gi, T &gr) {
             int j = j0 + (lane & (kPF - 1));
             j = j < n ? j : n - 1;
@@ -340,107 +457,153 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
         int gi_b, gi_n;
         T gr_b, gr_n;
         uint32_t s_off[kPF];
-        T s_r[kPF], s_q[kPF][V];
+        T s_r[kPF];
+        vec s_q[kPF][G];
         {
             int gi_a;
             T gr_a;
             grp_load(0, gi_a, gr_a);
             grp_load(kPF, gi_b, gr_b);
+            // both groups resolved here (group a is needed right away anyway): otherwise the
+            // loop would inherit "group b may be in flight" from this path and wait for it with
+            // a conservative, near-empty vmcnt at every iteration
+            asm volatile("" ::"v"(gi_a), "v"(gr_a), "v"(gi_b), "v"(gr_b));  // (no sinking)
             __builtin_amdgcn_sched_barrier(0);
-            // (an out-of-range rating adds q_oob to a real row offset instead of selecting it,
-            // so the item id is used unconditionally and no branch is generated)
 #pragma unroll
             for (int d = 0; d < kPF; ++d) {
-                s_off[d] = (uint32_t)readlane(gi_a, d) * qrow + (d < n ? 0u : q_oob);
+                s_off[d] = (uint32_t)readlane(gi_a, d) * qrow;
                 s_r[d] = readlane(gr_a, d);
 #pragma unroll
-                for (int v = 0; v < V; ++v) s_q[d][v] = Buf<T>::template ld<kLdAux>(q_rs, s_off[d] + cq[v]);
+                for (int v = 0; v < G; ++v) s_q[d][v] = L::template lds<kLdAux>(q_rs, cq[v], s_off[d]);
                 __builtin_amdgcn_sched_barrier(0);  // keep slot order: slot 0's row lands first
             }
         }
-        for (int j0 = 0; j0 < n; j0 += kPF) {
-            grp_load(j0 + 2 * kPF, gi_n, gr_n);
+        // c = mu + bu is carried instead of bu: err = (r - c) - dot, and
+        // c' = mu + bu' = lr_bu err + [(1 - lr_bu reg_bu) c + mu lr_bu reg_bu], the bracket off
+        // the chain (bu = c - mu is stored at the end)
+        T cb = hp.gm + bu_u;
+        const T kb = hp.gm * (T(1) - abu);
+        T cb_0 = abu * cb + kb;
+
+        // One rating in slot d.  FULL: every slot of the group is a real rating and the slot is
+        // refilled with rating j0 + kPF + d; tail group: slots past n run masked, no refill.
+        auto step = [&](auto full_c, const int j0, const int d) {
+            constexpr bool FULL = decltype(full_c)::value;
+            const bool valid = FULL || j0 + d < n;
+            vec pe[G], part2 = L::splat(T(0));
 #pragma unroll
-            for (int d = 0; d < kPF; ++d) {
-                const bool valid = j0 + d < n;  // tail slots run masked (OOB row, no state change)
-                T part = T(0);
+            for (int v = 0; v < G; ++v) {
+                pe[v] = PP ? p[v] + imp[v] : p[v];
+                part2 += s_q[d][v] * pe[v];
+            }
+            // everything that does not need err: fills the reduction's DPP wait states
+            vec dq_e[G], dq_0[G], dp_e[G], dp_0[G], dy_e[G];
 #pragma unroll
-                for (int v = 0; v < V; ++v) part += s_q[d][v] * (PP ? p[v] + imp[v] : p[v]);
-                const T dot = wave_sum(part);                 // <q_i, p_u (+imp)> + b_i
-                const T err = s_r[d] - (hp.gm + bu_u + dot);  // mf.pyx:250 / :483
-                T qd[V], qn[V];
+            for (int v = 0; v < G; ++v) {
+                const vec q = s_q[d][v];
+                dq_e[v] = lrq[v] * pe[v];  // d  = err (lr pe) + (-lr reg q)
+                dq_0[v] = nrq[v] * q;
+                dp_e[v] = lrp[v] * q;      // p' = err (lr q) + (1 - lr reg) p
+                dp_0[v] = ap[v] * p[v];
+                if (PP) dy_e[v] = lry[v] * q;
+            }
+            const T dot = wave_sum_u(L::hsum(part2));  // <q_i, p_u (+imp)> + b_i
+            const T e0 = s_r[d] - cb;
+            const T err = e0 - dot;                      // mf.pyx:250 / :483
+            vec qd[G];
 #pragma unroll
-                for (int v = 0; v < V; ++v) {  // mf.pyx:258-262 / :490-498, old puf and qif
-                    const T q = s_q[d][v], pv = p[v];
-                    const T pe = PP ? pv + imp[v] : pv;
-                    qd[v] = lrq[v] * (err * pe - regq[v] * q);
-                    qn[v] = q + qd[v];
-                    const T pn = pv + lrp[v] * (err * q - regp[v] * pv);
-                    p[v] = valid ? pn : pv;
-                    if (PP) {
-                        const T cn = decay * cacc[v] + lry[v] * (err * q / sqrt_n);
-                        const T in = decay * imp[v] + lry[v] * err * q;
-                        cacc[v] = valid ? cn : cacc[v];
-                        imp[v] = valid ? in : imp[v];
-                    }
-                }
-                const T bun = bu_u + lr_bu * (err - hp.reg_bu * bu_u);  // mf.pyx:253-254
-                bu_u = valid ? bun : bu_u;
-                if (PP) A = valid ? A * decay : A;
-                const uint32_t off = s_off[d];
-#pragma unroll
-                for (int v = 0; v < V; ++v) {
-                    if (LOG)  // (a tail slot's row offset n * qrow and beyond is dropped)
-                        Buf<T>::template st<0>(l_rs, (uint32_t)(j0 + d) * qrow + cl[v], qd[v]);
-                    else if (ATOM)
-                        Buf<T>::add(q_rs, qb, q_oob, off + cq[v], qd[v]);
-                    else
-                        Buf<T>::template st<0>(q_rs, off + cq[v], qn[v]);
-                }
-                // keep the next gather below the last use of the slot's old row: hoisting it would
-                // need a second register set and a copy (and a wait) at the loop latch
-                __builtin_amdgcn_sched_barrier(0);
-                s_off[d] = (uint32_t)readlane(gi_b, d) * qrow + (j0 + kPF + d < n ? 0u : q_oob);
-                s_r[d] = readlane(gr_b, d);
-#pragma unroll
-                for (int v = 0; v < V; ++v)
-                    s_q[d][v] = Buf<T>::template ld<kLdAux>(q_rs, s_off[d] + cq[v]);
-                if (DUPS && off < q_oob) {  // same item again within the window: forward the row
-#pragma unroll
-                    for (int dd = 0; dd < kPF; ++dd)
-                        if (s_off[dd] == off)
-#pragma unroll
-                            for (int v = 0; v < V; ++v) s_q[dd][v] = qn[v];
+            for (int v = 0; v < G; ++v) {  // mf.pyx:258-262 / :490-498, old puf and qif
+                qd[v] = err * dq_e[v] + dq_0[v];
+                const vec pn = err * dp_e[v] + dp_0[v];
+                p[v] = valid ? pn : p[v];
+                if (PP) {
+                    const vec cn = decay * cacc[v] + err * (dy_e[v] / sqrt_n);
+                    const vec in = decay * imp[v] + err * dy_e[v];
+                    cacc[v] = valid ? cn : cacc[v];
+                    imp[v] = valid ? in : imp[v];
                 }
             }
+            const T cbn = lr_bu * err + cb_0;  // mf.pyx:253-254
+            cb = valid ? cbn : cb;
+            cb_0 = abu * cb + kb;
+            if (PP) A = valid ? A * decay : A;
+            const uint32_t off = s_off[d];
+            vec stv[G];  // the row after this rating (kPlain stores it; DUPS forwards it)
+#pragma unroll
+            for (int v = 0; v < G; ++v) stv[v] = s_q[d][v] + qd[v];
+            if (FULL) {  // real rows only: the row offset rides in soffset, no address math
+#pragma unroll
+                for (int v = 0; v < G; ++v) {
+#ifndef MF_EXP_NO_LOG_STORE
+                    if (LOG) L::template sts<0>(l_rs, cl[v], (uint32_t)(j0 + d) * qrow, qd[v]);
+#endif
+                    if (ATOM) L::adds(q_rs, qb, q_oob, cq[v], off, qd[v]);
+                    if (MODE == kPlain) L::template sts<0>(q_rs, cq[v], off, stv[v]);
+                }
+            } else {     // masked slots: push the offset past the table / log segment
+                const uint32_t moff = valid ? off : off + q_oob;
+#pragma unroll
+                for (int v = 0; v < G; ++v) {
+                    if (LOG) L::template st<0>(l_rs, (uint32_t)(j0 + d) * qrow + cl[v], qd[v]);
+                    if (ATOM) L::add(q_rs, qb, q_oob, moff + cq[v], qd[v]);
+                    if (MODE == kPlain) L::template st<0>(q_rs, moff + cq[v], stv[v]);
+                }
+            }
+            // keep the next gather below the last use of the slot's old row: hoisting it would
+            // need a second register set and a copy (and a wait) at the loop latch
+            __builtin_amdgcn_sched_barrier(0);
+            if (FULL) {
+                s_off[d] = (uint32_t)readlane(gi_b, d) * qrow;
+                s_r[d] = readlane(gr_b, d);
+#pragma unroll
+                for (int v = 0; v < G; ++v) s_q[d][v] = L::template lds<kLdAux>(q_rs, cq[v], s_off[d]);
+            }
+            if (DUPS && valid) {  // same item again within the window: forward the row
+#pragma unroll
+                for (int dd = 0; dd < kPF; ++dd)
+                    if (s_off[dd] == off)
+#pragma unroll
+                        for (int v = 0; v < G; ++v) s_q[dd][v] = stv[v];
+            }
+        };
+        int j0 = 0;
+        for (; j0 + kPF <= n; j0 += kPF) {
+            grp_load(j0 + 2 * kPF, gi_n, gr_n);
+#pragma unroll
+            for (int d = 0; d < kPF; ++d) step(std::true_type{}, j0, d);
             gi_b = gi_n;
             gr_b = gr_n;
         }
+        if (j0 < n) {
 #pragma unroll
-        for (int v = 0; v < V; ++v) Buf<T>::template st<0>(p_rs, cu[v], p[v]);
+            for (int d = 0; d < kPF; ++d) step(std::false_type{}, j0, d);
+        }
+#pragma unroll
+        for (int v = 0; v < G; ++v) L::template st<0>(p_rs, cu[v], p[v]);
+        bu_u = cb - hp.gm;
         Buf<T>::template st<0>(b_rs, lane == 0 ? 0u : (uint32_t)sizeof(T), bu_u);
         __builtin_amdgcn_s_setprio(0);
 
         // SVD++ (3): y_j <- A y_j + c for every j in I_u
         if (PP) {
             for (int x = 0; x < n; x += 8) {
-                T g[8][V];
+                vec g[8][G];
                 uint32_t ro[8];
 #pragma unroll
                 for (int a = 0; a < 8; ++a) {
                     const int j = x + a < n ? x + a : n - 1;
                     ro[a] = (uint32_t)it[j] * yrow + (x + a < n ? 0u : y_oob);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) g[a][v] = Buf<T>::template ld<kYLdAux>(y_rs, ro[a] + cu[v]);
+                    for (int v = 0; v < G; ++v) g[a][v] = L::template ld<kYLdAux>(y_rs, ro[a] + cu[v]);
                 }
 #pragma unroll
                 for (int a = 0; a < 8; ++a)
 #pragma unroll
-                    for (int v = 0; v < V; ++v) {
+                    for (int v = 0; v < G; ++v) {
                         if (YATOM)
-                            Buf<T>::add(y_rs, yj, y_oob, ro[a] + cu[v], (A - T(1)) * g[a][v] + cacc[v]);
+                            L::add(y_rs, yj, y_oob, ro[a] + cu[v], (A - T(1)) * g[a][v] + cacc[v]);
                         else
-                            Buf<T>::template st<0>(y_rs, ro[a] + cu[v], A * g[a][v] + cacc[v]);
+                            L::template st<0>(y_rs, ro[a] + cu[v], A * g[a][v] + cacc[v]);
                     }
             }
         }
@@ -448,6 +611,22 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(
 
     for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w]);
 }
+
+#define MF_EPOCH_PARAMS                                                                         \
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,                      \
+        const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,       \
+        T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, int K,  \
+        int biased, Hyper<T> hp, int n_items, int64_t n_waves_req
+#define MF_EPOCH_ARGS \
+    row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, K, biased, hp, n_items, \
+        n_waves_req
+
+template <typename T, int G, int MODE, bool PP, bool DUPS>
+__global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
+{
+    epoch_body<T, G, MODE, PP, DUPS, kPF>(MF_EPOCH_ARGS);
+}
+
 
 // ---------------------------------------------------------------- item-table merge (epoch-chunk)
 //
@@ -547,48 +726,63 @@ __global__ __launch_bounds__(kBlock) void item_apply_kernel(T *tab, T *snap, int
 // 1/(N eta) for items whose row would have converged within the chunk (plain SUM
 // diverges on ML-1M).  eta as in mf_item_merge.
 
-template <typename T, int V>
+// One wave per piece (<= 64 rows): the piece's log-row indices arrive with ONE vector load
+// (lane l holds perm[beg + l]) and are broadcast with v_readlane, so the row gathers carry no
+// scalar-load round trips; rows are read 16 at a time in the 8-byte lane layout of the epoch
+// kernel (one dwordx2 per lane per 512 B of row).
+template <typename T, int G>
 __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
     const T *__restrict__ qlog, int ld, int n_cols, const int32_t *__restrict__ perm,
     const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums)
 {
+    using L = Lane8<T>;
+    using vec = typename L::vec;
+    constexpr int W = L::W;
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
     for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
-        const int beg = piece_beg[pc], end = piece_beg[pc + 1];
-        T acc[V];
+        const int beg = piece_beg[pc], cnt = piece_beg[pc + 1] - beg;  // 1 <= cnt <= 64
+        const int myk = perm[beg + (lane < cnt ? lane : cnt - 1)];
+        vec acc[G];
 #pragma unroll
-        for (int v = 0; v < V; ++v) acc[v] = T(0);
-        constexpr int kU = 8;
-        for (int x = beg; x < end; x += kU) {
-            T g[kU][V];
+        for (int v = 0; v < G; ++v) acc[v] = L::splat(T(0));
+        constexpr int kU = 16;  // rows in flight
+        for (int x = 0; x < cnt; x += kU) {
+            vec g[kU][G];
 #pragma unroll
             for (int a = 0; a < kU; ++a) {
-                const bool ok = x + a < end;
-                const T *row = qlog + (int64_t)perm[ok ? x + a : beg] * ld + lane;
+                const int k = readlane(myk, x + a < cnt ? x + a : cnt - 1);
+                const T *row = qlog + (int64_t)k * ld;
 #pragma unroll
-                for (int v = 0; v < V; ++v)
-                    g[a][v] = (ok && lane + kWave * v < n_cols) ? row[kWave * v] : T(0);
+                for (int v = 0; v < G; ++v) {  // (lanes past the row re-read column 0: no branch)
+                    const int c0 = (lane + kWave * v) * W;
+                    g[a][v] = *(const vec *)(row + (c0 < ld ? c0 : 0));
+                }
             }
 #pragma unroll
             for (int a = 0; a < kU; ++a)
+                if (x + a < cnt)
 #pragma unroll
-                for (int v = 0; v < V; ++v) acc[v] += g[a][v];
+                    for (int v = 0; v < G; ++v) acc[v] += g[a][v];
         }
 #pragma unroll
-        for (int v = 0; v < V; ++v)
-            if (lane + kWave * v < ld) sums[pc * ld + lane + kWave * v] = acc[v];
+        for (int v = 0; v < G; ++v) {
+            const int c0 = (lane + kWave * v) * W;
+#pragma unroll
+            for (int e = 0; e < W; ++e)
+                if (c0 + e < ld) sums[pc * ld + c0 + e] = c0 + e < n_cols ? L::get(acc[v], e) : T(0);
+        }
     }
 }
 
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     T *__restrict__ qb, int n_items, int ld, int n_fac, int bias_col, const T *__restrict__ sums,
-    const int32_t *__restrict__ item_piece_ptr, const int32_t *__restrict__ totals, int count_rule,
-    double eta_bias, double lr_fac, double reg_fac, const double *__restrict__ p2sum,
-    double p2_den, T *__restrict__ delta_out, int apply)
+    const int32_t *__restrict__ item_piece_ptr, const int32_t *__restrict__ totals,
+    int count_rule, double eta_bias, double lr_fac, double reg_fac,
+    const double *__restrict__ p2sum, double p2_den, T *__restrict__ delta_out, int apply)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
@@ -601,24 +795,26 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
         l_bias = log1p(-eta_bias);
     }
     for (int64_t i = wave; i < n_items; i += n_waves) {
-        const int p0 = item_piece_ptr ? item_piece_ptr[i] : (int)i;
-        const int p1 = item_piece_ptr ? item_piece_ptr[i + 1] : (int)i + 1;
         T acc[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) acc[v] = T(0);
-        constexpr int kU = 8;  // independent loads in flight
-        for (int pc = p0; pc < p1; pc += kU) {
-            T g[kU][V];
+        {
+            const int p0 = item_piece_ptr ? item_piece_ptr[i] : (int)i;
+            const int p1 = item_piece_ptr ? item_piece_ptr[i + 1] : (int)i + 1;
+            constexpr int kU = 8;  // independent loads in flight
+            for (int pc = p0; pc < p1; pc += kU) {
+                T g[kU][V];
 #pragma unroll
-            for (int a = 0; a < kU; ++a)
+                for (int a = 0; a < kU; ++a)
 #pragma unroll
-                for (int v = 0; v < V; ++v)
-                    g[a][v] = (pc + a < p1 && lane + kWave * v < ld)
-                                  ? sums[(int64_t)(pc + a) * ld + lane + kWave * v] : T(0);
+                    for (int v = 0; v < V; ++v)
+                        g[a][v] = (pc + a < p1 && lane + kWave * v < ld)
+                                      ? sums[(int64_t)(pc + a) * ld + lane + kWave * v] : T(0);
 #pragma unroll
-            for (int a = 0; a < kU; ++a)
+                for (int a = 0; a < kU; ++a)
 #pragma unroll
-                for (int v = 0; v < V; ++v) acc[v] += g[a][v];
+                    for (int v = 0; v < V; ++v) acc[v] += g[a][v];
+            }
         }
         const double N = totals ? (double)totals[i] : 0.0;
 #pragma unroll
@@ -774,6 +970,19 @@ int dispatch_v(int ld, F &&f)
     return set_err(MF_E_ARG, "n_factors/ld too large");
 }
 
+// G = 8-byte lane groups per row = ceil(ld * sizeof(T) / 512) (the epoch kernel's layout)
+template <typename T, typename F>
+int dispatch_g(int ld, F &&f)
+{
+    const int g = (int)(((int64_t)ld * sizeof(T) + 511) / 512);
+    if (g <= 1) return f(std::integral_constant<int, 1>{});
+    if (g <= 2) return f(std::integral_constant<int, 2>{});
+    if (g <= 3) return f(std::integral_constant<int, 3>{});
+    if (g <= 4) return f(std::integral_constant<int, 4>{});
+    if (g <= 5) return f(std::integral_constant<int, 5>{});
+    return set_err(MF_E_ARG, "n_factors/ld too large");
+}
+
 int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const void *bu,
                 const void *qb, const mf_hyper_t *hp, int K, int ldu, int ldq, int mode,
                 const void *qlog, int dtype)
@@ -796,9 +1005,10 @@ int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const v
 template <bool PP>
 int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, int32_t K,
-                 int32_t biased, const mf_hyper_t *hp, int32_t mode, int32_t n_waves, int32_t dups,
+                 int32_t biased, const mf_hyper_t *hp, int32_t mode, int32_t n_waves, int32_t flags,
                  int32_t dtype, void *stream)
 {
+    const bool dups = flags & MF_EPOCH_DUP_ITEMS;
     if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, qlog, dtype)) return rc;
     if (PP && !yj) return set_err(MF_E_ARG, "null yj");
     if (n_sched <= 0) return 0;
@@ -807,8 +1017,8 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
     auto run = [&](auto tag_t, auto mode_c) -> int {
         using T = decltype(tag_t);
         constexpr int M = decltype(mode_c)::value;
-        return dispatch_v<T>(ldq, [&](auto vc) -> int {
-            constexpr int V = decltype(vc)::value;
+        return dispatch_g<T>(ldq, [&](auto gc) -> int {
+            constexpr int V = decltype(gc)::value;
             // (kLog reads a snapshot: a repeated item sees the chunk-start row, no forwarding)
             auto kern = (dups && M != kLog) ? mf_epoch_kernel<T, V, M, PP, true>
                                             : mf_epoch_kernel<T, V, M, PP, false>;
@@ -840,26 +1050,26 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 400; }
+int mf_version(void) { return 500; }
 
 const char *mf_last_error(void) { return g_err; }
 
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves, int32_t dup_items,
+                 const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves, int32_t flags,
                  int32_t dtype, void *stream)
 {
     return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, nullptr, qlog, n_factors,
-                               biased, hp, mode, n_waves, dup_items, dtype, stream);
+                               biased, hp, mode, n_waves, flags, dtype, stream);
 }
 
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
                    const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves,
-                   int32_t dup_items, int32_t dtype, void *stream)
+                   int32_t flags, int32_t dtype, void *stream)
 {
     return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, n_factors, 1, hp,
-                              mode, n_waves, dup_items, dtype, stream);
+                              mode, n_waves, flags, dtype, stream);
 }
 
 int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *out, int32_t dtype,
@@ -892,8 +1102,8 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
     hipStream_t st = (hipStream_t)stream;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
-        return dispatch_v<T>(ld, [&](auto vc) -> int {
-            hipLaunchKernelGGL((log_reduce_kernel<T, decltype(vc)::value>), dim3(g), dim3(kBlock), 0,
+        return dispatch_g<T>(ld, [&](auto gc) -> int {
+            hipLaunchKernelGGL((log_reduce_kernel<T, decltype(gc)::value>), dim3(g), dim3(kBlock), 0,
                                st, (const T *)qlog, ld, n_cols, perm, piece_beg, n_pieces, (T *)sums);
             return check_launch("log_reduce_kernel");
         });

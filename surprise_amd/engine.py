@@ -118,11 +118,12 @@ class MFEngine(ItemSync):
         to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
         self.sched = [to_dev(np.asarray(c, np.int32)) for c in chunks]
         self._totals_local = []
-        self.logs = []  # "log" mode: per chunk (perm, piece_beg, item_piece_ptr, n_pieces)
+        self.logs = []  # "log" mode: per chunk, see _log_chunk
         for c in chunks:
             if self.mode == _lib.MF_MODE_LOG:
                 perm, pb, ipp, cnt = log_layout(row_ptr, items, c, self.n_items)
-                self.logs.append((to_dev(perm), to_dev(pb), to_dev(ipp), len(pb) - 1))
+                self.logs.append(dict(perm=to_dev(perm), pb=to_dev(pb), ipp=to_dev(ipp),
+                                      n_pieces=len(pb) - 1))
             else:
                 cnt = item_counts(c, row_ptr, items, self.n_items).astype(np.int32)
             self._totals_local.append(cnt)
@@ -150,7 +151,7 @@ class MFEngine(ItemSync):
             self.qlog = z(max(k_hi - k_lo, 1), ldq)
             # the kernels index the log by absolute CSR position k
             self._qlog_base = self.qlog.data_ptr() - k_lo * ldq * esz
-            self.sums = z(max(lg[3] for lg in self.logs), ldq)
+            self.sums = z(max(lg["n_pieces"] for lg in self.logs), ldq)
         snap_q = self.world > 1 and self.mode != _lib.MF_MODE_LOG
         self.qb_s = z(I, ldq) if snap_q else None
         self.yj_s = z(I, ld) if (self.world > 1 and self.yj is not None) else None
@@ -204,34 +205,46 @@ class MFEngine(ItemSync):
     def is_log(self):
         return self.mode == _lib.MF_MODE_LOG
 
+    def _epoch(self, sched, n_sched, n_waves, flags, st):
+        qlog = ctypes.c_void_p(self._qlog_base) if self.is_log else None
+        flags |= _lib.MF_EPOCH_DUP_ITEMS if self.dup_items else 0
+        if self.algo == "svd":
+            _lib.call("mf_svd_epoch", ctypes.byref(self._csr), self._ptr(sched), n_sched,
+                      self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
+                      self.ldq, self.K, int(self.biased), ctypes.byref(self._hyper), self.mode,
+                      qlog, n_waves, flags, self.dtype, st)
+        else:
+            _lib.call("mf_svdpp_epoch", ctypes.byref(self._csr), self._ptr(sched), n_sched,
+                      self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
+                      self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper),
+                      self.mode, qlog, n_waves, flags, self.dtype, st)
+
     def run_chunk(self, c: int, events=None):
-        """Launch the epoch kernel for chunk c (log mode: preceded by the <pu^2> reduction the
-        merge's count-aware weights use, taken at the chunk start like the oracle).  events:
-        optional (start, end) torch.cuda.Event pair recorded around the epoch kernel alone."""
+        """Run chunk c: the epoch kernel, preceded in "log" mode by the <pu^2> reduction of the
+        merge's count-aware weights (taken at the chunk start, like the oracle) and followed by
+        the reduction of the chunk's delta log into per-piece sums (mf_log_reduce); the fold
+        into the table happens in sync_items.  events: optional dict of torch.cuda.Event,
+        "start" / "end" recorded around the epoch kernel on its stream."""
         s = self.sched[c]
         st = self._st()
-        qlog = None
+        ev = events or {}
+        self._chunk = c
         if self.is_log:
-            qlog = ctypes.c_void_p(self._qlog_base)
             self.work.zero_()
             _lib.call("mf_sumsq", ctypes.c_void_p(self.pu.data_ptr() +
                                                   self.u_lo * self.ld * self.pu.element_size()),
-                      self.u_hi - self.u_lo, self.K, self.ld, self._ptr(self.work), self.dtype, st)
-        if events is not None:
-            events[0].record(self.stream)
-        if self.algo == "svd":
-            _lib.call("mf_svd_epoch", ctypes.byref(self._csr), self._ptr(s), s.numel(),
-                      self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
-                      self.ldq, self.K, int(self.biased), ctypes.byref(self._hyper), self.mode,
-                      qlog, self.n_waves, self.dup_items, self.dtype, st)
-        else:
-            _lib.call("mf_svdpp_epoch", ctypes.byref(self._csr), self._ptr(s), s.numel(),
-                      self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
-                      self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper),
-                      self.mode, qlog, self.n_waves, self.dup_items, self.dtype, st)
-        if events is not None:
-            events[1].record(self.stream)
-        self._chunk = c
+                      self.u_hi - self.u_lo, self.K, self.ld, self._ptr(self.work), self.dtype,
+                      st)
+        if "start" in ev:
+            ev["start"].record(self.stream)
+        self._epoch(s, s.numel(), self.n_waves, 0, st)
+        if "end" in ev:
+            ev["end"].record(self.stream)
+        if self.is_log:
+            lg = self.logs[c]
+            _lib.call("mf_log_reduce", ctypes.c_void_p(self._qlog_base), self.ldq, self.K + 1,
+                      self._ptr(lg["perm"]), self._ptr(lg["pb"]), lg["n_pieces"],
+                      self._ptr(self.sums), self.dtype, st)
 
     def _prepare(self, ctx):
         """Global per-item rating counts of every chunk (all ranks) for the count-aware rules."""
@@ -248,19 +261,17 @@ class MFEngine(ItemSync):
         return self.merge_rule == "count"
 
     def _log_fold(self, delta_out, apply):
-        """mf_log_reduce + mf_log_apply of the current chunk."""
+        """mf_log_apply of the current chunk (its pieces were reduced in run_chunk)."""
         c = getattr(self, "_chunk", 0)
-        perm, pb, ipp, n_pieces = self.logs[c]
-        st = self._st()
-        _lib.call("mf_log_reduce", ctypes.c_void_p(self._qlog_base), self.ldq, self.K + 1,
-                  self._ptr(perm), self._ptr(pb), n_pieces, self._ptr(self.sums), self.dtype, st)
+        lg = self.logs[c]
         count = self._count_rule()
         _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K, self.K,
-                  self._ptr(self.sums), self._ptr(ipp),
+                  self._ptr(self.sums), self._ptr(lg["ipp"]),
                   self._ptr(self.totals[c]) if count else None, ctypes.byref(self._hyper),
                   self._ptr(self.work), float(self.n_users * self.K),
                   _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM,
-                  None if delta_out is None else self._ptr(delta_out), int(apply), self.dtype, st)
+                  None if delta_out is None else self._ptr(delta_out), int(apply), self.dtype,
+                  self._st())
 
     def _snap_tables(self):
         """(table, snapshot, ld, bias_col, rule) of the tables merged by snapshot deltas."""

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_without_device(lib):
-    assert lib.mf_version() == 400
+    assert lib.mf_version() == 500
     # argument validation happens before any device call
     rc = lib.mf_item_merge(None, None, 10, 16, 10, 10, 1, 0, None, None, None, None, 0, 16,
                            None, None, 1, 0, None)
@@ -49,7 +49,7 @@ def test_version_and_error_without_device(lib):
 def test_header_constants_match_python():
     text = open(_lib.HEADER_PATH).read()
     for name, val in (("MF_F32", 0), ("MF_F64", 1), ("MF_MODE_PLAIN", 0), ("MF_MODE_ATOMIC", 1),
-                      ("MF_MODE_LOG", 2), ("MF_MERGE_SUM", 0), ("MF_MERGE_COUNT", 1), ("MF_MERGE_MEAN", 2),
+                      ("MF_MODE_LOG", 2), ("MF_MERGE_SUM", 0), ("MF_MERGE_COUNT", 1), ("MF_MERGE_MEAN", 2), ("MF_EPOCH_DUP_ITEMS", 1),
                       ("MF_MAX_FACTORS_F32", 512),
                       ("MF_MAX_FACTORS_F64", 256)):
         assert "#define %s" % name in text and str(val) in text.split("#define %s" % name)[1].split("\n")[0]
