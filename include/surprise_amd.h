@@ -103,10 +103,11 @@ int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, v
                    const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves,
                    int32_t flags, int32_t dtype, void *stream);
 
-/* out[0] += sum of x[r][c]^2 over r < n_rows, c < n_cols (x is [n_rows][ld]; out is one device
- * double).  The <pu^2> statistic of the count-aware merge rules. */
-int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *out, int32_t dtype,
-             void *stream);
+/* stat[0] += sum of x[r][c]^2 over r < n_rows, c < n_cols, stat[1] += n_rows * n_cols (x is
+ * [n_rows][ld]; stat is two device doubles; both parts add up across ranks).  <pu^2> =
+ * stat[0] / stat[1] is the statistic of the count-aware merge rules. */
+int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *stat,
+             int32_t dtype, void *stream);
 
 /*
  * Delta-log merge, step 1 (MF_MODE_LOG): sums[p][c] = sum_{x in [piece_beg[p], piece_beg[p+1])}
@@ -124,12 +125,12 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
  *   MF_MERGE_SUM:   w = 1;
  *   MF_MERGE_COUNT: w = (1 - (1-eta)^N) / (N eta), N = totals[i] (ratings of item i in the chunk,
  *                   all ranks), eta = lr_bi (1 + reg_bi) in bias_col and lr_qi (<p^2> + reg_qi)
- *                   in factor columns, <p^2> = p2sum[0] / p2_den (p2sum a device double).
+ *                   in factor columns, <p^2> = p2stat[0] / p2stat[1] (mf_sumsq's two doubles).
  */
 int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
                  const void *sums, const int32_t *item_piece_ptr, const int32_t *totals,
-                 const mf_hyper_t *hp, const double *p2sum, double p2_den, int32_t rule,
-                 void *delta_out, int32_t apply, int32_t dtype, void *stream);
+                 const mf_hyper_t *hp, const double *p2stat, int32_t rule, void *delta_out,
+                 int32_t apply, int32_t dtype, void *stream);
 
 /* Merge rules of mf_item_merge. */
 #define MF_MERGE_SUM   0 /* delta = sum_r d_r                                                      */
@@ -148,7 +149,7 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
  *   MF_MERGE_COUNT: w_r(i) = (n_r/N)(1-(1-eta)^N)/(1-(1-eta)^{n_r}) with eta = lr_bi (1 + reg_bi)
  *                   in column bias_col (-1: none) and eta = lr_qi (<pu^2> + reg_qi) in columns
  *                   < n_factors, <pu^2> being the mean squared entry of pu[:, :n_factors]
- *                   ([n_users][ldu], reduced on the device into `work`, 1 double of scratch);
+ *                   ([n_users][ldu], reduced on the device into `work`, 2 doubles of scratch);
  *   MF_MERGE_MEAN:  w_r(i) = n_r / N.
  * apply != 0: snap += delta and every replica := snap.  apply == 0: only delta_out is written
  * (the caller all-reduces it with RCCL SUM, then calls mf_item_apply).

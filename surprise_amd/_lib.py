@@ -49,7 +49,7 @@ SIGNATURES = {
     "mf_sumsq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
     "mf_log_reduce": [_vp, _i32, _i32, _vp, _vp, _i64, _vp, _i32, _vp],
     "mf_log_apply": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, ctypes.POINTER(MfHyper), _vp,
-                     _dbl, _i32, _vp, _i32, _i32, _vp],
+                     _i32, _vp, _i32, _i32, _vp],
     "mf_item_merge": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
                       ctypes.POINTER(MfHyper), _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp],
     "mf_item_apply": [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp],

@@ -660,6 +660,7 @@ __global__ __launch_bounds__(kBlock) void sumsq_kernel(const T *__restrict__ x, 
         double t = 0;
         for (int w = 0; w < kBlock / kWave; ++w) t += part[w];
         atomicAdd(out, t);
+        if (blockIdx.x == 0) atomicAdd(out + 1, (double)n_rows * K);  // {sum, count}
     }
 }
 
@@ -667,12 +668,12 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void item_merge_kernel(
     T *tab, T *snap, int n_items, int ld, int n_fac, int bias_col, int n_rep,
     const int32_t *__restrict__ counts, const int32_t *__restrict__ totals, int mean,
-    double l1m_bias, double lr_fac, double reg_fac, const double *__restrict__ p2sum,
-    double p2_den, T *__restrict__ delta, int apply)
+    double l1m_bias, double lr_fac, double reg_fac, const double *__restrict__ p2stat,
+    T *__restrict__ delta, int apply)
 {
     const int64_t total = (int64_t)n_items * ld, stride = total;
     double l1m_fac = 0;
-    if (counts && !mean) l1m_fac = log1p(-lr_fac * (*p2sum / p2_den + reg_fac));
+    if (counts && !mean) l1m_fac = log1p(-lr_fac * (p2stat[0] / p2stat[1] + reg_fac));
     for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < total;
          x += (int64_t)gridDim.x * kBlock) {
         const int i = (int)(x / ld), c = (int)(x - (int64_t)i * ld);
@@ -782,7 +783,7 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     T *__restrict__ qb, int n_items, int ld, int n_fac, int bias_col, const T *__restrict__ sums,
     const int32_t *__restrict__ item_piece_ptr, const int32_t *__restrict__ totals,
     int count_rule, double eta_bias, double lr_fac, double reg_fac,
-    const double *__restrict__ p2sum, double p2_den, T *__restrict__ delta_out, int apply)
+    const double *__restrict__ p2stat, T *__restrict__ delta_out, int apply)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
@@ -790,7 +791,7 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
     double eta_fac = 0, l_fac = 0, l_bias = 0;
     if (count_rule) {
-        eta_fac = lr_fac * (*p2sum / p2_den + reg_fac);
+        eta_fac = lr_fac * (p2stat[0] / p2stat[1] + reg_fac);
         l_fac = log1p(-eta_fac);
         l_bias = log1p(-eta_bias);
     }
@@ -1115,15 +1116,15 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
 
 int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
                  const void *sums, const int32_t *item_piece_ptr, const int32_t *totals,
-                 const mf_hyper_t *hp, const double *p2sum, double p2_den, int32_t rule,
-                 void *delta_out, int32_t apply, int32_t dtype, void *stream)
+                 const mf_hyper_t *hp, const double *p2stat, int32_t rule, void *delta_out,
+                 int32_t apply, int32_t dtype, void *stream)
 {
     if (n_items < 0 || ld < 1 || n_factors < 0 || n_factors > ld || bias_col >= ld)
         return set_err(MF_E_ARG, "bad shape");
     if (rule != MF_MERGE_SUM && rule != MF_MERGE_COUNT) return set_err(MF_E_ARG, "bad merge rule");
     const int count_rule = rule == MF_MERGE_COUNT;
-    if (count_rule && (!totals || !hp || !p2sum || !(p2_den > 0)))
-        return set_err(MF_E_ARG, "count-aware rule needs totals, hp, p2sum, p2_den > 0");
+    if (count_rule && (!totals || !hp || !p2stat))
+        return set_err(MF_E_ARG, "count-aware rule needs totals, hp, p2stat");
     if (n_items == 0 || (!apply && !delta_out)) return 0;
     if (!sums || (apply && !qb)) return set_err(MF_E_ARG, "null argument");
     const int g = grid_for_waves(default_waves(n_items));
@@ -1135,8 +1136,8 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
         return dispatch_v<T>(ld, [&](auto vc) -> int {
             hipLaunchKernelGGL((log_apply_kernel<T, decltype(vc)::value>), dim3(g), dim3(kBlock), 0,
                                st, (T *)qb, n_items, ld, n_factors, bias_col, (const T *)sums,
-                               item_piece_ptr, totals, count_rule, eta_b, lr_f, reg_f, p2sum,
-                               p2_den, (T *)delta_out, apply);
+                               item_piece_ptr, totals, count_rule, eta_b, lr_f, reg_f, p2stat,
+                               (T *)delta_out, apply);
             return check_launch("log_apply_kernel");
         });
     };
@@ -1164,13 +1165,12 @@ int mf_item_merge(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
     if (!delta_out && !apply) return 0;
     hipStream_t st = (hipStream_t)stream;
     const int64_t total = (int64_t)n_items * ld;
-    double l1m_bias = 0, lr_fac = 0, reg_fac = 0, den = 1;
+    double l1m_bias = 0, lr_fac = 0, reg_fac = 0;
     if (counts && !mean) {
         l1m_bias = bias_col >= 0 ? log1p(-hp->lr_bi * (1.0 + hp->reg_bi)) : 0.0;
         lr_fac = hp->lr_qi;
         reg_fac = hp->reg_qi;
-        den = (double)n_users * n_factors;
-        hipError_t e = hipMemsetAsync(work, 0, sizeof(double), st);
+        hipError_t e = hipMemsetAsync(work, 0, 2 * sizeof(double), st);
         if (e != hipSuccess) return set_err((int)e, "hipMemsetAsync(work)");
         const int g = grid_for_waves(n_users < 1024 ? n_users : 1024);
         if (dtype == MF_F32)
@@ -1185,12 +1185,12 @@ int mf_item_merge(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
     if (dtype == MF_F32)
         hipLaunchKernelGGL(item_merge_kernel<float>, dim3(g), dim3(kBlock), 0, st, (float *)tab,
                            (float *)snap, n_items, ld, n_factors, bias_col, n_replicas, counts,
-                           totals, mean, l1m_bias, lr_fac, reg_fac, (const double *)work, den,
+                           totals, mean, l1m_bias, lr_fac, reg_fac, (const double *)work,
                            (float *)delta_out, apply);
     else
         hipLaunchKernelGGL(item_merge_kernel<double>, dim3(g), dim3(kBlock), 0, st, (double *)tab,
                            (double *)snap, n_items, ld, n_factors, bias_col, n_replicas, counts,
-                           totals, mean, l1m_bias, lr_fac, reg_fac, (const double *)work, den,
+                           totals, mean, l1m_bias, lr_fac, reg_fac, (const double *)work,
                            (double *)delta_out, apply);
     return check_launch("item_merge_kernel");
 }

@@ -129,7 +129,7 @@ class MFEngine(ItemSync):
             self._totals_local.append(cnt)
         self.counts = [to_dev(t) for t in self._totals_local]  # this rank's n_r per chunk
         self.totals = None  # set by _prepare(): summed over every rank
-        self.work = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.work = torch.zeros(2, dtype=torch.float64, device=dev)  # {sum pu^2, count}
         self.dup_items = int(_has_duplicate_items(row_ptr, items))
 
         # ---- factor tables
@@ -268,8 +268,7 @@ class MFEngine(ItemSync):
         _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K, self.K,
                   self._ptr(self.sums), self._ptr(lg["ipp"]),
                   self._ptr(self.totals[c]) if count else None, ctypes.byref(self._hyper),
-                  self._ptr(self.work), float(self.n_users * self.K),
-                  _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM,
+                  self._ptr(self.work), _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM,
                   None if delta_out is None else self._ptr(delta_out), int(apply), self.dtype,
                   self._st())
 
@@ -343,7 +342,6 @@ class MFEngine(ItemSync):
             _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K, self.K,
                       self._ptr(bufs[0]), None, self._ptr(self.totals[c]) if count else None,
                       ctypes.byref(self._hyper), self._ptr(bufs[-1]),
-                      float(self.n_users * self.K),
                       _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM, None, 1, self.dtype, st)
             x = 1
         for tab, snap, ld, _, _ in self._snap_tables():
