@@ -314,6 +314,64 @@ __device__ __forceinline__ float wave_sum_u(float v) {
 }
 __device__ __forceinline__ double wave_sum_u(double v) { return readlane(wave_sum(v), 0); }
 
+// ---- one-element-per-lane ("Lane1") view of a row, for the float atomics: an atomic
+// instruction then covers 64 consecutive dwords (256 B) instead of every other dword of 512 B.
+// Lane1 group u, lane l holds column l + 64 u; for fp32 it has 2G groups, for fp64 it is the
+// Lane8 layout itself.  Conversions are ds_bpermute lane exchanges (no LDS storage).
+template <typename T, int G>
+struct Lane1 {
+    static constexpr int U = Lane8<T>::W * G;
+    typedef T type[U];
+};
+
+__device__ __forceinline__ float bperm(int src_lane, float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_lane << 2, __builtin_bit_cast(int, x)));
+}
+
+template <int G>
+__device__ __forceinline__ void to_lane1(const typename Lane8<float>::vec (&x)[G], float (&y)[2 * G]) {
+    const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+    for (int u = 0; u < 2 * G; ++u) {  // column c = lane + 64 u lives in Lane8 group u/2, lane c/2
+        const int src = 32 * (u & 1) + (lane >> 1);
+        const float a = bperm(src, x[u >> 1].x), b = bperm(src, x[u >> 1].y);
+        y[u] = (lane & 1) ? b : a;
+    }
+}
+template <int G>
+__device__ __forceinline__ void to_lane1(const double (&x)[G], double (&y)[G]) {
+#pragma unroll
+    for (int u = 0; u < G; ++u) y[u] = x[u];
+}
+
+template <int G>
+__device__ __forceinline__ void to_lane8(const float (&y)[2 * G], typename Lane8<float>::vec (&x)[G]) {
+    const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+    for (int v = 0; v < G; ++v) {  // column 2 (lane + 64 v) + e lives in Lane1 group 2v + (lane >= 32)
+        const int s0 = (2 * lane) & (kWave - 1);
+        const float lo0 = bperm(s0, y[2 * v]), hi0 = bperm(s0, y[2 * v + 1]);
+        const float lo1 = bperm(s0 + 1, y[2 * v]), hi1 = bperm(s0 + 1, y[2 * v + 1]);
+        x[v].x = lane < 32 ? lo0 : hi0;
+        x[v].y = lane < 32 ? lo1 : hi1;
+    }
+}
+// memory-side float add of one element per lane at voff + soff (rows out of range dropped)
+__device__ __forceinline__ void atom_add1(rsrc_t r, void *, uint32_t, uint32_t voff, uint32_t soff,
+                                          float v) {
+    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, voff, soff, 0);
+}
+__device__ __forceinline__ void atom_add1(rsrc_t, void *base, uint32_t bytes, uint32_t voff,
+                                          uint32_t soff, double v) {
+    if (voff + soff < bytes) atomicAdd((double *)base + (voff + soff) / sizeof(double), v);
+}
+
+template <int G>
+__device__ __forceinline__ void to_lane8(const double (&y)[G], double (&x)[G]) {
+#pragma unroll
+    for (int v = 0; v < G; ++v) x[v] = y[v];
+}
+
 // Item table row (ldq elements): [q_0 .. q_{K-1} | b_i | 0 ...].  The user row is extended in
 // registers with a constant 1 in column K, so <q_aug, p_aug> = <q_i, p_u> + b_i and the item
 // bias rides in the same gather / scatter as the item factors; its update
@@ -364,6 +422,14 @@ __device__ __forceinline__ void epoch_body(
     // offset past the table / log so their loads read 0 and their stores are dropped)
     uint32_t cq[G], cu[G], cl[G];
     vec one[G], lrq[G], nrq[G], lrp[G], ap[G], lry[G];
+    constexpr int U = Lane1<T, G>::U;  // Lane1 groups (atomics, SVD++ y rows)
+    uint32_t cq1[U], cy1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = lane + kWave * u;
+        cq1[u] = c < ldq ? (uint32_t)c * sizeof(T) : (uint32_t)n_items * ldq * sizeof(T);
+        cy1[u] = c < ldu ? (uint32_t)c * sizeof(T) : (uint32_t)n_items * ldu * sizeof(T);
+    }
 #pragma unroll
     for (int v = 0; v < G; ++v) {
         const int c0 = (lane + kWave * v) * W;  // first column of this lane's 8 bytes
@@ -422,25 +488,44 @@ __device__ __forceinline__ void epoch_body(
         T bu_u = Buf<T>::template ld<0>(b_rs, 0);
         const T sqrt_n = sqrt(T(n));  // mf.pyx:470
 
+        // SVD++: walk the user's y_j rows: 64 item ids per vector load (lane l holds entry
+        // x0 + l, read back with v_readlane), rows gathered kYB at a time; rows past the user's
+        // list get an out-of-range offset (load 0, store / atomic dropped).
+        constexpr int kYB = 32;
+        auto walk_y = [&](auto &&consume) {
+            for (int x0 = 0; x0 < n; x0 += kWave) {
+                const int gid = it[x0 + lane < n ? x0 + lane : n - 1];
+                const int cnt = n - x0 < kWave ? n - x0 : kWave;
+                for (int x = 0; x < cnt; x += kYB) {
+                    T g[kYB][U];
+                    uint32_t ro[kYB];
+#pragma unroll
+                    for (int a = 0; a < kYB; ++a) {
+                        ro[a] = (uint32_t)readlane(gid, x + a < kWave ? x + a : kWave - 1) * yrow +
+                                (x + a < cnt ? 0u : y_oob);
+#pragma unroll
+                        for (int u = 0; u < U; ++u)
+                            g[a][u] = Buf<T>::template ld<kYLdAux>(y_rs, ro[a] + cy1[u]);
+                    }
+                    consume(g, ro);
+                }
+            }
+        };
         // SVD++ (1): u_impl = sum_{j in I_u} y_j / sqrt|I_u|  (mf.pyx:473-476, per-term division)
         vec imp[G], cacc[G];
 #pragma unroll
         for (int v = 0; v < G; ++v) imp[v] = cacc[v] = L::splat(T(0));
         if (PP) {
-            for (int x = 0; x < n; x += 8) {
-                vec g[8][G];
+            T imp1[U];
 #pragma unroll
-                for (int a = 0; a < 8; ++a) {
-                    const int j = x + a < n ? x + a : n - 1;
-                    const uint32_t ro = (uint32_t)it[j] * yrow + (x + a < n ? 0u : y_oob);
+            for (int u = 0; u < U; ++u) imp1[u] = T(0);
+            walk_y([&](T (&g)[kYB][U], uint32_t (&)[kYB]) {
 #pragma unroll
-                    for (int v = 0; v < G; ++v) g[a][v] = L::template ld<kYLdAux>(y_rs, ro + cu[v]);
-                }
+                for (int a = 0; a < kYB; ++a)
 #pragma unroll
-                for (int a = 0; a < 8; ++a)
-#pragma unroll
-                    for (int v = 0; v < G; ++v) imp[v] += g[a][v] / sqrt_n;
-            }
+                    for (int u = 0; u < U; ++u) imp1[u] += g[a][u] / sqrt_n;
+            });
+            to_lane8<G>(imp1, imp);
         }
         T A = T(1);
 
@@ -531,23 +616,29 @@ __device__ __forceinline__ void epoch_body(
             vec stv[G];  // the row after this rating (kPlain stores it; DUPS forwards it)
 #pragma unroll
             for (int v = 0; v < G; ++v) stv[v] = s_q[d][v] + qd[v];
+            T qd1[U];  // kAtomic: the delta in the Lane1 view (contiguous 256-B atomics)
+            if (ATOM) to_lane1<G>(qd, qd1);
             if (FULL) {  // real rows only: the row offset rides in soffset, no address math
 #pragma unroll
                 for (int v = 0; v < G; ++v) {
 #ifndef MF_EXP_NO_LOG_STORE
                     if (LOG) L::template sts<0>(l_rs, cl[v], (uint32_t)(j0 + d) * qrow, qd[v]);
 #endif
-                    if (ATOM) L::adds(q_rs, qb, q_oob, cq[v], off, qd[v]);
                     if (MODE == kPlain) L::template sts<0>(q_rs, cq[v], off, stv[v]);
                 }
+                if (ATOM)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) atom_add1(q_rs, qb, q_oob, cq1[u], off, qd1[u]);
             } else {     // masked slots: push the offset past the table / log segment
                 const uint32_t moff = valid ? off : off + q_oob;
 #pragma unroll
                 for (int v = 0; v < G; ++v) {
                     if (LOG) L::template st<0>(l_rs, (uint32_t)(j0 + d) * qrow + cl[v], qd[v]);
-                    if (ATOM) L::add(q_rs, qb, q_oob, moff + cq[v], qd[v]);
                     if (MODE == kPlain) L::template st<0>(q_rs, moff + cq[v], stv[v]);
                 }
+                if (ATOM)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) atom_add1(q_rs, qb, q_oob, moff + cq1[u], 0, qd1[u]);
             }
             // keep the next gather below the last use of the slot's old row: hoisting it would
             // need a second register set and a copy (and a wait) at the loop latch
@@ -586,26 +677,19 @@ __device__ __forceinline__ void epoch_body(
 
         // SVD++ (3): y_j <- A y_j + c for every j in I_u
         if (PP) {
-            for (int x = 0; x < n; x += 8) {
-                vec g[8][G];
-                uint32_t ro[8];
+            T cacc1[U];
+            to_lane1<G>(cacc, cacc1);
+            walk_y([&](T (&g)[kYB][U], uint32_t (&ro)[kYB]) {
 #pragma unroll
-                for (int a = 0; a < 8; ++a) {
-                    const int j = x + a < n ? x + a : n - 1;
-                    ro[a] = (uint32_t)it[j] * yrow + (x + a < n ? 0u : y_oob);
+                for (int a = 0; a < kYB; ++a)
 #pragma unroll
-                    for (int v = 0; v < G; ++v) g[a][v] = L::template ld<kYLdAux>(y_rs, ro[a] + cu[v]);
-                }
-#pragma unroll
-                for (int a = 0; a < 8; ++a)
-#pragma unroll
-                    for (int v = 0; v < G; ++v) {
+                    for (int u = 0; u < U; ++u) {
                         if (YATOM)
-                            L::add(y_rs, yj, y_oob, ro[a] + cu[v], (A - T(1)) * g[a][v] + cacc[v]);
+                            atom_add1(y_rs, yj, y_oob, cy1[u], ro[a], (A - T(1)) * g[a][u] + cacc1[u]);
                         else
-                            L::template st<0>(y_rs, ro[a] + cu[v], A * g[a][v] + cacc[v]);
+                            Buf<T>::template st<0>(y_rs, ro[a] + cy1[u], A * g[a][u] + cacc1[u]);
                     }
-            }
+            });
         }
     };
 

@@ -13,15 +13,17 @@ from surprise_amd.engine import MFEngine  # noqa: E402
 from surprise_amd.model_selection import KFold  # noqa: E402
 
 mode = sys.argv[1] if len(sys.argv) > 1 else "log"
+algo = os.environ.get("PROBE_ALGO", "svd")
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 u, i, r = synthetic.shape("ml-1m")
 ts, _ = next(KFold(5, random_state=0).split(Dataset.load_from_arrays(u, i, r)))
 rp, it, rt = ts.csr()
 hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02, reg_pu=.02,
              reg_qi=.02, global_mean=float(ts.global_mean))
-eng = MFEngine((rp, it, rt), ts.n_items, K, hyper=hyper, mode=mode)
+eng = MFEngine((rp, it, rt), ts.n_items, K, hyper=hyper, mode=mode, algo=algo)
 rng = np.random.RandomState(0)
-eng.set_factors(rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K)))
+eng.set_factors(rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K)),
+                yj=rng.normal(0, .1, (ts.n_items, K)) if algo == "svdpp" else None)
 full = eng.sched[0].clone()
 deg = np.diff(rp)
 order = full.cpu().numpy()
@@ -39,7 +41,7 @@ def t_sched(s, n_waves=0, reps=10):
     return float(np.median(ts_[2:])) * 1e3
 
 
-print("mode", mode, "K", K, "max deg", deg.max(), "ratings", deg.sum())
+print("algo", algo, "mode", mode, "K", K, "max deg", deg.max(), "ratings", deg.sum())
 cases = [("full", order, 0), ("top1", order[:1], 0), ("top16", order[:16], 0),
                     ("top256", order[:256], 0), ("top1024", order[:1024], 0),
                     ("drop-top64", order[64:], 0), ("drop-top256", order[256:], 0),
