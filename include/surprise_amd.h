@@ -165,6 +165,41 @@ int mf_item_apply(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
                   const void *delta, int32_t dtype, void *stream);
 
 /*
+ * One epoch of NMF.sgd (matrix_factorization.pyx:646-735) in two race-free passes.
+ * mf_nmf_user_pass: one wave per user computes every rating's estimate
+ *   est = mu + b_u + b_i + <q_i, p_u>  (biased; the b_u recursion of :707-708 in the user's
+ *   order, b_i read from qb's column n_factors as the epoch-start snapshot) or <q_i, p_u>,
+ *   saves it in est[k] (k = CSR position) and, biased, the item-bias step in blog[k]; sums the
+ *   user's numerator / denominator (:712-713) and writes p_u's multiplicative step (:719-723) to
+ *   pu_next (pu itself stays the epoch's factors).  hp: reg_pu, lr_bu, reg_bu, lr_bi, reg_bi,
+ *   global_mean (0 when unbiased).
+ * mf_nmf_item_pass: one wave per item walks its ratings (csc_ptr[n_items+1], csc_pos[nnz] = CSR
+ *   positions in ir order, row_user[nnz] = user of each CSR position), sums p_u r and p_u est over
+ *   the OLD pu (:714-716) and takes q_i's step (:726-730) with hp->reg_qi; biased:
+ *   b_i += w * sum of blog (rule MF_MERGE_COUNT: w = (1 - (1-eta)^N) / (N eta),
+ *   eta = lr_bi (1 + reg_bi); MF_MERGE_SUM: w = 1).  Call it after the user pass, then swap
+ *   pu / pu_next.  pu, pu_next [n_users][ldu]; qb [n_items][ldq] = [q_i | b_i | 0 ...].
+ */
+int mf_nmf_user_pass(const mf_csr_t *csr, const void *pu, void *pu_next, void *bu, int32_t ldu,
+                     const void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
+                     const mf_hyper_t *hp, void *est, void *blog, int32_t dtype, void *stream);
+int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32_t *row_user,
+                     const void *ratings, const void *est, const void *blog, const void *pu,
+                     int32_t ldu, void *qb, int32_t ldq, int32_t n_items, int32_t n_factors,
+                     int32_t biased, const mf_hyper_t *hp, int32_t rule, int32_t dtype,
+                     void *stream);
+
+/*
+ * One epoch of baseline_als (optimize_baselines.pyx:14-54): b_i = sum over ir[i] of
+ * (r - mu - b_u) / (reg_i + |ir[i]|) for every item, then b_u = sum over ur[u] of
+ * (r - mu - b_i) / (reg_u + |ur[u]|) for every user.  csc as for mf_nmf_item_pass.
+ * (baseline_sgd, :57-84, is mf_svd_epoch with n_factors = 0.)
+ */
+int mf_baseline_als_epoch(const mf_csr_t *csr, const int64_t *csc_ptr, const int64_t *csc_pos,
+                          const int32_t *row_user, void *bu, void *bi, double global_mean,
+                          double reg_u, double reg_i, int32_t dtype, void *stream);
+
+/*
  * Batched SVD.estimate (matrix_factorization.pyx:269-299): for x < n, with u[x] < 0 / i[x] < 0
  * meaning an unknown user / item ('UKN__' ids, algo_base.py:137-144):
  *   biased:   est = mu (+bu[u] if known u) (+b_i if known i) (+ q_i.(pu[u] + imp[u]) if both)

@@ -182,6 +182,44 @@ def svdpp_sgd_deltalog(row_ptr, items, ratings, n_items, K, n_epochs, global_mea
     return pu, qi, yj, bu, bi
 
 
+def nmf_sgd(row_ptr, items, ratings, n_items, K, n_epochs, biased, global_mean, pu, qi,
+            reg_pu=.06, reg_qi=.06, reg_bu=.02, reg_bi=.02, lr_bu=.005, lr_bi=.005,
+            bu=None, bi=None, bias_log=False):
+    """In-place fp64 NMF.sgd (mf.pyx:646-735); bias_log=True: the GPU's snapshot + count-aware
+    schedule for the item biases. Returns (pu, qi, bu, bi)."""
+    row_ptr, items, ratings = _csr_args(row_ptr, items, ratings)
+    n_users = len(row_ptr) - 1
+    pu = np.ascontiguousarray(pu, dtype=np.float64)
+    qi = np.ascontiguousarray(qi, dtype=np.float64)
+    bu = np.zeros(n_users) if bu is None else np.ascontiguousarray(bu, dtype=np.float64)
+    bi = np.zeros(n_items) if bi is None else np.ascontiguousarray(bi, dtype=np.float64)
+    cnt = np.bincount(items, minlength=n_items).astype(np.int64)
+    lib().oracle_nmf_sgd(ctypes.c_int64(n_users), ctypes.c_int64(n_items), _p(row_ptr), _p(items),
+                         _p(ratings), _p(cnt), ctypes.c_int32(K), ctypes.c_int32(n_epochs),
+                         ctypes.c_int32(int(biased)), ctypes.c_double(global_mean),
+                         *[ctypes.c_double(x) for x in (reg_pu, reg_qi, reg_bu, reg_bi, lr_bu,
+                                                        lr_bi)],
+                         ctypes.c_int32(int(bias_log)), _p(pu), _p(qi), _p(bu), _p(bi))
+    return pu, qi, bu, bi
+
+
+def baseline_als(row_ptr, items, ratings, n_items, csc_ptr, csc_pos, global_mean, n_epochs=10,
+                 reg_u=15, reg_i=10):
+    """fp64 baseline_als (optimize_baselines.pyx:14-54); csc_ptr / csc_pos = Trainset.csc().
+    Returns (bu, bi)."""
+    row_ptr, items, ratings = _csr_args(row_ptr, items, ratings)
+    n_users = len(row_ptr) - 1
+    row_user = np.repeat(np.arange(n_users, dtype=np.int32), np.diff(row_ptr))
+    csc_ptr = np.ascontiguousarray(csc_ptr, np.int64)
+    csc_pos = np.ascontiguousarray(csc_pos, np.int64)
+    bu, bi = np.zeros(n_users), np.zeros(n_items)
+    lib().oracle_baseline_als(ctypes.c_int64(n_users), ctypes.c_int64(n_items), _p(row_ptr),
+                              _p(items), _p(ratings), _p(csc_ptr), _p(csc_pos), _p(row_user),
+                              ctypes.c_double(global_mean), ctypes.c_int32(n_epochs),
+                              ctypes.c_double(reg_u), ctypes.c_double(reg_i), _p(bu), _p(bi))
+    return bu, bi
+
+
 def svd_predict(u, i, K, biased, global_mean, pu, qi, bu, bi):
     """SVD.estimate on inner ids (-1 = unknown). Returns (est, impossible)."""
     u = np.ascontiguousarray(u, dtype=np.int32)

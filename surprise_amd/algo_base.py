@@ -1,7 +1,7 @@
 """AlgoBase -- the plugin API the hot path sits behind, mirroring
-surprise/prediction_algorithms/algo_base.py:22-218 (fit / train / predict /
-default_prediction / test).  Baseline and similarity helpers (:220-334) belong
-to other algorithm families and are out of scope.
+surprise/prediction_algorithms/algo_base.py:22-254 (fit / train / predict /
+default_prediction / test / compute_baselines).  The similarity helpers (:256-334) belong to
+the k-NN family and are out of scope.
 """
 import warnings
 
@@ -84,3 +84,20 @@ class AlgoBase:
         iterate_on = testset.tolist() if isinstance(testset, np.ndarray) else testset
         return [self.predict(uid, iid, r_ui_trans - self.trainset.offset, verbose=verbose)
                 for (uid, iid, r_ui_trans) in iterate_on]
+
+    def compute_baselines(self):
+        """algo_base.py:220-254: baselines once per trainset, by bsl_options['method']
+        ('als' default, or 'sgd'), computed on the device (optimize_baselines.py)."""
+        if self.bu is not None:
+            return self.bu, self.bi
+        from .optimize_baselines import baseline_als, baseline_sgd
+        method = dict(als=baseline_als, sgd=baseline_sgd)
+        method_name = self.bsl_options.get('method', 'als')
+        try:
+            fn = method[method_name]
+        except KeyError:
+            raise ValueError('Invalid method ' + method_name +
+                             ' for baseline computation.' +
+                             ' Available methods are als and sgd.')
+        self.bu, self.bi = fn(self)
+        return self.bu, self.bi

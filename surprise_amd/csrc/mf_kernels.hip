@@ -920,6 +920,254 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     }
 }
 
+// ---------------------------------------------------------------- NMF
+//
+// NMF.sgd (matrix_factorization.pyx:646-735): within an epoch the factors are constant; every
+// rating adds q_i r, q_i est to its user's numerator / denominator and p_u r, p_u est to its
+// item's, then both sides take a multiplicative step.  Two race-free passes per epoch:
+//   nmf_user_kernel  one wave per user: est of each rating (dot products of a 16-row batch are
+//                    independent; with biases the b_u recursion is a scalar chain), the user's
+//                    sums in registers, p_u's step into pu_next; est (and the item-bias step of
+//                    the rating, biased) saved per CSR position;
+//   nmf_item_kernel  one wave per item over its ratings (CSC order): p_u r, p_u est summed from
+//                    the OLD pu, q_i's step; biased: b_i += w(N) * sum of the saved bias steps
+//                    (the snapshot + count-aware rule of the delta log, oracle bias_log=1).
+
+template <typename T, int G, bool BIASED>
+__global__ __launch_bounds__(kBlock) void nmf_user_kernel(
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
+    const T *__restrict__ ratings, int n_users, const T *__restrict__ pu, T *__restrict__ pu_next,
+    T *__restrict__ bu, int ldu, const T *__restrict__ qb, int ldq, int K, T reg_pu, T lr_bu,
+    T reg_bu, T lr_bi, T reg_bi, T gm, T *__restrict__ est_out, T *__restrict__ blog)
+{
+    using L = Lane8<T>;
+    using vec = typename L::vec;
+    constexpr int W = L::W;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    int cq[G], cu[G];
+    vec fac[G];
+#pragma unroll
+    for (int v = 0; v < G; ++v) {
+        const int c0 = (lane + kWave * v) * W;
+        cq[v] = c0 < ldq ? c0 : 0;  // (lanes past the row re-read column 0: no branch)
+        cu[v] = c0 < ldu ? c0 : 0;
+#pragma unroll
+        for (int e = 0; e < W; ++e) L::set(fac[v], e, c0 + e < K ? T(1) : T(0));
+    }
+    // the bias column K of an item row: group, lane and element of the Lane8 layout
+    const int kg = K / (kWave * W), kl = (K / W) % kWave, ke = K % W;
+    const T abu = T(1) - lr_bu * reg_bu, kb = gm * (T(1) - abu);
+    constexpr int kB = 16;
+    for (int64_t u = wave; u < n_users; u += n_waves) {
+        const int64_t s = row_ptr[u];
+        const int n = (int)(row_ptr[u + 1] - s);
+        if (n <= 0) continue;
+        const T *prow = pu + u * (int64_t)ldu;
+        vec p[G], un[G], ud[G];
+#pragma unroll
+        for (int v = 0; v < G; ++v) {
+            p[v] = fac[v] * *(const vec *)(prow + cu[v]);
+            un[v] = ud[v] = L::splat(T(0));
+        }
+        T cb = BIASED ? gm + bu[u] : T(0);  // mu + b_u (NMF unbiased: est = dot exactly)
+        for (int x0 = 0; x0 < n; x0 += kWave) {
+            const int cnt = n - x0 < kWave ? n - x0 : kWave;
+            const int gi = items[s + x0 + (lane < cnt ? lane : cnt - 1)];
+            const T gr = ratings[s + x0 + (lane < cnt ? lane : cnt - 1)];
+            T e_l = T(0), b_l = T(0);
+            for (int x = 0; x < cnt; x += kB) {
+                vec q[kB][G];
+                T dot[kB], bi[kB];
+#pragma unroll
+                for (int a = 0; a < kB; ++a) {
+                    const T *qrow = qb + (int64_t)readlane(gi, x + a < cnt ? x + a : cnt - 1) * ldq;
+#pragma unroll
+                    for (int v = 0; v < G; ++v) q[a][v] = *(const vec *)(qrow + cq[v]);
+                }
+#pragma unroll
+                for (int a = 0; a < kB; ++a) {  // independent reductions: interleaved by the compiler
+                    vec part = L::splat(T(0));
+#pragma unroll
+                    for (int v = 0; v < G; ++v) part += q[a][v] * p[v];
+                    dot[a] = wave_sum_u(L::hsum(part));
+                    bi[a] = BIASED ? readlane(L::get(q[a][kg], ke), kl) : T(0);
+                }
+#pragma unroll
+                for (int a = 0; a < kB; ++a) {
+                    if (x + a >= cnt) break;
+                    const T r = readlane(gr, x + a);
+                    const T est = (cb + bi[a]) + dot[a];  // mf.pyx:703
+                    const T err = r - est;
+                    if (BIASED) {                          // mf.pyx:707-709
+                        const T bstep = lr_bi * (err - reg_bi * bi[a]);
+                        b_l = lane == x + a ? bstep : b_l;
+                        cb = lr_bu * err + (abu * cb + kb);
+                    }
+#pragma unroll
+                    for (int v = 0; v < G; ++v) {          // mf.pyx:712-716 (user side)
+                        un[v] += q[a][v] * r;
+                        ud[v] += q[a][v] * est;
+                    }
+                    e_l = lane == x + a ? est : e_l;
+                }
+            }
+            if (lane < cnt) {
+                est_out[s + x0 + lane] = e_l;
+                if (BIASED) blog[s + x0 + lane] = b_l;
+            }
+        }
+        const T nreg = (T)n * reg_pu;  // mf.pyx:719-723
+        T *orow = pu_next + u * (int64_t)ldu;
+#pragma unroll
+        for (int v = 0; v < G; ++v) {
+            const int c0 = (lane + kWave * v) * W;
+            if (c0 < ldu) {
+                vec o;
+#pragma unroll
+                for (int e = 0; e < W; ++e) {
+                    const T pf = L::get(p[v], e);
+                    const T den = L::get(ud[v], e) + nreg * pf;
+                    L::set(o, e, c0 + e < K ? pf * (L::get(un[v], e) / den) : T(0));
+                }
+                *(vec *)(orow + c0) = o;
+            }
+        }
+        if (BIASED && lane == 0) bu[u] = cb - gm;
+    }
+}
+
+template <typename T, int G, bool BIASED>
+__global__ __launch_bounds__(kBlock) void nmf_item_kernel(
+    const int64_t *__restrict__ csc_ptr, const int64_t *__restrict__ csc_pos,
+    const int32_t *__restrict__ row_user, const T *__restrict__ ratings, const T *__restrict__ est,
+    const T *__restrict__ blog, const T *__restrict__ pu, int ldu, T *__restrict__ qb, int ldq,
+    int K, int n_items, T reg_qi, double eta_b, int count_rule)
+{
+    using L = Lane8<T>;
+    using vec = typename L::vec;
+    constexpr int W = L::W;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    int cu[G];
+#pragma unroll
+    for (int v = 0; v < G; ++v) {
+        const int c0 = (lane + kWave * v) * W;
+        cu[v] = c0 < ldu ? c0 : 0;
+    }
+    constexpr int kB = 16;
+    for (int64_t i = wave; i < n_items; i += n_waves) {
+        const int64_t b = csc_ptr[i];
+        const int N = (int)(csc_ptr[i + 1] - b);
+        vec in[G], id[G];
+#pragma unroll
+        for (int v = 0; v < G; ++v) in[v] = id[v] = L::splat(T(0));
+        T bs = T(0);
+        for (int x0 = 0; x0 < N; x0 += kWave) {
+            const int cnt = N - x0 < kWave ? N - x0 : kWave;
+            const int64_t k = csc_pos[b + x0 + (lane < cnt ? lane : cnt - 1)];
+            const int uu = row_user[k];
+            const T r_l = ratings[k], e_l = est[k];
+            if (BIASED && lane < cnt) bs += blog[k];
+            for (int x = 0; x < cnt; x += kB) {
+                vec p[kB][G];
+#pragma unroll
+                for (int a = 0; a < kB; ++a) {
+                    const T *prow = pu + (int64_t)readlane(uu, x + a < cnt ? x + a : cnt - 1) * ldu;
+#pragma unroll
+                    for (int v = 0; v < G; ++v) p[a][v] = *(const vec *)(prow + cu[v]);
+                }
+#pragma unroll
+                for (int a = 0; a < kB; ++a) {
+                    if (x + a >= cnt) break;
+                    const T r = readlane(r_l, x + a), e = readlane(e_l, x + a);
+#pragma unroll
+                    for (int v = 0; v < G; ++v) {  // mf.pyx:712-716 (item side)
+                        in[v] += p[a][v] * r;
+                        id[v] += p[a][v] * e;
+                    }
+                }
+            }
+        }
+        const T nreg = (T)N * reg_qi;  // mf.pyx:726-730
+        T *qrow = qb + i * (int64_t)ldq;
+#pragma unroll
+        for (int v = 0; v < G; ++v) {
+            const int c0 = (lane + kWave * v) * W;
+#pragma unroll
+            for (int e = 0; e < W; ++e) {
+                const int c = c0 + e;
+                if (c < K) {
+                    const T qf = qrow[c];
+                    const T den = L::get(id[v], e) + nreg * qf;
+                    qrow[c] = qf * (L::get(in[v], e) / den);
+                }
+            }
+        }
+        if (BIASED) {
+            const T tot = wave_sum(bs);
+            if (lane == 0) {
+                double w = 1.0;
+                if (count_rule && N > 1) w = -expm1(N * log1p(-eta_b)) / (N * eta_b);
+                qrow[K] += (T)w * tot;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- baseline ALS (8(f) 4)
+//
+// baseline_als (optimize_baselines.pyx:14-54): per epoch every item's bias from the current user
+// biases, then every user's bias from the new item biases.  One wave per item / user, lanes
+// over its ratings, one wave sum.
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void als_item_kernel(
+    const int64_t *__restrict__ csc_ptr, const int64_t *__restrict__ csc_pos,
+    const int32_t *__restrict__ row_user, const T *__restrict__ ratings, const T *__restrict__ bu,
+    T *__restrict__ bi, int n_items, T gm, T reg_i)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    for (int64_t i = wave; i < n_items; i += n_waves) {
+        const int64_t b = csc_ptr[i];
+        const int N = (int)(csc_ptr[i + 1] - b);
+        T dev = T(0);
+        for (int x = lane; x < N; x += kWave) {
+            const int64_t k = csc_pos[b + x];
+            dev += ratings[k] - gm - bu[row_user[k]];  // :43-44
+        }
+        dev = wave_sum(dev);
+        if (lane == 0) bi[i] = dev / (reg_i + (T)N);  // :46
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void als_user_kernel(
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
+    const T *__restrict__ ratings, const T *__restrict__ bi, T *__restrict__ bu, int n_users, T gm,
+    T reg_u)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    for (int64_t u = wave; u < n_users; u += n_waves) {
+        const int64_t s = row_ptr[u];
+        const int n = (int)(row_ptr[u + 1] - s);
+        T dev = T(0);
+        for (int x = lane; x < n; x += kWave) dev += ratings[s + x] - gm - bi[items[s + x]];  // :50-51
+        dev = wave_sum(dev);
+        if (lane == 0) bu[u] = dev / (reg_u + (T)n);  // :52
+    }
+}
+
 // ---------------------------------------------------------------- inference
 
 template <typename T, int V>
@@ -1076,7 +1324,7 @@ int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const v
     if (!sched || !pu || !bu || !qb || !hp) return set_err(MF_E_ARG, "null argument");
     if (dtype != MF_F32 && dtype != MF_F64) return set_err(MF_E_ARG, "bad dtype");
     const int maxk = dtype == MF_F32 ? MF_MAX_FACTORS_F32 : MF_MAX_FACTORS_F64;
-    if (K < 1 || K > maxk) return set_err(MF_E_ARG, "n_factors out of range");
+    if (K < 0 || K > maxk) return set_err(MF_E_ARG, "n_factors out of range");
     if (ldu < K || ldq < K + 1) return set_err(MF_E_ARG, "need ldu >= n_factors, ldq >= n_factors+1");
     if (mode < MF_MODE_PLAIN || mode > MF_MODE_LOG) return set_err(MF_E_ARG, "bad mode");
     if (mode == MF_MODE_LOG && !qlog) return set_err(MF_E_ARG, "MF_MODE_LOG needs qlog");
@@ -1297,6 +1545,99 @@ int mf_item_apply(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
     return check_launch("item_apply_kernel");
 }
 
+int mf_nmf_user_pass(const mf_csr_t *csr, const void *pu, void *pu_next, void *bu, int32_t ldu,
+                     const void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
+                     const mf_hyper_t *hp, void *est, void *blog, int32_t dtype, void *stream)
+{
+    if (!csr || !csr->row_ptr || !csr->items || !csr->ratings) return set_err(MF_E_ARG, "null csr");
+    if (!pu || !pu_next || !qb || !hp || !est || (biased && (!bu || !blog)))
+        return set_err(MF_E_ARG, "null argument");
+    if (n_factors < 1 || ldu < n_factors || ldq < n_factors + 1)
+        return set_err(MF_E_ARG, "need ldu >= n_factors >= 1, ldq >= n_factors+1");
+    if (csr->n_users <= 0) return 0;
+    const int g = grid_for_waves(default_waves(csr->n_users));
+    hipStream_t st = (hipStream_t)stream;
+    auto run = [&](auto tag_t) -> int {
+        using T = decltype(tag_t);
+        return dispatch_g<T>(ldq, [&](auto gc) -> int {
+            constexpr int G = decltype(gc)::value;
+            auto k = biased ? nmf_user_kernel<T, G, true> : nmf_user_kernel<T, G, false>;
+            hipLaunchKernelGGL(k, dim3(g), dim3(kBlock), 0, st, csr->row_ptr, csr->items,
+                               (const T *)csr->ratings, csr->n_users, (const T *)pu, (T *)pu_next,
+                               (T *)bu, ldu, (const T *)qb, ldq, n_factors, (T)hp->reg_pu,
+                               (T)hp->lr_bu, (T)hp->reg_bu, (T)hp->lr_bi, (T)hp->reg_bi,
+                               (T)hp->global_mean, (T *)est, (T *)blog);
+            return check_launch("nmf_user_kernel");
+        });
+    };
+    if (dtype == MF_F32) return run(float{});
+    if (dtype == MF_F64) return run(double{});
+    return set_err(MF_E_ARG, "bad dtype");
+}
+
+int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32_t *row_user,
+                     const void *ratings, const void *est, const void *blog, const void *pu,
+                     int32_t ldu, void *qb, int32_t ldq, int32_t n_items, int32_t n_factors,
+                     int32_t biased, const mf_hyper_t *hp, int32_t rule, int32_t dtype,
+                     void *stream)
+{
+    if (!csc_ptr || !csc_pos || !row_user || !ratings || !est || !pu || !qb || !hp ||
+        (biased && !blog))
+        return set_err(MF_E_ARG, "null argument");
+    if (n_factors < 1 || ldu < n_factors || ldq < n_factors + 1)
+        return set_err(MF_E_ARG, "need ldu >= n_factors >= 1, ldq >= n_factors+1");
+    if (rule != MF_MERGE_SUM && rule != MF_MERGE_COUNT) return set_err(MF_E_ARG, "bad merge rule");
+    if (n_items <= 0) return 0;
+    const int g = grid_for_waves(default_waves(n_items));
+    hipStream_t st = (hipStream_t)stream;
+    const double eta_b = hp->lr_bi * (1.0 + hp->reg_bi);
+    auto run = [&](auto tag_t) -> int {
+        using T = decltype(tag_t);
+        return dispatch_g<T>(ldq, [&](auto gc) -> int {
+            constexpr int G = decltype(gc)::value;
+            auto k = biased ? nmf_item_kernel<T, G, true> : nmf_item_kernel<T, G, false>;
+            hipLaunchKernelGGL(k, dim3(g), dim3(kBlock), 0, st, csc_ptr, csc_pos, row_user,
+                               (const T *)ratings, (const T *)est, (const T *)blog, (const T *)pu,
+                               ldu, (T *)qb, ldq, n_factors, n_items, (T)hp->reg_qi, eta_b,
+                               rule == MF_MERGE_COUNT);
+            return check_launch("nmf_item_kernel");
+        });
+    };
+    if (dtype == MF_F32) return run(float{});
+    if (dtype == MF_F64) return run(double{});
+    return set_err(MF_E_ARG, "bad dtype");
+}
+
+int mf_baseline_als_epoch(const mf_csr_t *csr, const int64_t *csc_ptr, const int64_t *csc_pos,
+                          const int32_t *row_user, void *bu, void *bi, double global_mean,
+                          double reg_u, double reg_i, int32_t dtype, void *stream)
+{
+    if (!csr || !csr->row_ptr || !csr->items || !csr->ratings) return set_err(MF_E_ARG, "null csr");
+    if (!csc_ptr || !csc_pos || !row_user || !bu || !bi) return set_err(MF_E_ARG, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    const int gi = grid_for_waves(default_waves(csr->n_items > 0 ? csr->n_items : 1));
+    const int gu = grid_for_waves(default_waves(csr->n_users > 0 ? csr->n_users : 1));
+    auto run = [&](auto tag_t) -> int {
+        using T = decltype(tag_t);
+        if (csr->n_items > 0) {
+            hipLaunchKernelGGL(als_item_kernel<T>, dim3(gi), dim3(kBlock), 0, st, csc_ptr, csc_pos,
+                               row_user, (const T *)csr->ratings, (const T *)bu, (T *)bi,
+                               csr->n_items, (T)global_mean, (T)reg_i);
+            if (int rc = check_launch("als_item_kernel")) return rc;
+        }
+        if (csr->n_users > 0) {
+            hipLaunchKernelGGL(als_user_kernel<T>, dim3(gu), dim3(kBlock), 0, st, csr->row_ptr,
+                               csr->items, (const T *)csr->ratings, (const T *)bi, (T *)bu,
+                               csr->n_users, (T)global_mean, (T)reg_u);
+            if (int rc = check_launch("als_user_kernel")) return rc;
+        }
+        return 0;
+    };
+    if (dtype == MF_F32) return run(float{});
+    if (dtype == MF_F64) return run(double{});
+    return set_err(MF_E_ARG, "bad dtype");
+}
+
 int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, const void *bu,
                int32_t ldu, const void *qb, int32_t ldq, const void *imp, int32_t n_factors,
                int32_t biased, double global_mean, void *est, int32_t *impossible, int32_t dtype,
@@ -1305,7 +1646,7 @@ int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, co
     if (n <= 0) return 0;
     if (!u || !i || !pu || !bu || !qb || !est || !impossible)
         return set_err(MF_E_ARG, "null argument");
-    if (n_factors < 1 || ldu < n_factors || ldq < n_factors + 1)
+    if (n_factors < 0 || ldu < n_factors || ldq < n_factors + 1)
         return set_err(MF_E_ARG, "need ldu >= n_factors, ldq >= n_factors+1");
     const int64_t waves = default_waves(n);
     hipStream_t st = (hipStream_t)stream;

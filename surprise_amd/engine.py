@@ -79,11 +79,12 @@ class MFEngine(ItemSync):
             torch.device(device)
         self.dtype = _lib.MF_F64 if str(dtype) in ("float64", "f64", "double") else _lib.MF_F32
         self.tdt = torch.float64 if self.dtype == _lib.MF_F64 else torch.float32
-        if n_factors < 1 or n_factors > _lib.MAX_FACTORS[self.dtype]:
-            raise ValueError(f"n_factors must be in [1, {_lib.MAX_FACTORS[self.dtype]}] "
+        if n_factors < 0 or n_factors > _lib.MAX_FACTORS[self.dtype]:
+            raise ValueError(f"n_factors must be in [0, {_lib.MAX_FACTORS[self.dtype]}] "
                              f"for {dtype}, got {n_factors}")
         self.K = int(n_factors)
-        self.ld = int(ld) if ld else default_ld(self.K, self.dtype)
+        # (n_factors = 0 -- the biases alone, baseline_sgd -- still gets a non-empty user row)
+        self.ld = int(ld) if ld else (default_ld(self.K, self.dtype) if self.K else 16)
         self.ldq = default_ldq(self.K, self.dtype)
         row_ptr, items, ratings = csr
         row_ptr = np.asarray(row_ptr, np.int64)
@@ -393,3 +394,124 @@ def _has_duplicate_items(row_ptr, items) -> bool:
     users = np.repeat(np.arange(len(row_ptr) - 1, dtype=np.int64), np.diff(row_ptr))
     key = users * (int(np.max(items)) + 1) + np.asarray(items, np.int64)
     return len(np.unique(key)) != len(key)
+
+
+class NMFEngine:
+    """NMF.sgd on one GPU (matrix_factorization.pyx:646-735): per epoch mf_nmf_user_pass then
+    mf_nmf_item_pass, then the user-factor buffers swap.  Layout as MFEngine: pu / pu_next
+    T[U, ldu], qb T[I, ldq] = [q_i | b_i | 0..], bu T[U]; per rating est T[nnz] (and the item-bias
+    step blog T[nnz] when biased); the item-major view csc_ptr / csc_pos / row_user."""
+
+    def __init__(self, csr, csc, n_items, n_factors, *, hyper, biased=False, dtype="float32",
+                 device=None, bias_rule="count"):
+        torch = _lib.require_gpu()
+        self.torch = torch
+        self.dev = torch.device("cuda", torch.cuda.current_device()) if device is None else \
+            torch.device(device)
+        self.dtype = _lib.MF_F64 if str(dtype) in ("float64", "f64", "double") else _lib.MF_F32
+        self.tdt = torch.float64 if self.dtype == _lib.MF_F64 else torch.float32
+        if n_factors < 1 or n_factors > _lib.MAX_FACTORS[self.dtype]:
+            raise ValueError(f"n_factors must be in [1, {_lib.MAX_FACTORS[self.dtype]}] "
+                             f"for {dtype}, got {n_factors}")
+        self.K = int(n_factors)
+        self.ld = default_ld(self.K, self.dtype)
+        self.ldq = default_ldq(self.K, self.dtype)
+        self.biased = bool(biased)
+        row_ptr, items, ratings = csr
+        row_ptr = np.asarray(row_ptr, np.int64)
+        self.n_users, self.n_items = len(row_ptr) - 1, int(n_items)
+        self.stream = torch.cuda.current_stream(self.dev)
+        to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev)
+        self.row_ptr = to_dev(row_ptr)
+        self.items = to_dev(np.asarray(items, np.int32))
+        self.ratings = to_dev(np.asarray(ratings, np.float64)).to(self.tdt)
+        self._csr = _lib.MfCsr(self.row_ptr.data_ptr(), self.items.data_ptr(),
+                               self.ratings.data_ptr(), self.n_users, self.n_items)
+        csc_ptr, csc_pos = csc
+        self.csc_ptr = to_dev(np.asarray(csc_ptr, np.int64))
+        self.csc_pos = to_dev(np.asarray(csc_pos, np.int64))
+        self.row_user = to_dev(np.repeat(np.arange(self.n_users, dtype=np.int32),
+                                         np.diff(row_ptr)))
+        z = lambda *shape: torch.zeros(*shape, dtype=self.tdt, device=self.dev)
+        nnz = max(len(items), 1)
+        self.pu, self.pu_next = z(self.n_users, self.ld), z(self.n_users, self.ld)
+        self.bu, self.qb = z(self.n_users), z(self.n_items, self.ldq)
+        self.est = z(nnz)
+        self.blog = z(nnz) if self.biased else None
+        self._hyper = _lib.MfHyper(**hyper)
+        if not self.biased:
+            self._hyper.global_mean = 0.0  # mf.pyx:682-683
+        self.rule = _lib.MF_MERGE_COUNT if bias_rule == "count" else _lib.MF_MERGE_SUM
+
+    def _ptr(self, t):
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+    def set_factors(self, pu, qi):
+        K, t = self.K, self.torch
+        self.pu.zero_()
+        self.pu[:, :K].copy_(t.from_numpy(np.ascontiguousarray(pu, np.float64)).to(self.dev, self.tdt))
+        self.qb.zero_()
+        self.qb[:, :K].copy_(t.from_numpy(np.ascontiguousarray(qi, np.float64)).to(self.dev, self.tdt))
+        self.bu.zero_()
+
+    def epoch(self):
+        st = ctypes.c_void_p(self.stream.cuda_stream)
+        _lib.call("mf_nmf_user_pass", ctypes.byref(self._csr), self._ptr(self.pu),
+                  self._ptr(self.pu_next), self._ptr(self.bu), self.ld, self._ptr(self.qb),
+                  self.ldq, self.K, int(self.biased), ctypes.byref(self._hyper),
+                  self._ptr(self.est), self._ptr(self.blog), self.dtype, st)
+        _lib.call("mf_nmf_item_pass", self._ptr(self.csc_ptr), self._ptr(self.csc_pos),
+                  self._ptr(self.row_user), self._ptr(self.ratings), self._ptr(self.est),
+                  self._ptr(self.blog), self._ptr(self.pu), self.ld, self._ptr(self.qb),
+                  self.ldq, self.n_items, self.K, int(self.biased), ctypes.byref(self._hyper),
+                  self.rule, self.dtype, st)
+        self.pu, self.pu_next = self.pu_next, self.pu
+
+    def get_factors(self):
+        self.stream.synchronize()
+        K = self.K
+        h = lambda x: x.to(self.torch.float64).cpu().numpy()
+        return dict(pu=h(self.pu[:, :K]), qi=h(self.qb[:, :K]), bu=h(self.bu),
+                    bi=h(self.qb[:, K]))
+
+    def predict(self, u, i, global_mean):
+        """Batched estimate (the SVD formula, mf.pyx:737-759) -> (est fp64, impossible bool)."""
+        t = self.torch
+        n = len(u)
+        du = t.from_numpy(np.ascontiguousarray(u, np.int32)).to(self.dev)
+        di = t.from_numpy(np.ascontiguousarray(i, np.int32)).to(self.dev)
+        est = t.zeros(n, dtype=self.tdt, device=self.dev)
+        bad = t.zeros(n, dtype=t.int32, device=self.dev)
+        _lib.call("mf_predict", n, self._ptr(du), self._ptr(di), self._ptr(self.pu),
+                  self._ptr(self.bu), self.ld, self._ptr(self.qb), self.ldq, None, self.K,
+                  int(self.biased), float(global_mean), self._ptr(est), self._ptr(bad),
+                  self.dtype, ctypes.c_void_p(self.stream.cuda_stream))
+        self.stream.synchronize()
+        return est.to(t.float64).cpu().numpy(), bad.cpu().numpy().astype(bool)
+
+
+def baseline_als_device(csr, csc, n_items, global_mean, n_epochs, reg_u, reg_i,
+                        dtype="float64"):
+    """baseline_als (optimize_baselines.pyx:14-54) on the device; returns fp64 (bu, bi)."""
+    torch = _lib.require_gpu()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    dt = _lib.MF_F64 if str(dtype) in ("float64", "f64", "double") else _lib.MF_F32
+    tdt = torch.float64 if dt == _lib.MF_F64 else torch.float32
+    row_ptr, items, ratings = csr
+    row_ptr = np.asarray(row_ptr, np.int64)
+    n_users = len(row_ptr) - 1
+    to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    rp, it = to_dev(row_ptr), to_dev(np.asarray(items, np.int32))
+    rt = to_dev(np.asarray(ratings, np.float64)).to(tdt)
+    cp, cs = to_dev(np.asarray(csc[0], np.int64)), to_dev(np.asarray(csc[1], np.int64))
+    ru = to_dev(np.repeat(np.arange(n_users, dtype=np.int32), np.diff(row_ptr)))
+    bu = torch.zeros(n_users, dtype=tdt, device=dev)
+    bi = torch.zeros(n_items, dtype=tdt, device=dev)
+    c = _lib.MfCsr(rp.data_ptr(), it.data_ptr(), rt.data_ptr(), n_users, int(n_items))
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    p = lambda x: ctypes.c_void_p(x.data_ptr())
+    for _ in range(n_epochs):
+        _lib.call("mf_baseline_als_epoch", ctypes.byref(c), p(cp), p(cs), p(ru), p(bu), p(bi),
+                  float(global_mean), float(reg_u), float(reg_i), dt, st)
+    torch.cuda.current_stream(dev).synchronize()
+    return bu.to(torch.float64).cpu().numpy(), bi.to(torch.float64).cpu().numpy()

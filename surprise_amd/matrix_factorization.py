@@ -275,3 +275,81 @@ class SVDpp(_MFBase):
         if self._imp is None:
             self._imp = self._engine.user_implicit()
         return self._engine.predict(u, i, self.trainset.global_mean, imp=self._imp)
+
+
+def _as_trainset(trainset):
+    """Our Trainset for a reference (dict-of-lists) surprise.Trainset, duck-typed."""
+    if isinstance(trainset, Trainset):
+        return trainset
+    return Trainset(trainset.ur, trainset.ir, trainset.n_users, trainset.n_items,
+                    trainset.n_ratings, trainset.rating_scale, trainset.offset, {}, {})
+
+
+class NMF(_MFBase):
+    """Non-negative MF trained on the GPU (matrix_factorization.pyx:525-759).
+
+    Same constructor arguments and defaults as the reference (:628-644), same
+    ``rng.uniform`` initialisation draws (pu then qi, :673-677), same attributes.  An
+    epoch is two race-free HIP passes (include/surprise_amd.h, mf_nmf_user_pass /
+    mf_nmf_item_pass): unbiased, this is the reference's arithmetic up to summation
+    order; biased, the item biases follow the delta-log schedule (epoch-start snapshot,
+    count-aware merge).  Keyword-only device option: ``dtype``."""
+
+    _algo = "nmf"
+
+    def __init__(self, n_factors=15, n_epochs=50, biased=False, reg_pu=.06, reg_qi=.06,
+                 reg_bu=.02, reg_bi=.02, lr_bu=.005, lr_bi=.005, init_low=0, init_high=1,
+                 random_state=None, verbose=False, *, dtype="float32"):
+        self.n_factors = n_factors
+        self.n_epochs = n_epochs
+        self.biased = biased
+        self.reg_pu = reg_pu
+        self.reg_qi = reg_qi
+        self.lr_bu = lr_bu
+        self.lr_bi = lr_bi
+        self.reg_bu = reg_bu
+        self.reg_bi = reg_bi
+        self.init_low = init_low
+        self.init_high = init_high
+        self.random_state = random_state
+        self.verbose = verbose
+        if self.init_low < 0:
+            raise ValueError('init_low should be greater than zero')
+        self._device_options(dtype, "auto", 1, False, 0, False)
+        AlgoBase.__init__(self)
+
+    def fit(self, trainset):
+        AlgoBase.fit(self, trainset)
+        self.sgd(trainset)
+        return self
+
+    def sgd(self, trainset):
+        """mf.pyx:646-735 on the device."""
+        from .engine import NMFEngine
+
+        _lib.require_gpu()
+        ts = _as_trainset(trainset)
+        rng = get_rng(self.random_state)
+        n_users, n_items, K = trainset.n_users, trainset.n_items, self.n_factors
+        pu = rng.uniform(self.init_low, self.init_high, size=(n_users, K))
+        qi = rng.uniform(self.init_low, self.init_high, size=(n_items, K))
+        hyper = dict(lr_bu=self.lr_bu, lr_bi=self.lr_bi, reg_bu=self.reg_bu, reg_bi=self.reg_bi,
+                     reg_pu=self.reg_pu, reg_qi=self.reg_qi,
+                     global_mean=float(self.trainset.global_mean))
+        eng = NMFEngine(ts.csr(), ts.csc(), n_items, K, hyper=hyper, biased=self.biased,
+                        dtype=self.dtype)
+        eng.set_factors(pu, qi)
+        for e in range(self.n_epochs):
+            if self.verbose:
+                print("Processing epoch {}".format(e))
+            eng.epoch()
+        f = eng.get_factors()
+        self._engine = eng
+        self.bu, self.bi, self.pu, self.qi = f["bu"], f["bi"], f["pu"], f["qi"]
+
+    def estimate(self, u, i):
+        """mf.pyx:737-759 (host numpy fp64, per call)."""
+        return SVD.estimate(self, u, i)
+
+    def _predict_inner(self, u, i):
+        return self._engine.predict(u, i, self.trainset.global_mean if self.biased else 0.0)

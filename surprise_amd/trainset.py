@@ -51,6 +51,7 @@ class Trainset:
         self._inner2raw_id_items = None
         self._csr = None
         self._raw_pos = None  # position of each CSR entry in the raw (insertion) order
+        self._dict_built = ur is not None and ir is not None
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -137,6 +138,27 @@ class Trainset:
                 ir[il[x]].append((ul[x], rl[x]))
             self._ir = ir
         return self._ir
+
+    def csc(self):
+        """(item_ptr int64[n_items+1], pos int64[nnz]): for every item, the CSR positions of its
+        ratings in ``ir[i]``'s list order (raw insertion order, trainset.py:37-54)."""
+        row_ptr, items, _ = self.csr()
+        if self._dict_built and self._raw_pos is None:
+            # dict-built: follow ir's lists, locating each (u, i) in the CSR
+            users = np.repeat(np.arange(self.n_users, dtype=np.int64), np.diff(row_ptr))
+            key = users * self.n_items + np.asarray(items, np.int64)
+            srt = np.argsort(key, kind="stable")
+            pos, ptr = [], [0]
+            for i in range(self.n_items):
+                for u, _ in self._ir.get(i, []):
+                    pos.append(srt[np.searchsorted(key[srt], u * self.n_items + i)])
+                ptr.append(len(pos))
+            return np.asarray(ptr, np.int64), np.asarray(pos, np.int64)
+        pos = self._raw_pos if self._raw_pos is not None else np.arange(len(items))
+        order = np.lexsort((pos, items))  # by item, then raw insertion order
+        ptr = np.zeros(self.n_items + 1, np.int64)
+        np.cumsum(np.bincount(items, minlength=self.n_items), out=ptr[1:])
+        return ptr, order.astype(np.int64)
 
     def knows_user(self, uid):
         """trainset.py:62-74: ``uid in ur``."""

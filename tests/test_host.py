@@ -232,3 +232,17 @@ def test_fit_without_gpu_fails_loudly(u1):
     ts, _ = u1
     with pytest.raises(SurpriseAMDError):
         SVD(n_factors=2, n_epochs=1).fit(ts)
+
+
+def test_nmf_and_baseline_argument_errors():
+    """test_NMF.py (init_low < 0) and test_bsl_options.py (unknown method): raised before any
+    device work."""
+    import pytest
+    from surprise_amd import NMF, BaselineOnly, Trainset
+    with pytest.raises(ValueError):
+        NMF(n_factors=1, n_epochs=1, init_low=-1, random_state=1)
+    ts = Trainset.from_csr(np.array([0, 1], np.int64), np.array([0], np.int32),
+                           np.array([3.0]), 1)
+    algo = BaselineOnly(bsl_options={"method": "wrong_name"})
+    with pytest.raises(ValueError, match="Invalid method wrong_name"):
+        algo.fit(ts)

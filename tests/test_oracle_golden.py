@@ -288,3 +288,69 @@ def test_deltalog_one_chunk_within_1e3_of_reference(golden, u1, name):
     P, f = run_oracle_log("SVD", case["params"], row_ptr, items, ratings, ts.n_items,
                           ts.global_mean)
     assert abs(_oracle_test_rmse(P, f, "SVD", ts, list(test))[1] - case["rmse"]) < 1e-3
+
+
+# ----------------------------------------------------------------------------- NMF, baselines
+
+@pytest.fixture(scope="module")
+def golden_ext():
+    import json
+    with open(os.path.join(GOLDEN, "golden_ext.json")) as f:
+        meta = json.load(f)
+    return meta, dict(np.load(os.path.join(GOLDEN, "golden_ext_arrays.npz")))
+
+
+def run_oracle_nmf(params, ts):
+    """NMF.__init__ defaults (mf.pyx:628-644) + NMF.sgd via the oracle."""
+    p = dict(n_factors=15, n_epochs=50, biased=False, reg_pu=.06, reg_qi=.06, reg_bu=.02,
+             reg_bi=.02, lr_bu=.005, lr_bi=.005, init_low=0, init_high=1, random_state=None)
+    p.update(params)
+    rng = get_rng(p["random_state"])
+    pu = rng.uniform(p["init_low"], p["init_high"], size=(ts.n_users, p["n_factors"]))
+    qi = rng.uniform(p["init_low"], p["init_high"], size=(ts.n_items, p["n_factors"]))
+    row_ptr, items, ratings = ts.csr()
+    pu, qi, bu, bi = orc.nmf_sgd(row_ptr, items, ratings, ts.n_items, p["n_factors"],
+                                 p["n_epochs"], p["biased"], ts.global_mean, pu, qi,
+                                 *[p[k] for k in ("reg_pu", "reg_qi", "reg_bu", "reg_bi", "lr_bu",
+                                                  "lr_bi")])
+    return p, dict(pu=pu, qi=qi, bu=bu, bi=bi)
+
+
+def run_oracle_bsl(bsl_options, ts):
+    """BaselineOnly.fit -> compute_baselines (algo_base.py:220-254) via the oracle."""
+    row_ptr, items, ratings = ts.csr()
+    method = bsl_options.get("method", "als")
+    if method == "als":
+        ptr, pos = ts.csc()
+        return orc.baseline_als(row_ptr, items, ratings, ts.n_items, ptr, pos, ts.global_mean,
+                                bsl_options.get("n_epochs", 10), bsl_options.get("reg_u", 15),
+                                bsl_options.get("reg_i", 10))
+    lr, reg = bsl_options.get("learning_rate", .005), bsl_options.get("reg", .02)
+    hp = orc.hyper(lr_bu=lr, lr_bi=lr, reg_bu=reg, reg_bi=reg)
+    _, _, bu, bi = orc.svd_sgd(row_ptr, items, ratings, ts.n_items, 0,
+                               bsl_options.get("n_epochs", 20), True, ts.global_mean, hp,
+                               np.zeros((ts.n_users, 0)), np.zeros((ts.n_items, 0)))
+    return bu, bi
+
+
+@pytest.mark.parametrize("name", ["nmf_default", "nmf_k5_e3", "nmf_k8_e5_hyper",
+                                  "nmf_biased_k10_e10", "nmf_biased_k4_e3"])
+def test_nmf_oracle_bit_exact(golden_ext, u1, name):
+    meta, _ = golden_ext
+    case = meta["cases"][name]
+    ts, test = u1
+    p, f = run_oracle_nmf(case["params"], ts)
+    assert _sha(f["pu"], f["qi"]) == case["sha_pu_qi"]
+    assert _sha(f["bu"], f["bi"]) == case["sha_bu_bi"]
+
+
+@pytest.mark.parametrize("name", ["bsl_als_default", "bsl_als_e3_reg", "bsl_sgd_default",
+                                  "bsl_sgd_hyper"])
+def test_baseline_oracle(golden_ext, u1, name):
+    """baseline_sgd is bit-exact (SVD with no factors); baseline_als sums ir[i] in the reference's
+    list order, bit-exact as well."""
+    meta, arr = golden_ext
+    case = meta["cases"][name]
+    ts, _ = u1
+    bu, bi = run_oracle_bsl(case["params"]["bsl_options"], ts)
+    assert _sha(bu, bi) == case["sha_bu_bi"]
