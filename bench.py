@@ -38,6 +38,9 @@ def parse():
     p.add_argument("--shape", default="ml-1m")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rmse", action="store_true")
+    p.add_argument("--backend", default="nccl",
+                   help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
+                        "several ranks on one GPU)")
     return p.parse_args()
 
 
@@ -62,10 +65,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend != "nccl":  # rehearsal: several ranks may share the box's one GPU
+        local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     ctx = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
         ctx = DistContext()
 
     u, i, r = synthetic.shape(args.shape)
@@ -87,6 +95,8 @@ def main():
         eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, algo=args.algo, hyper=hyper,
                        mode=mode, n_chunks=args.chunks, world=world)
         eng.set_factors(pu, qi, yj=yj)
+        # global per-item rating counts (all ranks) for the count-aware item fold
+        eng._prepare(ctx)
         return eng
 
     eng = make_engine()

@@ -3,28 +3,61 @@
 ``hipcc`` cross-compiles without a GPU, so this runs in the CPU container too.
 The output lives next to this file so it travels with the repo snapshot to the
 GPU box (it is git-ignored, not gpurun-ignored).
+
+csrc/mf_kernels.hip is compiled as 13 translation units in parallel: the main unit (every
+kernel but the SGD epoch kernel, the C ABI) and one unit per (dtype, mode, SVD/SVD++) holding
+that combination's epoch-kernel instantiations (-DMF_TU_EPOCH, see the top of the file).
 """
 from __future__ import annotations
 
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(_HERE, "csrc", "mf_kernels.hip")
 HDR = os.path.join(os.path.dirname(_HERE), "include", "surprise_amd.h")
 OUT = os.path.join(_HERE, "libsurprise_amd.so")
+OBJ_DIR = os.path.join(_HERE, "csrc", "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SURPRISE_AMD_ARCH", "gfx950")
+FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"]
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    newest = max(os.path.getmtime(SRC), os.path.getmtime(HDR))
+def units():
+    """(object name, extra defines) of every translation unit."""
+    out = [("main", [])]
+    for t in ("float", "double"):
+        for m in (0, 1, 2):  # MF_MODE_PLAIN, MF_MODE_ATOMIC, MF_MODE_LOG
+            for pp in (0, 1):
+                out.append((f"epoch_{t}_m{m}_pp{pp}",
+                            ["-DMF_TU_EPOCH", f"-DMF_INST_T={t}", f"-DMF_INST_M={m}",
+                             f"-DMF_INST_PP={pp}", "-Wno-unused-function",
+                             "-Wno-unused-const-variable"]))
+    return out
+
+
+def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -> str:
+    newest = max(os.path.getmtime(SRC), os.path.getmtime(HDR), os.path.getmtime(__file__))
     if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= newest:
         return OUT
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-o", OUT + ".tmp", SRC]
+    os.makedirs(OBJ_DIR, exist_ok=True)
+
+    def compile_one(u):
+        name, defs = u
+        obj = os.path.join(OBJ_DIR, name + ".o")
+        cmd = [HIPCC, *FLAGS, *defs, "-c", "-o", obj, SRC]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = jobs or min(len(units()), max(1, min(os.cpu_count() or 1, 16)))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, units()))
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(OUT + ".tmp", OUT)
     return OUT

@@ -28,6 +28,18 @@
 
 #include "../../include/surprise_amd.h"
 
+// Build layout: this file is compiled once as the main translation unit (everything but the
+// epoch kernels) and once per (dtype, mode, SVD/SVD++) with -DMF_TU_EPOCH -DMF_INST_T=...
+// -DMF_INST_M=... -DMF_INST_PP=..., each of those defining only mf_ext::launch_epoch_tm for
+// its combination (surprise_amd/build.py compiles the units in parallel and links them).
+namespace mf_ext {
+extern thread_local char g_err[256];
+template <typename T, int M, bool PP>
+int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
+                    int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, int32_t K,
+                    int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, void *stream);
+}  // namespace mf_ext
+
 namespace {
 
 constexpr int kWave = 64;
@@ -38,7 +50,7 @@ constexpr int kBlock = 256;  // 4 waves per workgroup
 constexpr int kPF = MF_PF;   // item rows gathered ahead of use
 
 
-thread_local char g_err[256] = "";
+using mf_ext::g_err;
 
 int set_err(int code, const char *msg) {
     snprintf(g_err, sizeof(g_err), "%s (code %d)", msg, code);
@@ -52,6 +64,25 @@ int check_launch(const char *what) {
         return (int)e;
     }
     return 0;
+}
+
+int grid_for_waves(int64_t waves) {
+    int64_t blocks = (waves * kWave + kBlock - 1) / kBlock;
+    if (blocks < 1) blocks = 1;
+    return (int)blocks;
+}
+
+// G = 8-byte lane groups per row = ceil(ld * sizeof(T) / 512) (the epoch kernel's layout)
+template <typename T, typename F>
+int dispatch_g(int ld, F &&f)
+{
+    const int g = (int)(((int64_t)ld * sizeof(T) + 511) / 512);
+    if (g <= 1) return f(std::integral_constant<int, 1>{});
+    if (g <= 2) return f(std::integral_constant<int, 2>{});
+    if (g <= 3) return f(std::integral_constant<int, 3>{});
+    if (g <= 4) return f(std::integral_constant<int, 4>{});
+    if (g <= 5) return f(std::integral_constant<int, 5>{});
+    return set_err(MF_E_ARG, "n_factors/ld too large");
 }
 
 template <typename T>
@@ -487,6 +518,7 @@ __device__ __forceinline__ void epoch_body(
         for (int v = 0; v < G; ++v) p[v] = L::template ld<0>(p_rs, cu[v]) + one[v];
         T bu_u = Buf<T>::template ld<0>(b_rs, 0);
         const T sqrt_n = sqrt(T(n));  // mf.pyx:470
+        const T rs_n = T(1) / sqrt_n;  // one division per user; the terms are multiplied
 
         // SVD++: walk the user's y_j rows: 64 item ids per vector load (lane l holds entry
         // x0 + l, read back with v_readlane), rows gathered kYB at a time; rows past the user's
@@ -512,9 +544,9 @@ __device__ __forceinline__ void epoch_body(
             }
         };
         // SVD++ (1): u_impl = sum_{j in I_u} y_j / sqrt|I_u|  (mf.pyx:473-476, per-term division)
-        vec imp[G], cacc[G];
+        vec imp[G], imp0[G];
 #pragma unroll
-        for (int v = 0; v < G; ++v) imp[v] = cacc[v] = L::splat(T(0));
+        for (int v = 0; v < G; ++v) imp[v] = L::splat(T(0));
         if (PP) {
             T imp1[U];
 #pragma unroll
@@ -523,10 +555,12 @@ __device__ __forceinline__ void epoch_body(
 #pragma unroll
                 for (int a = 0; a < kYB; ++a)
 #pragma unroll
-                    for (int u = 0; u < U; ++u) imp1[u] += g[a][u] / sqrt_n;
+                    for (int u = 0; u < U; ++u) imp1[u] += g[a][u] * rs_n;
             });
             to_lane8<G>(imp1, imp);
         }
+#pragma unroll
+        for (int v = 0; v < G; ++v) imp0[v] = imp[v];
         T A = T(1);
 
         // software pipeline: slot d holds the gathered row of rating j0 + d.  The item ids and
@@ -601,10 +635,8 @@ __device__ __forceinline__ void epoch_body(
                 qd[v] = err * dq_e[v] + dq_0[v];
                 const vec pn = err * dp_e[v] + dp_0[v];
                 p[v] = valid ? pn : p[v];
-                if (PP) {
-                    const vec cn = decay * cacc[v] + err * (dy_e[v] / sqrt_n);
+                if (PP) {  // imp' = decay imp + lr_yj err q (the c of y_j <- A y_j + c: below)
                     const vec in = decay * imp[v] + err * dy_e[v];
-                    cacc[v] = valid ? cn : cacc[v];
                     imp[v] = valid ? in : imp[v];
                 }
             }
@@ -677,6 +709,11 @@ __device__ __forceinline__ void epoch_body(
 
         // SVD++ (3): y_j <- A y_j + c for every j in I_u
         if (PP) {
+            // c obeys the same recurrence as imp (c' = decay c + lr_yj err q / sqrt n) from 0
+            // instead of imp0, so c = (imp - A imp0) / sqrt n: no per-rating c update
+            vec cacc[G];
+#pragma unroll
+            for (int v = 0; v < G; ++v) cacc[v] = (imp[v] - A * imp0[v]) * rs_n;
             T cacc1[U];
             to_lane1<G>(cacc, cacc1);
             walk_y([&](T (&g)[kYB][U], uint32_t (&ro)[kYB]) {
@@ -710,6 +747,39 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
 {
     epoch_body<T, G, MODE, PP, DUPS, kPF>(MF_EPOCH_ARGS);
 }
+
+}  // namespace
+
+#ifdef MF_TU_EPOCH
+namespace mf_ext {
+template <typename T, int M, bool PP>
+int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
+                    int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, int32_t K,
+                    int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, void *stream)
+{
+    return dispatch_g<T>(ldq, [&](auto gc) -> int {
+        constexpr int V = decltype(gc)::value;
+        // (kLog reads a snapshot: a repeated item sees the chunk-start row, no forwarding)
+        auto kern = (dups && M != kLog) ? mf_epoch_kernel<T, V, M, PP, true>
+                                        : mf_epoch_kernel<T, V, M, PP, false>;
+        hipLaunchKernelGGL(kern, dim3(grid_for_waves(waves)), dim3(kBlock), 0, (hipStream_t)stream,
+                           csr->row_ptr, csr->items, (const T *)csr->ratings, sched, n_sched,
+                           (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, (T *)qlog, K, biased,
+                           cast_hyper<T>(hp), csr->n_items, waves);
+        return check_launch(PP ? "mf_epoch_kernel<svdpp>" : "mf_epoch_kernel<svd>");
+    });
+}
+template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
+    const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
+    void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, void *);
+}  // namespace mf_ext
+#else  // the main translation unit
+
+namespace mf_ext {
+thread_local char g_err[256] = "";
+}
+
+namespace {
 
 
 // ---------------------------------------------------------------- item-table merge (epoch-chunk)
@@ -1261,12 +1331,6 @@ __global__ void wave_sum_selftest_kernel(const T *in, T *out, int n_waves)
 
 // ---------------------------------------------------------------- launch helpers
 
-int grid_for_waves(int64_t waves) {
-    int64_t blocks = (waves * kWave + kBlock - 1) / kBlock;
-    if (blocks < 1) blocks = 1;
-    return (int)blocks;
-}
-
 int n_cus() {
     static int n_cu = 0;
     if (n_cu == 0) {
@@ -1303,19 +1367,6 @@ int dispatch_v(int ld, F &&f)
     return set_err(MF_E_ARG, "n_factors/ld too large");
 }
 
-// G = 8-byte lane groups per row = ceil(ld * sizeof(T) / 512) (the epoch kernel's layout)
-template <typename T, typename F>
-int dispatch_g(int ld, F &&f)
-{
-    const int g = (int)(((int64_t)ld * sizeof(T) + 511) / 512);
-    if (g <= 1) return f(std::integral_constant<int, 1>{});
-    if (g <= 2) return f(std::integral_constant<int, 2>{});
-    if (g <= 3) return f(std::integral_constant<int, 3>{});
-    if (g <= 4) return f(std::integral_constant<int, 4>{});
-    if (g <= 5) return f(std::integral_constant<int, 5>{});
-    return set_err(MF_E_ARG, "n_factors/ld too large");
-}
-
 int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const void *bu,
                 const void *qb, const mf_hyper_t *hp, int K, int ldu, int ldq, int mode,
                 const void *qlog, int dtype)
@@ -1346,21 +1397,11 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
     if (PP && !yj) return set_err(MF_E_ARG, "null yj");
     if (n_sched <= 0) return 0;
     const int64_t waves = n_waves > 0 ? n_waves : default_waves(n_sched);
-    hipStream_t st = (hipStream_t)stream;
     auto run = [&](auto tag_t, auto mode_c) -> int {
         using T = decltype(tag_t);
         constexpr int M = decltype(mode_c)::value;
-        return dispatch_g<T>(ldq, [&](auto gc) -> int {
-            constexpr int V = decltype(gc)::value;
-            // (kLog reads a snapshot: a repeated item sees the chunk-start row, no forwarding)
-            auto kern = (dups && M != kLog) ? mf_epoch_kernel<T, V, M, PP, true>
-                                            : mf_epoch_kernel<T, V, M, PP, false>;
-            hipLaunchKernelGGL(kern, dim3(grid_for_waves(waves)), dim3(kBlock), 0, st,
-                               csr->row_ptr, csr->items, (const T *)csr->ratings, sched, n_sched,
-                               (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, (T *)qlog, K, biased,
-                               cast_hyper<T>(hp), csr->n_items, waves);
-            return check_launch(PP ? "mf_epoch_kernel<svdpp>" : "mf_epoch_kernel<svd>");
-        });
+        return mf_ext::launch_epoch_tm<T, M, PP>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj,
+                                                  qlog, K, biased, hp, waves, dups, stream);
     };
     auto by_mode = [&](auto tag_t) -> int {
         switch (mode) {
@@ -1711,3 +1752,5 @@ int mf_selftest_wave_sum(const void *in, void *out, int32_t n_waves, int32_t dty
 }
 
 }  // extern "C"
+
+#endif  // MF_TU_EPOCH
