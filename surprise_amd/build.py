@@ -37,16 +37,20 @@ def units():
     return out
 
 
-def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -> str:
+def build(force: bool = False, verbose: bool = False, jobs: int | None = None, out: str = OUT,
+          extra: tuple = ()) -> str:
+    """Build (when stale) and return the library path.  out / extra: experiment variants
+    (tools/ builds libraries with -D switches next to the product one)."""
     newest = max(os.path.getmtime(SRC), os.path.getmtime(HDR), os.path.getmtime(__file__))
-    if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= newest:
-        return OUT
-    os.makedirs(OBJ_DIR, exist_ok=True)
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= newest:
+        return out
+    obj_dir = OBJ_DIR if out == OUT else out + ".obj"
+    os.makedirs(obj_dir, exist_ok=True)
 
     def compile_one(u):
         name, defs = u
-        obj = os.path.join(OBJ_DIR, name + ".o")
-        cmd = [HIPCC, *FLAGS, *defs, "-c", "-o", obj, SRC]
+        obj = os.path.join(obj_dir, name + ".o")
+        cmd = [HIPCC, *FLAGS, *extra, *defs, "-c", "-o", obj, SRC]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
@@ -55,12 +59,12 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
     jobs = jobs or min(len(units()), max(1, min(os.cpu_count() or 1, 16)))
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(compile_one, units()))
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

@@ -44,6 +44,9 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kBlock = 256;  // 4 waves per workgroup
+#ifndef MF_EXP_YATOM
+#define MF_EXP_YATOM 1
+#endif
 #ifndef MF_PF
 #define MF_PF 8
 #endif
@@ -658,9 +661,11 @@ __device__ __forceinline__ void epoch_body(
 #endif
                     if (MODE == kPlain) L::template sts<0>(q_rs, cq[v], off, stv[v]);
                 }
+#ifndef MF_EXP_NO_QATOM
                 if (ATOM)
 #pragma unroll
                     for (int u = 0; u < U; ++u) atom_add1(q_rs, qb, q_oob, cq1[u], off, qd1[u]);
+#endif
             } else {     // masked slots: push the offset past the table / log segment
                 const uint32_t moff = valid ? off : off + q_oob;
 #pragma unroll
@@ -708,7 +713,11 @@ __device__ __forceinline__ void epoch_body(
         __builtin_amdgcn_s_setprio(0);
 
         // SVD++ (3): y_j <- A y_j + c for every j in I_u
+#ifdef MF_EXP_NO_YWALK2
+        if (false) {
+#else
         if (PP) {
+#endif
             // c obeys the same recurrence as imp (c' = decay c + lr_yj err q / sqrt n) from 0
             // instead of imp0, so c = (imp - A imp0) / sqrt n: no per-rating c update
             vec cacc[G];
@@ -721,7 +730,7 @@ __device__ __forceinline__ void epoch_body(
                 for (int a = 0; a < kYB; ++a)
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-                        if (YATOM)
+                        if (YATOM && MF_EXP_YATOM)
                             atom_add1(y_rs, yj, y_oob, cy1[u], ro[a], (A - T(1)) * g[a][u] + cacc1[u]);
                         else
                             Buf<T>::template st<0>(y_rs, ro[a] + cy1[u], A * g[a][u] + cacc1[u]);
