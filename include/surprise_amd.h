@@ -37,8 +37,9 @@ extern "C" {
 #define MF_MODE_PLAIN  0 /* shared item table, plain load/store (lock-free Hogwild!; with one wave
                             the exact sequential order of the reference)                           */
 #define MF_MODE_ATOMIC 1 /* shared item table, item deltas applied with float atomics              */
-#define MF_MODE_LOG    2 /* item table read-only for the epoch-chunk, every rating's item delta
-                            written to a delta log (row = CSR position), folded into the table by
+#define MF_MODE_LOG    2 /* item table read-only for the epoch-chunk, every rating's item
+                            gradient g = err * pe (pe = the user row [+ u_impl], 1 in the bias
+                            column) written to a log (row = CSR position), folded into the table by
                             mf_log_reduce + mf_log_apply: race-free, independent of scheduling     */
 
 #define MF_E_ARG          1001 /* invalid argument (shape, mode, dtype, n_factors too large)      */
@@ -76,8 +77,9 @@ typedef struct mf_csr {
  *   pu [n_users][ldu], bu [n_users], qb [n_items][ldq]
  *   biased    : 0 reproduces SVD(biased=False) (hp->global_mean must then be 0)
  *   mode      : MF_MODE_*
- *   qlog      : MF_MODE_LOG: device [nnz][ldq] delta log, row k = rating k of the CSR (whole rows
- *               written, zero padding included); each user's segment must be < 2^30
+ *   qlog      : MF_MODE_LOG: device [nnz][ldq] gradient log, row k = err_k * [p_u | 1 | 0..] of
+ *               rating k of the CSR (the user row before the rating's step; whole rows written,
+ *               zero padding included); each user's segment must be < 2^30
  *               bytes (|I_u| * ldq * sizeof(dtype)).  Other modes: NULL.
  *   n_waves   : wavefronts to launch (<= 0: library default = fill the GPU);
  *               1 with MF_MODE_PLAIN gives the exact sequential reference order when
@@ -121,7 +123,10 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
 /*
  * Delta-log merge, step 2: S_i = sum of sums[p] over p in [item_piece_ptr[i], item_piece_ptr[i+1])
  * (item_piece_ptr NULL: S_i = sums[i], e.g. after an all-reduce).  delta_out (nullable,
- * [n_items][ld]) receives S; apply != 0 adds w * S_i to qb[i] in columns < n_factors and bias_col:
+ * [n_items][ld]) receives S; apply != 0 turns the summed gradients into the summed item steps,
+ * D_i = lr o (S_i - N reg o qb[i])  (lr, reg = lr_qi, reg_qi in columns < n_factors and lr_bi,
+ * reg_bi in bias_col; bias_col < 0: none), N = totals[i] (ratings of item i in the chunk, all
+ * ranks; required with apply), and adds w * D_i to qb[i]:
  *   MF_MERGE_SUM:   w = 1;
  *   MF_MERGE_COUNT: w = (1 - (1-eta)^N) / (N eta), N = totals[i] (ratings of item i in the chunk,
  *                   all ranks), eta = lr_bi (1 + reg_bi) in bias_col and lr_qi (<p^2> + reg_qi)

@@ -414,9 +414,10 @@ __device__ __forceinline__ void to_lane8(const double (&y)[G], double (&x)[G]) {
 // MODE decides what happens to the item row after a rating:
 //   kPlain  store q_i + d (lock-free Hogwild!; with one wave: the exact sequential reference);
 //   kAtomic memory-side float add of d;
-//   kLog    the item table is a read-only snapshot for the whole epoch-chunk and d goes to row k
-//           of the delta log (k = the rating's CSR position); mf_log_reduce / mf_log_apply fold
-//           the log into the table afterwards.  Race-free and independent of wave scheduling.
+//   kLog    the item table is a read-only snapshot for the whole epoch-chunk and the rating's
+//           gradient g = err pe (d = lr o (g - reg o q)) goes to row k of the delta log (k = the
+//           rating's CSR position); mf_log_reduce / mf_log_apply fold the log into the table
+//           afterwards (q += w o lr o (sum g - N reg o q)).  Race-free, independent of scheduling.
 // SVD++'s y_j rows are shared state in every mode (kPlain: stores, kAtomic / kLog: float adds).
 //
 // Per rating the dependent chain is: p -> <q, p> partial (packed mul) -> wave sum -> err ->
@@ -635,7 +636,8 @@ __device__ __forceinline__ void epoch_body(
             vec qd[G];
 #pragma unroll
             for (int v = 0; v < G; ++v) {  // mf.pyx:258-262 / :490-498, old puf and qif
-                qd[v] = err * dq_e[v] + dq_0[v];
+                // (kLog logs the gradient err pe; mf_log_apply applies lr and reg per column)
+                qd[v] = LOG ? err * pe[v] : err * dq_e[v] + dq_0[v];
                 const vec pn = err * dp_e[v] + dp_0[v];
                 p[v] = valid ? pn : p[v];
                 if (PP) {  // imp' = decay imp + lr_yj err q (the c of y_j <- A y_j + c: below)
@@ -742,7 +744,293 @@ __device__ __forceinline__ void epoch_body(
     for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w]);
 }
 
-#define MF_EPOCH_PARAMS                                                                         \
+#ifndef MF_LA_BANK
+#define MF_LA_BANK 8  // ratings per bank in the lookahead body (two banks alternate)
+#endif
+#ifndef MF_LOG_AUX
+#define MF_LOG_AUX 0  // cache policy of the lookahead body's log stores
+#endif
+
+// ---- two 64-lane sums at once (the lookahead body's X and Y): the halves are exchanged with one
+// v_permlane32_swap so that lanes 0-31 carry x's partials and lanes 32-63 y's, then one 5-step
+// DPP reduction inside each half (the last step a row_bcast:15) leaves x's sum in lane 31 and
+// y's in lane 63: 9 instructions for both (one wave_sum_u alone is 8).
+__device__ __forceinline__ void swap32(float &a, float &b) {
+    auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, a), __builtin_bit_cast(int, b),
+                                              false, false);
+    a = __builtin_bit_cast(float, (int)r[0]);
+    b = __builtin_bit_cast(float, (int)r[1]);
+}
+__device__ __forceinline__ void swap32(double &a, double &b) {
+    const long long ua = __builtin_bit_cast(long long, a), ub = __builtin_bit_cast(long long, b);
+    float al = __builtin_bit_cast(float, (int)(ua & 0xffffffffll));
+    float ah = __builtin_bit_cast(float, (int)(ua >> 32));
+    float bl = __builtin_bit_cast(float, (int)(ub & 0xffffffffll));
+    float bh = __builtin_bit_cast(float, (int)(ub >> 32));
+    swap32(al, bl);
+    swap32(ah, bh);
+    auto join = [](float lo, float hi) {
+        return __builtin_bit_cast(double, ((long long)__builtin_bit_cast(int, hi) << 32) |
+                                              (unsigned int)__builtin_bit_cast(int, lo));
+    };
+    a = join(al, ah);
+    b = join(bl, bh);
+}
+template <typename T>
+__device__ __forceinline__ void wave_sum2_u(T x, T y, T &sx, T &sy) {
+    swap32(x, y);     // x = [x_lo | y_lo], y = [x_hi | y_hi]
+    T z = x + y;      // lanes 0-31: x's partials, lanes 32-63: y's
+    z += dpp<0xB1>(z);   // quad_perm [1,0,3,2]
+    z += dpp<0x4E>(z);   // quad_perm [2,3,0,1]
+    z += dpp<0x141>(z);  // row_half_mirror
+    z += dpp<0x140>(z);  // row_mirror: every row holds its 16-lane sum
+    z += dpp<0x142>(z);  // row_bcast:15: row 1 += row 0, row 3 += row 2 (rows 0, 2: unused)
+    sx = readlane(z, 31);
+    sy = readlane(z, 63);
+}
+
+// ---- SVD rating loop in lookahead form (kLog, SVD, G = 1: K <= 127 fp32 / K <= 63 fp64)
+//
+// Per user, with q_k = the snapshot row [q | b] of rating k and p_k's column K the constant 1:
+//   dot_k = <q_k, p_k>,  err_k = r_k - c_k - dot_k,  c_k = mu + bu_k,
+//   p_{k+1} = ap o p_k + err_k D_k,  D_k = lrp o q_k   (ap = 1 - lr_pu reg_pu, lrp = lr_pu on
+//   factor columns; 1 and 0 elsewhere),  c_{k+1} = lr_bu err_k + c0_k,  c0_k = abu c_k + kb.
+// One step back, dot_k = X_k + err_{k-1} Y_k with X_k = <q_k, ap o p_{k-1}>, Y_k = <q_k, D_{k-1}>:
+//   err_k = (r_k - c0_{k-1}) - X_k - err_{k-1} (Y_k + lr_bu)        -- one FMA after err_{k-1}.
+// X_{k+1} and Y_{k+1} need p_k = A_{k-1} + err_{k-1} D_{k-1} (A = ap o p), i.e. err_{k-1}: their
+// reduction (wave_sum2_u) runs a whole rating ahead of its use, beside the next rating's work,
+// instead of on the err -> p -> dot -> err chain.  The log row of rating k is g_k = err_k p_k
+// (columns 0..K; mf_log_apply turns the sums into the item steps).  Same arithmetic as the
+// reference recursion up to rounding (fp64: equal to the delta-log oracle to 1e-9,
+// tests/test_gpu_parity.py).
+template <typename T, int G>
+__device__ __forceinline__ void epoch_body_la(
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
+    const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
+    T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *qlog, int K,
+    int biased, Hyper<T> hp, int n_items, int64_t n_waves_req)
+{
+    using L = Lane8<T>;
+    using vec = typename L::vec;
+    constexpr int W = L::W;
+    constexpr int kB = MF_LA_BANK;  // ratings per bank of gathered rows (a power of 2 <= 64)
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t grid_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
+    if (wave >= n_waves) return;
+
+    const uint32_t qrow = (uint32_t)ldq * sizeof(T), prow = (uint32_t)ldu * sizeof(T);
+    const uint32_t q_oob = (uint32_t)n_items * qrow;
+    uint32_t cq[G], cu[G], cl[G];
+    vec one[G], lrp[G], ap[G];
+#pragma unroll
+    for (int v = 0; v < G; ++v) {
+        const int c0 = (lane + kWave * v) * W;
+        const uint32_t b = (uint32_t)c0 * sizeof(T);
+        cq[v] = c0 < ldq ? b : q_oob;
+        cu[v] = c0 < ldu ? b : prow;  // >= the pu record (K elements): dropped
+        cl[v] = c0 < ldq ? b : kLogOob;
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            const int c = c0 + e;
+            const bool fac = c < K, bias = biased && c == K;
+            L::set(one[v], e, bias ? T(1) : T(0));
+            L::set(lrp[v], e, fac ? hp.lr_pu : T(0));
+            L::set(ap[v], e, fac ? T(1) - hp.lr_pu * hp.reg_pu : T(1));
+        }
+    }
+    const T lr_bu = biased ? hp.lr_bu : T(0);
+    const T abu = T(1) - lr_bu * hp.reg_bu;
+    const T kb = hp.gm * (T(1) - abu);
+    const rsrc_t q_rs = make_rsrc(qb, q_oob);
+    const int prio_len = (int)(row_ptr[sched[0] + 1] - row_ptr[sched[0]]);
+
+    auto do_user = [&](const int u) {
+        const int64_t s = row_ptr[u];
+        const int n = (int)(row_ptr[u + 1] - s);
+        if (n <= 0) return;
+        if (n * 2 > prio_len) __builtin_amdgcn_s_setprio(3);
+        else if (n * 4 > prio_len) __builtin_amdgcn_s_setprio(2);
+        else if (n * 8 > prio_len) __builtin_amdgcn_s_setprio(1);
+        const rsrc_t l_rs = make_rsrc(qlog + s * ldq, (uint32_t)n * qrow);
+        const int32_t *__restrict__ it = items + s;
+        const T *__restrict__ rt = ratings + s;
+        const rsrc_t p_rs = make_rsrc(pu + (int64_t)u * ldu, (uint32_t)K * sizeof(T));
+        const rsrc_t b_rs = make_rsrc(bu + u, sizeof(T));
+
+        vec p0[G];
+#pragma unroll
+        for (int v = 0; v < G; ++v) p0[v] = L::template ld<0>(p_rs, cu[v]) + one[v];
+        const T bu0 = Buf<T>::template ld<0>(b_rs, 0);
+
+        // Two banks of kB gathered rows alternate.  At the start of a bank: the ids of the bank
+        // after next are requested, then the next bank's rows, THEN the previous bank's kB log
+        // rows (held in registers) are stored.  vmcnt retires in issue order and a store stays
+        // counted for thousands of cycles under load: this order lets every wait for a row skip
+        // the most recent stores (a row's wait covers stores a whole bank older than it).
+        // Rows past n are clamped to the user's last rating (real rows); their log stores fall
+        // outside l_rs and are dropped.
+        auto grp_load = [&](int j0, uint32_t &go, T &gr) {
+            int j = j0 + (lane & (kB - 1));
+            j = j < n ? j : n - 1;
+            go = (uint32_t)it[j] * qrow;
+            gr = rt[j];
+        };
+        vec bank[2][kB][G];
+        T br[2][kB];
+        vec lg[kB][G];
+        uint32_t go_n1, go_n2;
+        T gr_n1, gr_n2;
+        auto fill = [&](const int bk, const uint32_t go, const T gr) {
+#pragma unroll
+            for (int d = 0; d < kB; ++d) {
+                const uint32_t off = readlane((int)go, d);
+                br[bk][d] = readlane(gr, d);
+#pragma unroll
+                for (int v = 0; v < G; ++v) bank[bk][d][v] = L::template lds<0>(q_rs, cq[v], off);
+            }
+        };
+        auto flush = [&](const int j0p) {  // log rows j0p .. j0p + kB - 1
+#pragma unroll
+            for (int d = 0; d < kB; ++d)
+#pragma unroll
+                for (int v = 0; v < G; ++v)
+                    L::template sts<MF_LOG_AUX>(l_rs, cl[v], (uint32_t)(j0p + d) * qrow, lg[d][v]);
+        };
+        {
+            uint32_t go0;
+            T gr0;
+            grp_load(0, go0, gr0);
+            grp_load(kB, go_n1, gr_n1);
+            asm volatile("" ::"v"(go0), "v"(gr0), "v"(go_n1), "v"(gr_n1));
+            __builtin_amdgcn_sched_barrier(0);
+            fill(0, go0, gr0);
+        }
+        // state entering rating k: err_p = err_{k-1}, c0_p = c0_{k-1}, A_p = A_{k-1}, D_p = D_{k-1},
+        // X = X_k, Yb = Y_k + lr_bu (k = 0: err_{-1} = 0, c0_{-1} = c_0, A_{-1} = p_0, D_{-1} = 0,
+        // X_0 = <q_0, p_0>)
+        T err_p = T(0), c0_p = hp.gm + bu0, X, Yb = T(0);
+        vec A_p[G], D_p[G];
+        {
+            vec part = L::splat(T(0));
+#pragma unroll
+            for (int v = 0; v < G; ++v) {
+                A_p[v] = p0[v];
+                D_p[v] = L::splat(T(0));
+                part += bank[0][0][v] * p0[v];
+            }
+            X = wave_sum_u(L::hsum(part));
+        }
+
+        auto step = [&](auto full_c, auto bank_c, const int j0, const int d) {
+            constexpr bool FULL = decltype(full_c)::value;
+            constexpr int bk = decltype(bank_c)::value;
+            const int k = j0 + d;
+            const bool valid = FULL || k < n;
+            vec (&qn)[G] = d + 1 < kB ? bank[bk][d + 1] : bank[bk ^ 1][0];  // rating k+1's row
+            // keep the first read (and the wait) of rating k+1's row in this step, and the
+            // steps' memory waits in order
+#pragma unroll
+            for (int v = 0; v < G; ++v) asm volatile("" : "+v"(qn[v])::"memory");
+            const T err = (br[bk][d] - c0_p) - X - err_p * Yb;  // mf.pyx:250
+            const T c0 = abu * (lr_bu * err_p + c0_p) + kb;     // mf.pyx:253, one rating late
+            vec pk[G], A[G], D[G], px = L::splat(T(0)), py = L::splat(T(0));
+#pragma unroll
+            for (int v = 0; v < G; ++v) {
+                pk[v] = A_p[v] + err_p * D_p[v];  // p_k (mf.pyx:258-262, one rating late)
+                A[v] = ap[v] * pk[v];
+                D[v] = lrp[v] * bank[bk][d][v];
+                px += qn[v] * A[v];
+                py += qn[v] * D[v];
+                lg[d][v] = err * pk[v];  // the log row g_k = err_k p_k (old p, mf.pyx:261)
+            }
+            T Xn, Yn;
+            wave_sum2_u(L::hsum(px), L::hsum(py), Xn, Yn);  // X_{k+1}, Y_{k+1}
+            if (FULL) {
+                err_p = err;
+                c0_p = c0;
+                X = Xn;
+                Yb = Yn + lr_bu;
+#pragma unroll
+                for (int v = 0; v < G; ++v) {
+                    A_p[v] = A[v];
+                    D_p[v] = D[v];
+                }
+            } else {
+                err_p = valid ? err : err_p;
+                c0_p = valid ? c0 : c0_p;
+                X = valid ? Xn : X;
+                Yb = valid ? Yn + lr_bu : Yb;
+#pragma unroll
+                for (int v = 0; v < G; ++v) {
+                    A_p[v] = valid ? A[v] : A_p[v];
+                    D_p[v] = valid ? D[v] : D_p[v];
+                }
+            }
+        };
+        int j0 = 0;
+        // one full bank: ratings j0 .. j0 + kB - 1 in bank bk (FIRST: nothing to flush yet)
+        auto full_bank = [&](auto bank_c, auto first_c) {
+            constexpr int bk = decltype(bank_c)::value;
+            grp_load(j0 + 2 * kB, go_n2, gr_n2);
+            asm volatile("" ::: "memory");  // issue order: ids, rows, then the stores
+            fill(bk ^ 1, go_n1, gr_n1);
+            asm volatile("" ::: "memory");
+            if (!decltype(first_c)::value) flush(j0 - kB);
+            go_n1 = go_n2;
+            gr_n1 = gr_n2;
+#pragma unroll
+            for (int d = 0; d < kB; ++d) step(std::true_type{}, bank_c, j0, d);
+            j0 += kB;
+        };
+        // the last ratings j0 .. n-1 (0 < n - j0 < kB) in bank bk: the previous bank's log rows
+        // go out first (the steps reuse their registers), then masked steps and their rows
+        auto tail_bank = [&](auto bank_c) {
+            if (j0 > 0) flush(j0 - kB);
+#pragma unroll
+            for (int d = 0; d < kB; ++d) step(std::false_type{}, bank_c, j0, d);
+            flush(j0);
+        };
+        using B0 = std::integral_constant<int, 0>;
+        using B1 = std::integral_constant<int, 1>;
+        using Yes = std::true_type;
+        using No = std::false_type;
+        if (n >= kB) {
+            full_bank(B0{}, Yes{});
+            for (; j0 + 2 * kB <= n;) {
+                full_bank(B1{}, No{});
+                full_bank(B0{}, No{});
+            }
+            if (j0 + kB <= n) {
+                full_bank(B1{}, No{});
+                if (j0 < n) tail_bank(B0{});
+                else flush(j0 - kB);
+            } else if (j0 < n) {
+                tail_bank(B1{});
+            } else {
+                flush(j0 - kB);
+            }
+        } else {
+            tail_bank(B0{});
+        }
+        // after rating n-1: p_n = A_{n-1} + err_{n-1} D_{n-1}, c_n = lr_bu err_{n-1} + c0_{n-1}
+#pragma unroll
+        for (int v = 0; v < G; ++v) L::template st<0>(p_rs, cu[v], A_p[v] + err_p * D_p[v]);
+        const T bu_u = lr_bu * err_p + c0_p - hp.gm;
+        Buf<T>::template st<0>(b_rs, lane == 0 ? 0u : (uint32_t)sizeof(T), bu_u);
+        __builtin_amdgcn_s_setprio(0);
+    };
+
+    for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w]);
+}
+
+#ifndef MF_LA
+#define MF_LA 1
+#endif
+
+#define MF_EPOCH_PARAMS                                                                       \
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,                      \
         const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,       \
         T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, int K,  \
@@ -754,7 +1042,11 @@ __device__ __forceinline__ void epoch_body(
 template <typename T, int G, int MODE, bool PP, bool DUPS>
 __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
 {
-    epoch_body<T, G, MODE, PP, DUPS, kPF>(MF_EPOCH_ARGS);
+    if constexpr (MODE == kLog && !PP && G == 1 && MF_LA)
+        epoch_body_la<T, G>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, qlog,
+                            K, biased, hp, n_items, n_waves_req);
+    else
+        epoch_body<T, G, MODE, PP, DUPS, kPF>(MF_EPOCH_ARGS);
 }
 
 }  // namespace
@@ -945,8 +1237,9 @@ template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     T *__restrict__ qb, int n_items, int ld, int n_fac, int bias_col, const T *__restrict__ sums,
     const int32_t *__restrict__ item_piece_ptr, const int32_t *__restrict__ totals,
-    int count_rule, double eta_bias, double lr_fac, double reg_fac,
-    const double *__restrict__ p2stat, T *__restrict__ delta_out, int apply)
+    int count_rule, double eta_bias, double lr_fac, double reg_fac, double lr_f, double reg_f,
+    double lr_b, double reg_b, const double *__restrict__ p2stat, T *__restrict__ delta_out,
+    int apply)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
@@ -988,12 +1281,14 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
             const int64_t x = i * ld + c;
             if (delta_out) delta_out[x] = acc[v];
             if (apply && (c < n_fac || c == bias_col)) {
+                const bool b = c == bias_col;
                 double w = 1.0;
-                if (count_rule && N > 1.0) {
-                    const bool b = c == bias_col;
+                if (count_rule && N > 1.0)
                     w = -expm1(N * (b ? l_bias : l_fac)) / (N * (b ? eta_bias : eta_fac));
-                }
-                qb[x] += (T)w * acc[v];
+                // the log holds gradients g_k = err_k pe_k: sum_k d_k = lr (S - N reg q)
+                const T q = qb[x];
+                const T d = (T)(b ? lr_b : lr_f) * (acc[v] - (T)N * (T)(b ? reg_b : reg_f) * q);
+                qb[x] = q + (T)w * d;
             }
         }
     }
@@ -1433,7 +1728,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 500; }
+int mf_version(void) { return 600; }
 
 const char *mf_last_error(void) { return g_err; }
 
@@ -1507,19 +1802,22 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
     const int count_rule = rule == MF_MERGE_COUNT;
     if (count_rule && (!totals || !hp || !p2stat))
         return set_err(MF_E_ARG, "count-aware rule needs totals, hp, p2stat");
+    if (apply && (!totals || !hp)) return set_err(MF_E_ARG, "apply needs totals and hp");
     if (n_items == 0 || (!apply && !delta_out)) return 0;
     if (!sums || (apply && !qb)) return set_err(MF_E_ARG, "null argument");
     const int g = grid_for_waves(default_waves(n_items));
     hipStream_t st = (hipStream_t)stream;
     const double eta_b = count_rule ? hp->lr_bi * (1.0 + hp->reg_bi) : 0.0;
-    const double lr_f = count_rule ? hp->lr_qi : 0.0, reg_f = count_rule ? hp->reg_qi : 0.0;
+    const double lr_c = count_rule ? hp->lr_qi : 0.0, reg_c = count_rule ? hp->reg_qi : 0.0;
+    const double lr_f = hp ? hp->lr_qi : 0.0, reg_f = hp ? hp->reg_qi : 0.0;
+    const double lr_b = hp ? hp->lr_bi : 0.0, reg_b = hp ? hp->reg_bi : 0.0;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
         return dispatch_v<T>(ld, [&](auto vc) -> int {
             hipLaunchKernelGGL((log_apply_kernel<T, decltype(vc)::value>), dim3(g), dim3(kBlock), 0,
                                st, (T *)qb, n_items, ld, n_factors, bias_col, (const T *)sums,
-                               item_piece_ptr, totals, count_rule, eta_b, lr_f, reg_f, p2stat,
-                               (T *)delta_out, apply);
+                               item_piece_ptr, totals, count_rule, eta_b, lr_c, reg_c, lr_f,
+                               reg_f, lr_b, reg_b, p2stat, (T *)delta_out, apply);
             return check_launch("log_apply_kernel");
         });
     };

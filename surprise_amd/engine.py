@@ -256,6 +256,17 @@ class MFEngine(ItemSync):
                 ctx.all_reduce_sum(tt)
             self.totals.append(tt)
 
+    def _totals(self):
+        """Per-item rating counts of every chunk over all ranks (a single rank: its own)."""
+        if self.totals is None:
+            self._prepare(None)
+        return self.totals
+
+    @property
+    def _bias_col(self):
+        """Item-row column of b_i for mf_log_apply (-1: unbiased, the column never moves)."""
+        return self.K if self.biased else -1
+
     def _count_rule(self):
         if self.merge_rule == "count" and self.totals is None:
             self._prepare(None)
@@ -266,9 +277,9 @@ class MFEngine(ItemSync):
         c = getattr(self, "_chunk", 0)
         lg = self.logs[c]
         count = self._count_rule()
-        _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K, self.K,
-                  self._ptr(self.sums), self._ptr(lg["ipp"]),
-                  self._ptr(self.totals[c]) if count else None, ctypes.byref(self._hyper),
+        _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K,
+                  self._bias_col, self._ptr(self.sums), self._ptr(lg["ipp"]),
+                  self._ptr(self._totals()[c]), ctypes.byref(self._hyper),
                   self._ptr(self.work), _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM,
                   None if delta_out is None else self._ptr(delta_out), int(apply), self.dtype,
                   self._st())
@@ -340,8 +351,8 @@ class MFEngine(ItemSync):
         x = 0
         if self.is_log:  # bufs[-1] is the all-reduced sum of squares of pu
             count = self._count_rule()
-            _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K, self.K,
-                      self._ptr(bufs[0]), None, self._ptr(self.totals[c]) if count else None,
+            _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K,
+                      self._bias_col, self._ptr(bufs[0]), None, self._ptr(self._totals()[c]),
                       ctypes.byref(self._hyper), self._ptr(bufs[-1]),
                       _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM, None, 1, self.dtype, st)
             x = 1
