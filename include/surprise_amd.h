@@ -81,6 +81,11 @@ typedef struct mf_csr {
  *               rating k of the CSR (the user row before the rating's step; whole rows written,
  *               zero padding included); each user's segment must be < 2^30
  *               bytes (|I_u| * ldq * sizeof(dtype)).  Other modes: NULL.
+ *   elog      : NULL, or (MF_MODE_LOG, ldq * sizeof(dtype) <= 512 B) the checkpoint form of the
+ *               log: device [nnz + mf_ckpt_interval()] errors, elog[k] = err_k, and qlog row k
+ *               holds [p_u | 1 | 0..] before rating k only where k - row_ptr[u] is a multiple of
+ *               mf_ckpt_interval() (other rows are not written); mf_log_replay rebuilds the
+ *               gradients.  ~1/8 of the log bytes: the epoch kernel's memory traffic.
  *   n_waves   : wavefronts to launch (<= 0: library default = fill the GPU);
  *               1 with MF_MODE_PLAIN gives the exact sequential reference order when
  *               sched = 0..n_users-1.
@@ -90,8 +95,8 @@ typedef struct mf_csr {
 #define MF_EPOCH_DUP_ITEMS   1
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves, int32_t flags,
-                 int32_t dtype, void *stream);
+                 const mf_hyper_t *hp, int32_t mode, void *qlog, void *elog, int32_t n_waves,
+                 int32_t flags, int32_t dtype, void *stream);
 
 /*
  * One epoch-chunk of SVD++ SGD (SVDpp.sgd epoch body, matrix_factorization.pyx:463-498) in the
@@ -119,6 +124,23 @@ int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *
 int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *perm,
                   const int32_t *piece_beg, int64_t n_pieces, void *sums, int32_t dtype,
                   void *stream);
+
+/*
+ * Delta-log merge, step 1 for the checkpoint form (mf_svd_epoch with elog): the same sums as
+ * mf_log_reduce would give on the gradient log, sums[p][c] = sum over the piece's ratings k of
+ * err_k * p_k[c] (c <= n_factors; 0 above), where p_k is rebuilt from the checkpoint row
+ * c_k = ck_pos[x] <= k (x = the rating's index in perm; c_k = k - ((k - row_ptr[u]) mod
+ * mf_ckpt_interval())) by the epoch kernel's recursion p <- ap * p + err_m * lr_pu * q_{item(m)}
+ * (ap = 1 - lr_pu * reg_pu on factor columns) over the snapshot item rows qb -- call it before
+ * mf_log_apply.  Requires ldq * sizeof(dtype) <= 512 B.
+ */
+int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_factors,
+                  const mf_csr_t *csr, const void *qb, const mf_hyper_t *hp, const int32_t *perm,
+                  const int32_t *ck_pos, const int32_t *piece_beg, int64_t n_pieces, void *sums,
+                  int32_t dtype, void *stream);
+
+/* Checkpoint interval of the checkpoint log (ratings per stored user row). */
+int mf_ckpt_interval(void);
 
 /*
  * Delta-log merge, step 2: S_i = sum of sums[p] over p in [item_piece_ptr[i], item_piece_ptr[i+1])

@@ -43,11 +43,14 @@ _vp, _i32, _i64, _dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.
 # name -> argtypes (all return int except mf_last_error)
 SIGNATURES = {
     "mf_svd_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32, _i32,
-                     ctypes.POINTER(MfHyper), _i32, _vp, _i32, _i32, _i32, _vp],
+                     ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_svdpp_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp, _i32,
                        ctypes.POINTER(MfHyper), _i32, _vp, _i32, _i32, _i32, _vp],
     "mf_sumsq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
     "mf_log_reduce": [_vp, _i32, _i32, _vp, _vp, _i64, _vp, _i32, _vp],
+    "mf_log_replay": [_vp, _vp, _i32, _i32, ctypes.POINTER(MfCsr), _vp,
+                      ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _i32, _vp],
+    "mf_ckpt_interval": [],
     "mf_log_apply": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, ctypes.POINTER(MfHyper), _vp,
                      _i32, _vp, _i32, _i32, _vp],
     "mf_item_merge": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,

@@ -36,7 +36,7 @@ namespace mf_ext {
 extern thread_local char g_err[256];
 template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
-                    int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, int32_t K,
+                    int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, void *stream);
 }  // namespace mf_ext
 
@@ -744,6 +744,10 @@ __device__ __forceinline__ void epoch_body(
     for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w]);
 }
 
+#ifndef MF_CKPT
+#define MF_CKPT 2  // checkpoint interval of the SVD log (elog != NULL): a user row per 2 ratings
+#endif
+constexpr int kCkpt = MF_CKPT;
 #ifndef MF_LA_BANK
 #define MF_LA_BANK 8  // ratings per bank in the lookahead body (two banks alternate)
 #endif
@@ -803,17 +807,18 @@ __device__ __forceinline__ void wave_sum2_u(T x, T y, T &sx, T &sy) {
 // (columns 0..K; mf_log_apply turns the sums into the item steps).  Same arithmetic as the
 // reference recursion up to rounding (fp64: equal to the delta-log oracle to 1e-9,
 // tests/test_gpu_parity.py).
-template <typename T, int G>
+template <typename T, int G, bool CK>
 __device__ __forceinline__ void epoch_body_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
-    T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *qlog, int K,
+    T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *qlog, T *elog, int K,
     int biased, Hyper<T> hp, int n_items, int64_t n_waves_req)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
     constexpr int W = L::W;
     constexpr int kB = MF_LA_BANK;  // ratings per bank of gathered rows (a power of 2 <= 64)
+    static_assert(!CK || (kB % kCkpt == 0 && kB <= kWave), "checkpoints: whole banks");
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -855,6 +860,7 @@ __device__ __forceinline__ void epoch_body_la(
         else if (n * 4 > prio_len) __builtin_amdgcn_s_setprio(2);
         else if (n * 8 > prio_len) __builtin_amdgcn_s_setprio(1);
         const rsrc_t l_rs = make_rsrc(qlog + s * ldq, (uint32_t)n * qrow);
+        const rsrc_t e_rs = make_rsrc(CK ? elog + s : qlog, (uint32_t)n * sizeof(T));
         const int32_t *__restrict__ it = items + s;
         const T *__restrict__ rt = ratings + s;
         const rsrc_t p_rs = make_rsrc(pu + (int64_t)u * ldu, (uint32_t)K * sizeof(T));
@@ -880,7 +886,11 @@ __device__ __forceinline__ void epoch_body_la(
         };
         vec bank[2][kB][G];
         T br[2][kB];
-        vec lg[kB][G];
+        // log rows of the current bank: CK: the checkpoints p_k (k = 0 mod kCkpt) and err_k in
+        // lane k mod kB of ev; otherwise every rating's gradient row g_k = err_k p_k
+        constexpr int kLg = CK ? kB / kCkpt : kB;
+        vec lg[kLg][G];
+        T ev = T(0);
         uint32_t go_n1, go_n2;
         T gr_n1, gr_n2;
         auto fill = [&](const int bk, const uint32_t go, const T gr) {
@@ -893,11 +903,39 @@ __device__ __forceinline__ void epoch_body_la(
             }
         };
         auto flush = [&](const int j0p) {  // log rows j0p .. j0p + kB - 1
+            if constexpr (CK) {
 #pragma unroll
-            for (int d = 0; d < kB; ++d)
+                for (int x = 0; x < kLg; ++x)
+#pragma unroll
+                    for (int v = 0; v < G; ++v)
+                        L::template sts<MF_LOG_AUX>(l_rs, cl[v], (uint32_t)(j0p + x * kCkpt) * qrow,
+                                                    lg[x][v]);
+                Buf<T>::template st<0>(e_rs, lane < kB ? (uint32_t)(j0p + lane) * sizeof(T) : kLogOob, ev);
+                return;
+            }
+#if defined(MF_EXP_PAIR_STORE)  // timing experiment only: 2 rows per dwordx4 (wrong layout)
+#pragma unroll
+            for (int d = 0; d < kB; d += 2)
+#pragma unroll
+                for (int v = 0; v < G; ++v) {
+                    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+                    const auto a = __builtin_bit_cast(unsigned long long, lg[d][v]);
+                    const auto b = __builtin_bit_cast(unsigned long long, lg[d + 1][v]);
+                    u4 w = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+                    __builtin_amdgcn_raw_buffer_store_b128(w, l_rs, cl[v] < kLogOob ? 2 * cl[v] : kLogOob,
+                                                           (uint32_t)(j0p + d) * qrow, 0);
+                }
+#else
+#pragma unroll
+            for (int d = 0; d < kB; ++d) {
+#if defined(MF_EXP_HALF_STORE)  // timing experiment only: every other row
+                if (d & 1) continue;
+#endif
 #pragma unroll
                 for (int v = 0; v < G; ++v)
                     L::template sts<MF_LOG_AUX>(l_rs, cl[v], (uint32_t)(j0p + d) * qrow, lg[d][v]);
+            }
+#endif
         };
         {
             uint32_t go0;
@@ -944,8 +982,10 @@ __device__ __forceinline__ void epoch_body_la(
                 D[v] = lrp[v] * bank[bk][d][v];
                 px += qn[v] * A[v];
                 py += qn[v] * D[v];
-                lg[d][v] = err * pk[v];  // the log row g_k = err_k p_k (old p, mf.pyx:261)
+                if (!CK) lg[d][v] = err * pk[v];  // the log row g_k = err_k p_k (old p, mf.pyx:261)
+                else if (d % kCkpt == 0) lg[d / kCkpt][v] = pk[v];  // checkpoint p_k
             }
+            if (CK) ev = lane == d ? err : ev;
             T Xn, Yn;
             wave_sum2_u(L::hsum(px), L::hsum(py), Xn, Yn);  // X_{k+1}, Y_{k+1}
             if (FULL) {
@@ -999,7 +1039,7 @@ __device__ __forceinline__ void epoch_body_la(
         using No = std::false_type;
         if (n >= kB) {
             full_bank(B0{}, Yes{});
-            for (; j0 + 2 * kB <= n;) {
+            while (j0 + 2 * kB <= n) {  // (full_bank advances j0)
                 full_bank(B1{}, No{});
                 full_bank(B0{}, No{});
             }
@@ -1033,8 +1073,8 @@ __device__ __forceinline__ void epoch_body_la(
 #define MF_EPOCH_PARAMS                                                                       \
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,                      \
         const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,       \
-        T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, int K,  \
-        int biased, Hyper<T> hp, int n_items, int64_t n_waves_req
+        T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, T *elog,\
+        int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req
 #define MF_EPOCH_ARGS \
     row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, K, biased, hp, n_items, \
         n_waves_req
@@ -1042,11 +1082,16 @@ __device__ __forceinline__ void epoch_body_la(
 template <typename T, int G, int MODE, bool PP, bool DUPS>
 __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
 {
-    if constexpr (MODE == kLog && !PP && G == 1 && MF_LA)
-        epoch_body_la<T, G>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, qlog,
-                            K, biased, hp, n_items, n_waves_req);
-    else
+    if constexpr (MODE == kLog && !PP && G == 1 && MF_LA) {
+        if (elog)
+            epoch_body_la<T, G, true>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
+                                      qlog, elog, K, biased, hp, n_items, n_waves_req);
+        else
+            epoch_body_la<T, G, false>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb,
+                                       ldq, qlog, elog, K, biased, hp, n_items, n_waves_req);
+    } else {
         epoch_body<T, G, MODE, PP, DUPS, kPF>(MF_EPOCH_ARGS);
+    }
 }
 
 }  // namespace
@@ -1055,9 +1100,12 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
 namespace mf_ext {
 template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
-                    int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, int32_t K,
+                    int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, void *stream)
 {
+    // the checkpoint log exists for the lookahead body only: SVD, kLog, one lane group
+    if (elog && (PP || M != kLog || !MF_LA || (int64_t)ldq * sizeof(T) > 512))
+        return set_err(MF_E_UNSUPPORTED, "checkpoint log: SVD, MF_MODE_LOG, ldq * size <= 512 B only");
     return dispatch_g<T>(ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         // (kLog reads a snapshot: a repeated item sees the chunk-start row, no forwarding)
@@ -1065,14 +1113,14 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                                         : mf_epoch_kernel<T, V, M, PP, false>;
         hipLaunchKernelGGL(kern, dim3(grid_for_waves(waves)), dim3(kBlock), 0, (hipStream_t)stream,
                            csr->row_ptr, csr->items, (const T *)csr->ratings, sched, n_sched,
-                           (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, (T *)qlog, K, biased,
-                           cast_hyper<T>(hp), csr->n_items, waves);
+                           (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K,
+                           biased, cast_hyper<T>(hp), csr->n_items, waves);
         return check_launch(PP ? "mf_epoch_kernel<svdpp>" : "mf_epoch_kernel<svd>");
     });
 }
 template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
-    void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, void *);
+    void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, void *);
 }  // namespace mf_ext
 #else  // the main translation unit
 
@@ -1229,6 +1277,131 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
 #pragma unroll
             for (int e = 0; e < W; ++e)
                 if (c0 + e < ld) sums[pc * ld + c0 + e] = c0 + e < n_cols ? L::get(acc[v], e) : T(0);
+        }
+    }
+}
+
+#ifndef MF_REPLAY_U
+#define MF_REPLAY_U 8  // ratings per replay group
+#endif
+#ifndef MF_REPLAY_WPC
+#define MF_REPLAY_WPC 16  // replay waves per CU
+#endif
+
+// ---------------------------------------------------------------- checkpoint-log replay
+//
+// The SVD log in checkpoint form (mf_svd_epoch with elog != NULL): per user, the row p_c before
+// the rating at every segment position c = 0 mod kCkpt (qlog row c, CSR position) and err_k of
+// every rating (elog[k]).  The gradient of rating k, g_k = err_k p_k, is rebuilt here by
+// replaying the user recursion p_{m+1} = ap o p_m + err_m (lrp o q_{i_m}) from its checkpoint
+// (k - c < kCkpt steps) over the SNAPSHOT item rows -- the operations of the epoch kernel's
+// lookahead body, in its order -- and summed per piece exactly like log_reduce_kernel.  The
+// epoch then writes ~(ldq * size / kCkpt + size) bytes per rating instead of a whole row.
+// One wave per piece (<= 64 ratings of one item): lane x holds rating x's position, checkpoint,
+// step count, and the item-row offsets / errs of its replayed positions (vector gathers once per
+// piece); per rating only v_readlane broadcasts, the row gathers and packed FMAs remain.
+template <typename T, int G>
+__global__ __launch_bounds__(kBlock) void log_replay_kernel(
+    const T *__restrict__ ckpt, const T *__restrict__ elog, int ldq, int K,
+    const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T reg_pu,
+    const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
+    const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums)
+{
+    using L = Lane8<T>;
+    using vec = typename L::vec;
+    constexpr int W = L::W;
+    constexpr int kR = kCkpt - 1;    // replay steps at most
+    constexpr int kU = MF_REPLAY_U;  // ratings per group; two groups in flight
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const uint32_t qrow = (uint32_t)ldq * sizeof(T), q_oob = (uint32_t)n_items * qrow;
+    const rsrc_t q_rs = make_rsrc(qb, q_oob);
+    uint32_t cq[G];
+    int cc[G];
+    vec lrp[G], ap[G];
+#pragma unroll
+    for (int v = 0; v < G; ++v) {
+        const int c0 = (lane + kWave * v) * W;
+        cq[v] = c0 < ldq ? (uint32_t)c0 * sizeof(T) : q_oob;
+        cc[v] = c0 < ldq ? c0 : 0;  // (lanes past the row re-read column 0: no branch)
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            const bool fac = c0 + e < K;
+            L::set(lrp[v], e, fac ? lr_pu : T(0));
+            L::set(ap[v], e, fac ? T(1) - lr_pu * reg_pu : T(1));
+        }
+    }
+    for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
+        const int beg = piece_beg[pc], cnt = piece_beg[pc + 1] - beg;  // 1 <= cnt <= 64
+        const int xl = beg + (lane < cnt ? lane : cnt - 1);
+        const int k_l = perm[xl], c_l = ck_pos[xl];  // lane x: rating x and its checkpoint
+        const int r_l = k_l - c_l;                    // steps from the checkpoint (< kCkpt)
+        const T ek_l = lane < cnt ? elog[k_l] : T(0);  // lanes >= cnt: weight 0
+        uint32_t qo_l[kR];  // q_oob for steps the rating does not take (load 0, no traffic)
+        T e_l[kR];
+#pragma unroll
+        for (int m = 0; m < kR; ++m) {
+            const int pm = m < r_l ? c_l + m : k_l;
+            qo_l[m] = m < r_l ? (uint32_t)items[pm] * qrow : q_oob;
+            e_l[m] = elog[pm];
+        }
+        vec acc[G];
+#pragma unroll
+        for (int v = 0; v < G; ++v) acc[v] = L::splat(T(0));
+        // every load unconditional (masked rows read 0): the waits stay counted, so one group's
+        // rows arrive while the other group computes
+        auto load_grp = [&](const int x0, vec (&p)[kU][G], vec (&q)[kU][kR][G]) {
+#pragma unroll
+            for (int y = 0; y < kU; ++y) {  // (x past cnt: lane cnt-1's rating, weight 0)
+                const int x = x0 + y < kWave ? x0 + y : kWave - 1;
+                const T *row = ckpt + (int64_t)readlane(c_l, x) * ldq;
+#pragma unroll
+                for (int v = 0; v < G; ++v) p[y][v] = *(const vec *)(row + cc[v]);
+#pragma unroll
+                for (int m = 0; m < kR; ++m) {
+                    const uint32_t off = readlane((int)qo_l[m], x);
+#pragma unroll
+                    for (int v = 0; v < G; ++v) q[y][m][v] = L::template lds<0>(q_rs, cq[v], off);
+                }
+            }
+        };
+        auto comp_grp = [&](const int x0, vec (&p)[kU][G], vec (&q)[kU][kR][G]) {
+#pragma unroll
+            for (int y = 0; y < kU; ++y) {
+                const int x = x0 + y < kWave ? x0 + y : kWave - 1;
+                const int r = readlane(r_l, x);
+#pragma unroll
+                for (int m = 0; m < kR; ++m) {
+                    const T e = readlane(e_l[m], x);
+#pragma unroll
+                    for (int v = 0; v < G; ++v) {  // the epoch kernel's p_{m+1} = A_m + err_m D_m
+                        const vec A = ap[v] * p[y][v], D = lrp[v] * q[y][m][v];
+                        const vec pn = A + e * D;
+                        p[y][v] = m < r ? pn : p[y][v];
+                    }
+                }
+                const T ek = readlane(ek_l, x);
+#pragma unroll
+                for (int v = 0; v < G; ++v) acc[v] += ek * p[y][v];  // g_k = err_k p_k, in order
+            }
+        };
+        vec pA[kU][G], qA[kU][kR][G], pB[kU][G], qB[kU][kR][G];
+        load_grp(0, pA, qA);
+        for (int x0 = 0; x0 < cnt; x0 += 2 * kU) {
+            load_grp(x0 + kU, pB, qB);
+            comp_grp(x0, pA, qA);
+            if (x0 + kU >= cnt) break;
+            load_grp(x0 + 2 * kU, pA, qA);
+            comp_grp(x0 + kU, pB, qB);
+        }
+#pragma unroll
+        for (int v = 0; v < G; ++v) {
+            const int c0 = (lane + kWave * v) * W;
+#pragma unroll
+            for (int e = 0; e < W; ++e)
+                if (c0 + e < ldq) sums[pc * ldq + c0 + e] = c0 + e <= K ? L::get(acc[v], e) : T(0);
         }
     }
 }
@@ -1692,7 +1865,7 @@ int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const v
 
 template <bool PP>
 int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
-                 int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, int32_t K,
+                 int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                  int32_t biased, const mf_hyper_t *hp, int32_t mode, int32_t n_waves, int32_t flags,
                  int32_t dtype, void *stream)
 {
@@ -1705,7 +1878,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         using T = decltype(tag_t);
         constexpr int M = decltype(mode_c)::value;
         return mf_ext::launch_epoch_tm<T, M, PP>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj,
-                                                  qlog, K, biased, hp, waves, dups, stream);
+                                                  qlog, elog, K, biased, hp, waves, dups, stream);
     };
     auto by_mode = [&](auto tag_t) -> int {
         switch (mode) {
@@ -1728,17 +1901,18 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 600; }
+int mf_version(void) { return 700; }
 
 const char *mf_last_error(void) { return g_err; }
 
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
-                 const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves, int32_t flags,
-                 int32_t dtype, void *stream)
+                 const mf_hyper_t *hp, int32_t mode, void *qlog, void *elog, int32_t n_waves,
+                 int32_t flags, int32_t dtype, void *stream)
 {
-    return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, nullptr, qlog, n_factors,
-                               biased, hp, mode, n_waves, flags, dtype, stream);
+    if (elog && mode != MF_MODE_LOG) return set_err(MF_E_ARG, "elog needs MF_MODE_LOG");
+    return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, nullptr, qlog, elog,
+                               n_factors, biased, hp, mode, n_waves, flags, dtype, stream);
 }
 
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
@@ -1746,8 +1920,8 @@ int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, v
                    const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves,
                    int32_t flags, int32_t dtype, void *stream)
 {
-    return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, n_factors, 1, hp,
-                              mode, n_waves, flags, dtype, stream);
+    return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, nullptr,
+                              n_factors, 1, hp, mode, n_waves, flags, dtype, stream);
 }
 
 int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *out, int32_t dtype,
@@ -1790,6 +1964,37 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
     if (dtype == MF_F64) return run(double{});
     return set_err(MF_E_ARG, "bad dtype");
 }
+
+int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_factors,
+                  const mf_csr_t *csr, const void *qb, const mf_hyper_t *hp, const int32_t *perm,
+                  const int32_t *ck_pos, const int32_t *piece_beg, int64_t n_pieces, void *sums,
+                  int32_t dtype, void *stream)
+{
+    if (n_pieces < 0 || ldq < n_factors + 1 || n_factors < 0) return set_err(MF_E_ARG, "bad shape");
+    if (n_pieces == 0) return 0;
+    if (!qlog || !elog || !csr || !qb || !hp || !perm || !ck_pos || !piece_beg || !sums)
+        return set_err(MF_E_ARG, "null argument");
+    if ((int64_t)ldq * (dtype == MF_F64 ? 8 : 4) > 512)
+        return set_err(MF_E_UNSUPPORTED, "checkpoint log: ldq * size <= 512 B only");
+    const int64_t cap = (int64_t)n_cus() * MF_REPLAY_WPC;
+    const int g = grid_for_waves(n_pieces < cap ? n_pieces : cap);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MF_F32)
+        hipLaunchKernelGGL((log_replay_kernel<float, 1>), dim3(g), dim3(kBlock), 0, st,
+                           (const float *)qlog, (const float *)elog, ldq, n_factors, csr->items,
+                           (const float *)qb, csr->n_items, (float)hp->lr_pu, (float)hp->reg_pu,
+                           perm, ck_pos, piece_beg, n_pieces, (float *)sums);
+    else if (dtype == MF_F64)
+        hipLaunchKernelGGL((log_replay_kernel<double, 1>), dim3(g), dim3(kBlock), 0, st,
+                           (const double *)qlog, (const double *)elog, ldq, n_factors, csr->items,
+                           (const double *)qb, csr->n_items, hp->lr_pu, hp->reg_pu, perm, ck_pos,
+                           piece_beg, n_pieces, (double *)sums);
+    else
+        return set_err(MF_E_ARG, "bad dtype");
+    return check_launch("log_replay_kernel");
+}
+
+int mf_ckpt_interval(void) { return kCkpt; }
 
 int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
                  const void *sums, const int32_t *item_piece_ptr, const int32_t *totals,

@@ -18,6 +18,7 @@ allocates device memory, supplies the stream and runs the RCCL all-reduce.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -66,12 +67,22 @@ def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS):
     return perm, piece_beg, item_piece_ptr, counts.astype(np.int32)
 
 
+def ckpt_positions(row_ptr, perm, interval):
+    """Checkpoint position of every log position (mf_log_replay's ck_pos): for rating k of user
+    u, k - ((k - row_ptr[u]) mod interval)."""
+    row_ptr = np.asarray(row_ptr, np.int64)
+    k = np.asarray(perm, np.int64)
+    u = np.searchsorted(row_ptr, k, side="right") - 1
+    return (k - ((k - row_ptr[u]) % interval)).astype(np.int32)
+
+
 class MFEngine(ItemSync):
     """SVD / SVD++ SGD on one GPU (one rank of a multi-GPU job)."""
 
     def __init__(self, csr, n_items, n_factors, *, algo="svd", hyper=None, biased=True,
                  dtype="float32", mode="log", n_chunks=1, users=None, deterministic=False,
-                 user_order=None, n_waves=0, device=None, ld=None, world=1, merge="count"):
+                 user_order=None, n_waves=0, device=None, ld=None, world=1, merge="count",
+                 ckpt=None):
         torch = _lib.require_gpu()
         self.torch = torch
         self.algo = algo
@@ -105,7 +116,9 @@ class MFEngine(ItemSync):
         # ---- CSR + schedules
         dev = self.dev
         self.row_ptr = torch.from_numpy(np.ascontiguousarray(row_ptr)).to(dev)
-        self.items = torch.from_numpy(np.ascontiguousarray(items, np.int32)).to(dev)
+        # (padded: mf_log_replay reads up to mf_ckpt_interval() positions past a rating)
+        self.items = torch.from_numpy(np.concatenate([np.asarray(items, np.int32),
+                                                      np.zeros(64, np.int32)])).to(dev)
         self.ratings = torch.from_numpy(np.ascontiguousarray(ratings, np.float64)).to(
             dev, self.tdt)
         self._csr = _lib.MfCsr(self.row_ptr.data_ptr(), self.items.data_ptr(),
@@ -143,6 +156,7 @@ class MFEngine(ItemSync):
         self.u_lo = int(self.users.min()) if len(self.users) else 0
         self.u_hi = int(self.users.max()) + 1 if len(self.users) else 0
         self.qlog = None
+        self.ckpt = False
         if self.mode == _lib.MF_MODE_LOG:
             k_lo, k_hi = int(row_ptr[self.u_lo]), int(row_ptr[self.u_hi])
             deg = np.diff(row_ptr)
@@ -153,6 +167,17 @@ class MFEngine(ItemSync):
             # the kernels index the log by absolute CSR position k
             self._qlog_base = self.qlog.data_ptr() - k_lo * ldq * esz
             self.sums = z(max(lg["n_pieces"] for lg in self.logs), ldq)
+            # SVD with one-group rows: the checkpoint form (a user row every mf_ckpt_interval()
+            # ratings + err per rating; mf_log_replay rebuilds the gradients)
+            if ckpt is None:
+                ckpt = os.environ.get("SURPRISE_AMD_CKPT", "1") != "0"
+            self.ckpt = bool(ckpt) and algo == "svd" and ldq * esz <= 512
+            if self.ckpt:
+                self.elog = z(k_hi - k_lo + 64)
+                self._elog_base = self.elog.data_ptr() - k_lo * esz
+                C = _lib.load().mf_ckpt_interval()
+                for c, lg in zip(chunks, self.logs):
+                    lg["ck"] = to_dev(ckpt_positions(row_ptr, lg["perm"].cpu().numpy(), C))
         snap_q = self.world > 1 and self.mode != _lib.MF_MODE_LOG
         self.qb_s = z(I, ldq) if snap_q else None
         self.yj_s = z(I, ld) if (self.world > 1 and self.yj is not None) else None
@@ -208,12 +233,13 @@ class MFEngine(ItemSync):
 
     def _epoch(self, sched, n_sched, n_waves, flags, st):
         qlog = ctypes.c_void_p(self._qlog_base) if self.is_log else None
+        elog = ctypes.c_void_p(self._elog_base) if self.ckpt else None
         flags |= _lib.MF_EPOCH_DUP_ITEMS if self.dup_items else 0
         if self.algo == "svd":
             _lib.call("mf_svd_epoch", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
                       self.ldq, self.K, int(self.biased), ctypes.byref(self._hyper), self.mode,
-                      qlog, n_waves, flags, self.dtype, st)
+                      qlog, elog, n_waves, flags, self.dtype, st)
         else:
             _lib.call("mf_svdpp_epoch", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
@@ -241,7 +267,14 @@ class MFEngine(ItemSync):
         self._epoch(s, s.numel(), self.n_waves, 0, st)
         if "end" in ev:
             ev["end"].record(self.stream)
-        if self.is_log:
+        if self.is_log and self.ckpt:
+            lg = self.logs[c]
+            _lib.call("mf_log_replay", ctypes.c_void_p(self._qlog_base),
+                      ctypes.c_void_p(self._elog_base), self.ldq, self.K, ctypes.byref(self._csr),
+                      self._ptr(self.qb), ctypes.byref(self._hyper), self._ptr(lg["perm"]),
+                      self._ptr(lg["ck"]), self._ptr(lg["pb"]), lg["n_pieces"],
+                      self._ptr(self.sums), self.dtype, st)
+        elif self.is_log:
             lg = self.logs[c]
             _lib.call("mf_log_reduce", ctypes.c_void_p(self._qlog_base), self.ldq, self.K + 1,
                       self._ptr(lg["perm"]), self._ptr(lg["pb"]), lg["n_pieces"],
