@@ -144,7 +144,9 @@ int mf_ckpt_interval(void);
 
 /*
  * Delta-log merge, step 2: S_i = sum of sums[p] over p in [item_piece_ptr[i], item_piece_ptr[i+1])
- * (item_piece_ptr NULL: S_i = sums[i], e.g. after an all-reduce).  delta_out (nullable,
+ * (item_piece_ptr NULL: S_i = sums[i], e.g. after an all-reduce), plus -- when sums2 is not NULL
+ * (a chunk whose users were logged as two groups, e.g. on two streams) -- the sum of sums2[p] over
+ * p in [item_piece_ptr2[i], item_piece_ptr2[i+1]), added in that order.  delta_out (nullable,
  * [n_items][ld]) receives S; apply != 0 turns the summed gradients into the summed item steps,
  * D_i = lr o (S_i - N reg o qb[i])  (lr, reg = lr_qi, reg_qi in columns < n_factors and lr_bi,
  * reg_bi in bias_col; bias_col < 0: none), N = totals[i] (ratings of item i in the chunk, all
@@ -155,9 +157,10 @@ int mf_ckpt_interval(void);
  *                   in factor columns, <p^2> = p2stat[0] / p2stat[1] (mf_sumsq's two doubles).
  */
 int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
-                 const void *sums, const int32_t *item_piece_ptr, const int32_t *totals,
-                 const mf_hyper_t *hp, const double *p2stat, int32_t rule, void *delta_out,
-                 int32_t apply, int32_t dtype, void *stream);
+                 const void *sums, const int32_t *item_piece_ptr, const void *sums2,
+                 const int32_t *item_piece_ptr2, const int32_t *totals, const mf_hyper_t *hp,
+                 const double *p2stat, int32_t rule, void *delta_out, int32_t apply, int32_t dtype,
+                 void *stream);
 
 /* Merge rules of mf_item_merge. */
 #define MF_MERGE_SUM   0 /* delta = sum_r d_r                                                      */

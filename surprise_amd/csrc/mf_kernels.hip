@@ -1284,6 +1284,9 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
 #ifndef MF_REPLAY_U
 #define MF_REPLAY_U 8  // ratings per replay group
 #endif
+#ifndef MF_REPLAY_NT
+#define MF_REPLAY_NT 0  // 1: checkpoint rows read non-temporally (measured slower)
+#endif
 #ifndef MF_REPLAY_WPC
 #define MF_REPLAY_WPC 16  // replay waves per CU
 #endif
@@ -1358,7 +1361,9 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
                 const int x = x0 + y < kWave ? x0 + y : kWave - 1;
                 const T *row = ckpt + (int64_t)readlane(c_l, x) * ldq;
 #pragma unroll
-                for (int v = 0; v < G; ++v) p[y][v] = *(const vec *)(row + cc[v]);
+                for (int v = 0; v < G; ++v)  // (non-temporal: keep L2 for the item rows)
+                    p[y][v] = MF_REPLAY_NT ? __builtin_nontemporal_load((const vec *)(row + cc[v]))
+                                           : *(const vec *)(row + cc[v]);
 #pragma unroll
                 for (int m = 0; m < kR; ++m) {
                     const uint32_t off = readlane((int)qo_l[m], x);
@@ -1409,7 +1414,8 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     T *__restrict__ qb, int n_items, int ld, int n_fac, int bias_col, const T *__restrict__ sums,
-    const int32_t *__restrict__ item_piece_ptr, const int32_t *__restrict__ totals,
+    const int32_t *__restrict__ item_piece_ptr, const T *__restrict__ sums2,
+    const int32_t *__restrict__ item_piece_ptr2, const int32_t *__restrict__ totals,
     int count_rule, double eta_bias, double lr_fac, double reg_fac, double lr_f, double reg_f,
     double lr_b, double reg_b, const double *__restrict__ p2stat, T *__restrict__ delta_out,
     int apply)
@@ -1428,9 +1434,12 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
         T acc[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) acc[v] = T(0);
-        {
-            const int p0 = item_piece_ptr ? item_piece_ptr[i] : (int)i;
-            const int p1 = item_piece_ptr ? item_piece_ptr[i + 1] : (int)i + 1;
+        // the item's pieces in sums, then (split log) its pieces in sums2, in that fixed order
+        for (int part = 0; part < (sums2 ? 2 : 1); ++part) {
+            const T *__restrict__ sp = part ? sums2 : sums;
+            const int32_t *__restrict__ ipp = part ? item_piece_ptr2 : item_piece_ptr;
+            const int p0 = ipp ? ipp[i] : (int)i;
+            const int p1 = ipp ? ipp[i + 1] : (int)i + 1;
             constexpr int kU = 8;  // independent loads in flight
             for (int pc = p0; pc < p1; pc += kU) {
                 T g[kU][V];
@@ -1439,7 +1448,7 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
 #pragma unroll
                     for (int v = 0; v < V; ++v)
                         g[a][v] = (pc + a < p1 && lane + kWave * v < ld)
-                                      ? sums[(int64_t)(pc + a) * ld + lane + kWave * v] : T(0);
+                                      ? sp[(int64_t)(pc + a) * ld + lane + kWave * v] : T(0);
 #pragma unroll
                 for (int a = 0; a < kU; ++a)
 #pragma unroll
@@ -1901,7 +1910,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 700; }
+int mf_version(void) { return 800; }
 
 const char *mf_last_error(void) { return g_err; }
 
@@ -1997,10 +2006,12 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
 int mf_ckpt_interval(void) { return kCkpt; }
 
 int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
-                 const void *sums, const int32_t *item_piece_ptr, const int32_t *totals,
-                 const mf_hyper_t *hp, const double *p2stat, int32_t rule, void *delta_out,
-                 int32_t apply, int32_t dtype, void *stream)
+                 const void *sums, const int32_t *item_piece_ptr, const void *sums2,
+                 const int32_t *item_piece_ptr2, const int32_t *totals, const mf_hyper_t *hp,
+                 const double *p2stat, int32_t rule, void *delta_out, int32_t apply, int32_t dtype,
+                 void *stream)
 {
+    if (sums2 && !item_piece_ptr2) return set_err(MF_E_ARG, "sums2 needs item_piece_ptr2");
     if (n_items < 0 || ld < 1 || n_factors < 0 || n_factors > ld || bias_col >= ld)
         return set_err(MF_E_ARG, "bad shape");
     if (rule != MF_MERGE_SUM && rule != MF_MERGE_COUNT) return set_err(MF_E_ARG, "bad merge rule");
@@ -2021,7 +2032,8 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
         return dispatch_v<T>(ld, [&](auto vc) -> int {
             hipLaunchKernelGGL((log_apply_kernel<T, decltype(vc)::value>), dim3(g), dim3(kBlock), 0,
                                st, (T *)qb, n_items, ld, n_factors, bias_col, (const T *)sums,
-                               item_piece_ptr, totals, count_rule, eta_b, lr_c, reg_c, lr_f,
+                               item_piece_ptr, (const T *)sums2, item_piece_ptr2, totals,
+                               count_rule, eta_b, lr_c, reg_c, lr_f,
                                reg_f, lr_b, reg_b, p2stat, (T *)delta_out, apply);
             return check_launch("log_apply_kernel");
         });

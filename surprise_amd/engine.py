@@ -67,6 +67,19 @@ def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS):
     return perm, piece_beg, item_piece_ptr, counts.astype(np.int32)
 
 
+def split_heavy(users, row_ptr, heavy):
+    """[rest, heaviest] of a chunk's users (schedule order kept): the heaviest are those with
+    >= heavy * the largest degree.  One group only when either would be empty."""
+    users = np.asarray(users, np.int32)
+    deg = np.diff(np.asarray(row_ptr, np.int64))[users]
+    if not len(users) or heavy <= 0:
+        return [users]
+    h = deg >= heavy * deg.max()
+    if h.all() or not h.any():
+        return [users]
+    return [users[~h], users[h]]
+
+
 def ckpt_positions(row_ptr, perm, interval):
     """Checkpoint position of every log position (mf_log_replay's ck_pos): for rating k of user
     u, k - ((k - row_ptr[u]) mod interval)."""
@@ -82,7 +95,7 @@ class MFEngine(ItemSync):
     def __init__(self, csr, n_items, n_factors, *, algo="svd", hyper=None, biased=True,
                  dtype="float32", mode="log", n_chunks=1, users=None, deterministic=False,
                  user_order=None, n_waves=0, device=None, ld=None, world=1, merge="count",
-                 ckpt=None):
+                 ckpt=None, heavy=None):
         torch = _lib.require_gpu()
         self.torch = torch
         self.algo = algo
@@ -130,17 +143,44 @@ class MFEngine(ItemSync):
         else:
             chunks = chunk_users(self.users, row_ptr, self.n_chunks)
         to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-        self.sched = [to_dev(np.asarray(c, np.int32)) for c in chunks]
+        esz_q = self.ldq * esz
+        # SVD with one-group rows logs in checkpoint form (a user row every mf_ckpt_interval()
+        # ratings + err per rating; mf_log_replay rebuilds the gradients)
+        if ckpt is None:
+            ckpt = os.environ.get("SURPRISE_AMD_CKPT", "1") != "0"
+        self.ckpt = (self.mode == _lib.MF_MODE_LOG and bool(ckpt) and algo == "svd"
+                     and esz_q <= 512)
+        # ... and then splits each chunk's users in two launches on two streams: the heaviest
+        # users (>= heavy * the chunk's largest degree: their sequential chains bound the epoch)
+        # beside the rest, whose log replay then overlaps the heavy chains
+        if heavy is None:
+            heavy = float(os.environ.get("SURPRISE_AMD_HEAVY", "0"))
+        C = _lib.load().mf_ckpt_interval() if self.ckpt else 0
+        self.side = torch.cuda.Stream(device=dev) if self.ckpt and heavy > 0 else None
+        self.sched = []
         self._totals_local = []
-        self.logs = []  # "log" mode: per chunk, see _log_chunk
+        self.logs = []  # "log" mode: per chunk, the item grouping of the log (log_layout)
         for c in chunks:
-            if self.mode == _lib.MF_MODE_LOG:
-                perm, pb, ipp, cnt = log_layout(row_ptr, items, c, self.n_items)
-                self.logs.append(dict(perm=to_dev(perm), pb=to_dev(pb), ipp=to_dev(ipp),
-                                      n_pieces=len(pb) - 1))
-            else:
-                cnt = item_counts(c, row_ptr, items, self.n_items).astype(np.int32)
-            self._totals_local.append(cnt)
+            c = np.asarray(c, np.int32)
+            if self.mode != _lib.MF_MODE_LOG:
+                self.sched.append(to_dev(c))
+                self._totals_local.append(
+                    item_counts(c, row_ptr, items, self.n_items).astype(np.int32))
+                continue
+            parts = split_heavy(c, row_ptr, heavy) if self.side is not None else [c]
+            lgs = []
+            for us in parts:
+                perm, pb, ipp, cnt = log_layout(row_ptr, items, us, self.n_items)
+                lg = dict(sched=to_dev(us), perm=to_dev(perm), pb=to_dev(pb), ipp=to_dev(ipp),
+                          n_pieces=len(pb) - 1, cnt=cnt)
+                if self.ckpt:
+                    lg["ck"] = to_dev(ckpt_positions(row_ptr, perm, C))
+                lgs.append(lg)
+            main = lgs[0]
+            main["heavy"] = lgs[1] if len(lgs) > 1 else None
+            self.sched.append(main["sched"])
+            self.logs.append(main)
+            self._totals_local.append(sum(lg.pop("cnt") for lg in lgs).astype(np.int32))
         self.counts = [to_dev(t) for t in self._totals_local]  # this rank's n_r per chunk
         self.totals = None  # set by _prepare(): summed over every rank
         self.work = torch.zeros(2, dtype=torch.float64, device=dev)  # {sum pu^2, count}
@@ -156,7 +196,6 @@ class MFEngine(ItemSync):
         self.u_lo = int(self.users.min()) if len(self.users) else 0
         self.u_hi = int(self.users.max()) + 1 if len(self.users) else 0
         self.qlog = None
-        self.ckpt = False
         if self.mode == _lib.MF_MODE_LOG:
             k_lo, k_hi = int(row_ptr[self.u_lo]), int(row_ptr[self.u_hi])
             deg = np.diff(row_ptr)
@@ -166,18 +205,12 @@ class MFEngine(ItemSync):
             self.qlog = z(max(k_hi - k_lo, 1), ldq)
             # the kernels index the log by absolute CSR position k
             self._qlog_base = self.qlog.data_ptr() - k_lo * ldq * esz
-            self.sums = z(max(lg["n_pieces"] for lg in self.logs), ldq)
-            # SVD with one-group rows: the checkpoint form (a user row every mf_ckpt_interval()
-            # ratings + err per rating; mf_log_replay rebuilds the gradients)
-            if ckpt is None:
-                ckpt = os.environ.get("SURPRISE_AMD_CKPT", "1") != "0"
-            self.ckpt = bool(ckpt) and algo == "svd" and ldq * esz <= 512
+            # per chunk: the main group's piece sums, then the heavy group's
+            self.sums = z(max(lg["n_pieces"] + (lg["heavy"]["n_pieces"] if lg["heavy"] else 0)
+                              for lg in self.logs), ldq)
             if self.ckpt:
                 self.elog = z(k_hi - k_lo + 64)
                 self._elog_base = self.elog.data_ptr() - k_lo * esz
-                C = _lib.load().mf_ckpt_interval()
-                for c, lg in zip(chunks, self.logs):
-                    lg["ck"] = to_dev(ckpt_positions(row_ptr, lg["perm"].cpu().numpy(), C))
         snap_q = self.world > 1 and self.mode != _lib.MF_MODE_LOG
         self.qb_s = z(I, ldq) if snap_q else None
         self.yj_s = z(I, ld) if (self.world > 1 and self.yj is not None) else None
@@ -249,9 +282,12 @@ class MFEngine(ItemSync):
     def run_chunk(self, c: int, events=None):
         """Run chunk c: the epoch kernel, preceded in "log" mode by the <pu^2> reduction of the
         merge's count-aware weights (taken at the chunk start, like the oracle) and followed by
-        the reduction of the chunk's delta log into per-piece sums (mf_log_reduce); the fold
-        into the table happens in sync_items.  events: optional dict of torch.cuda.Event,
-        "start" / "end" recorded around the epoch kernel on its stream."""
+        the reduction of the chunk's log into per-piece sums (mf_log_reduce, or mf_log_replay
+        for the checkpoint form); the fold into the table happens in sync_items.  A split chunk
+        runs its heavy users' epoch + replay on the side stream beside the rest, joined before
+        returning.  events: optional dict of torch.cuda.Event: "start" (main stream, before the
+        epoch kernels), "end" (after the main epoch kernel), "end_h" (after the heavy one)."""
+        torch = self.torch
         s = self.sched[c]
         st = self._st()
         ev = events or {}
@@ -264,21 +300,41 @@ class MFEngine(ItemSync):
                       st)
         if "start" in ev:
             ev["start"].record(self.stream)
+        lg = self.logs[c] if self.is_log else None
+        hv = lg["heavy"] if lg is not None else None
+        if hv is not None:  # heavy users: their own launch (one wave each) on the side stream
+            fork = torch.cuda.Event()
+            fork.record(self.stream)
+            self.side.wait_event(fork)
+            sh = ctypes.c_void_p(self.side.cuda_stream)
+            n_h = hv["sched"].numel()
+            self._epoch(hv["sched"], n_h, n_h, 0, sh)
+            if "end_h" in ev:
+                ev["end_h"].record(self.side)
+            self._reduce_log(hv, self.sums.data_ptr() +
+                             lg["n_pieces"] * self.ldq * self.sums.element_size(), sh)
+            join = torch.cuda.Event()
+            join.record(self.side)
         self._epoch(s, s.numel(), self.n_waves, 0, st)
         if "end" in ev:
             ev["end"].record(self.stream)
-        if self.is_log and self.ckpt:
-            lg = self.logs[c]
+        if lg is not None:
+            self._reduce_log(lg, self.sums.data_ptr(), st)
+        if hv is not None:
+            self.stream.wait_event(join)
+
+    def _reduce_log(self, lg, sums_ptr, st):
+        """Piece sums of one user group's log: mf_log_replay (checkpoint form) or mf_log_reduce."""
+        if self.ckpt:
             _lib.call("mf_log_replay", ctypes.c_void_p(self._qlog_base),
                       ctypes.c_void_p(self._elog_base), self.ldq, self.K, ctypes.byref(self._csr),
                       self._ptr(self.qb), ctypes.byref(self._hyper), self._ptr(lg["perm"]),
                       self._ptr(lg["ck"]), self._ptr(lg["pb"]), lg["n_pieces"],
-                      self._ptr(self.sums), self.dtype, st)
-        elif self.is_log:
-            lg = self.logs[c]
+                      ctypes.c_void_p(sums_ptr), self.dtype, st)
+        else:
             _lib.call("mf_log_reduce", ctypes.c_void_p(self._qlog_base), self.ldq, self.K + 1,
                       self._ptr(lg["perm"]), self._ptr(lg["pb"]), lg["n_pieces"],
-                      self._ptr(self.sums), self.dtype, st)
+                      ctypes.c_void_p(sums_ptr), self.dtype, st)
 
     def _prepare(self, ctx):
         """Global per-item rating counts of every chunk (all ranks) for the count-aware rules."""
@@ -309,9 +365,13 @@ class MFEngine(ItemSync):
         """mf_log_apply of the current chunk (its pieces were reduced in run_chunk)."""
         c = getattr(self, "_chunk", 0)
         lg = self.logs[c]
+        hv = lg["heavy"]
         count = self._count_rule()
+        sums2 = (ctypes.c_void_p(self.sums.data_ptr() + lg["n_pieces"] * self.ldq *
+                                 self.sums.element_size()) if hv is not None else None)
         _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K,
-                  self._bias_col, self._ptr(self.sums), self._ptr(lg["ipp"]),
+                  self._bias_col, self._ptr(self.sums), self._ptr(lg["ipp"]), sums2,
+                  self._ptr(hv["ipp"]) if hv is not None else None,
                   self._ptr(self._totals()[c]), ctypes.byref(self._hyper),
                   self._ptr(self.work), _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM,
                   None if delta_out is None else self._ptr(delta_out), int(apply), self.dtype,
@@ -385,7 +445,8 @@ class MFEngine(ItemSync):
         if self.is_log:  # bufs[-1] is the all-reduced sum of squares of pu
             count = self._count_rule()
             _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K,
-                      self._bias_col, self._ptr(bufs[0]), None, self._ptr(self._totals()[c]),
+                      self._bias_col, self._ptr(bufs[0]), None, None, None,
+                      self._ptr(self._totals()[c]),
                       ctypes.byref(self._hyper), self._ptr(bufs[-1]),
                       _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM, None, 1, self.dtype, st)
             x = 1

@@ -20,7 +20,7 @@ ts, _ = next(KFold(5, random_state=0).split(Dataset.load_from_arrays(u, i, r)))
 rp, it, rt = ts.csr()
 hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02, reg_pu=.02,
              reg_qi=.02, global_mean=float(ts.global_mean))
-eng = MFEngine((rp, it, rt), ts.n_items, K, hyper=hyper, mode=mode, algo=algo)
+eng = MFEngine((rp, it, rt), ts.n_items, K, hyper=hyper, mode=mode, algo=algo, heavy=0)
 rng = np.random.RandomState(0)
 eng.set_factors(rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K)),
                 yj=rng.normal(0, .1, (ts.n_items, K)) if algo == "svdpp" else None)
