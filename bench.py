@@ -8,7 +8,8 @@ Workload (one "step" = one epoch = one pass of the HIP SGD kernel over the train
 
 Prints ONE JSON line on rank 0 with the contract fields plus:
   roofline      the epoch kernel's algorithmic bytes / its HIP-event-timed launch duration
-                (merge_ms_per_chunk: the delta-log fold + all-reduce that follows it)
+                (every EVENT_EVERY-th step is instrumented; rest_of_step_ms: the log replay +
+                fold, or the multi-rank merge + all-reduce, that follows the epoch kernel)
   cpu_baseline  the fp64 C restatement of the reference loop (oracle/), 1 host thread
   rmse          held-out RMSE of a full 20-epoch fit vs the fp64 sequential oracle (same seed)
 """
@@ -24,6 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); 6.29 TB/s measured copy
+EVENT_EVERY = 4  # steps between HIP-event-instrumented steps
 
 
 def parse():
@@ -112,20 +114,23 @@ def main():
         ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    # The epoch kernel's duration is taken with HIP events on the stream it runs on, on every
+    # EVENT_EVERY-th step of the timed region: a recorded timing event idles the GPU for a few us
+    # (measured: ~12 us per instrumented step of ~0.25 ms), which the other steps do not pay.
+    for step in range(args.steps):
         for c in range(eng.n_chunks):
-            ev = {k: torch.cuda.Event(enable_timing=True)
-                  for k in ("start", "end", "end_h", "step_end")}
+            if step % EVENT_EVERY or os.environ.get("BENCH_NO_EVENTS"):
+                eng.run_chunk(c)
+                eng.sync_items(ctx)
+                continue
+            ev = {k: torch.cuda.Event(enable_timing=True) for k in ("start", "end", "end_h")}
             eng.run_chunk(c, events=ev)  # HIP events on the streams the kernels run on
             eng.sync_items(ctx)
-            ev["step_end"].record(stream)
             recs.append((c, ev))
     torch.cuda.synchronize()
     if ctx is not None:
         ctx.barrier()
     elapsed = time.perf_counter() - t0
-    # per chunk: the epoch kernel, and the rest of the step (log reduction + fold, or the
-    # multi-rank merge + all-reduce)
     # (a split chunk runs its heaviest users' epoch kernel on a second stream: the epoch phase
     # ends with the later of the two launches)
     def span(ev):
@@ -133,8 +138,7 @@ def main():
         if eng.logs and eng.logs[0].get("heavy") is not None:
             t = max(t, ev["start"].elapsed_time(ev["end_h"]))
         return t
-    kern_ms = [span(ev) for _, ev in recs]
-    merge_ms = [ev["start"].elapsed_time(ev["step_end"]) - span(ev) for _, ev in recs]
+    kern_ms = [span(ev) for _, ev in recs] or [float("nan")]
     if ctx is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -181,7 +185,9 @@ def main():
                           "launch_ms": launch_ms,
                           "algorithmic_bytes_per_update": K_bytes,
                           "updates_per_launch": per_launch_updates,
-                          "merge_ms_per_chunk": float(np.mean(merge_ms))}
+                          "instrumented_steps": len(recs),
+                          "rest_of_step_ms": elapsed / args.steps * 1e3 / eng.n_chunks
+                          - launch_ms}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

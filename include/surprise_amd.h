@@ -81,7 +81,7 @@ typedef struct mf_csr {
  *               rating k of the CSR (the user row before the rating's step; whole rows written,
  *               zero padding included); each user's segment must be < 2^30
  *               bytes (|I_u| * ldq * sizeof(dtype)).  Other modes: NULL.
- *   elog      : NULL, or (MF_MODE_LOG, ldq * sizeof(dtype) <= 512 B) the checkpoint form of the
+ *   elog      : NULL, or (MF_MODE_LOG, ldq * sizeof(dtype) <= 1 KiB) the checkpoint form of the
  *               log: device [nnz + mf_ckpt_interval()] errors, elog[k] = err_k, and qlog row k
  *               holds [p_u | 1 | 0..] before rating k only where k - row_ptr[u] is a multiple of
  *               mf_ckpt_interval() (other rows are not written); mf_log_replay rebuilds the
@@ -132,7 +132,7 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
  * c_k = ck_pos[x] <= k (x = the rating's index in perm; c_k = k - ((k - row_ptr[u]) mod
  * mf_ckpt_interval())) by the epoch kernel's recursion p <- ap * p + err_m * lr_pu * q_{item(m)}
  * (ap = 1 - lr_pu * reg_pu on factor columns) over the snapshot item rows qb -- call it before
- * mf_log_apply.  Requires ldq * sizeof(dtype) <= 512 B.
+ * mf_log_apply.  Requires ldq * sizeof(dtype) <= 1 KiB.
  */
 int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_factors,
                   const mf_csr_t *csr, const void *qb, const mf_hyper_t *hp, const int32_t *perm,

@@ -748,6 +748,10 @@ __device__ __forceinline__ void epoch_body(
 #define MF_CKPT 2  // checkpoint interval of the SVD log (elog != NULL): a user row per 2 ratings
 #endif
 constexpr int kCkpt = MF_CKPT;
+#ifndef MF_LA_MAX_G
+#define MF_LA_MAX_G 2  // lookahead body / checkpoint log for rows of up to 2 lane groups (1 KiB)
+#endif
+constexpr int kLaMaxG = MF_LA_MAX_G;
 #ifndef MF_LA_BANK
 #define MF_LA_BANK 8  // ratings per bank in the lookahead body (two banks alternate)
 #endif
@@ -1082,7 +1086,7 @@ __device__ __forceinline__ void epoch_body_la(
 template <typename T, int G, int MODE, bool PP, bool DUPS>
 __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
 {
-    if constexpr (MODE == kLog && !PP && G == 1 && MF_LA) {
+    if constexpr (MODE == kLog && !PP && G <= kLaMaxG && MF_LA) {
         if (elog)
             epoch_body_la<T, G, true>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
                                       qlog, elog, K, biased, hp, n_items, n_waves_req);
@@ -1104,8 +1108,8 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, void *stream)
 {
     // the checkpoint log exists for the lookahead body only: SVD, kLog, one lane group
-    if (elog && (PP || M != kLog || !MF_LA || (int64_t)ldq * sizeof(T) > 512))
-        return set_err(MF_E_UNSUPPORTED, "checkpoint log: SVD, MF_MODE_LOG, ldq * size <= 512 B only");
+    if (elog && (PP || M != kLog || !MF_LA || (int64_t)ldq * sizeof(T) > 512 * kLaMaxG))
+        return set_err(MF_E_UNSUPPORTED, "checkpoint log: SVD, MF_MODE_LOG, ldq * size <= 1 KiB only");
     return dispatch_g<T>(ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         // (kLog reads a snapshot: a repeated item sees the chunk-start row, no forwarding)
@@ -1983,24 +1987,29 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
     if (n_pieces == 0) return 0;
     if (!qlog || !elog || !csr || !qb || !hp || !perm || !ck_pos || !piece_beg || !sums)
         return set_err(MF_E_ARG, "null argument");
-    if ((int64_t)ldq * (dtype == MF_F64 ? 8 : 4) > 512)
-        return set_err(MF_E_UNSUPPORTED, "checkpoint log: ldq * size <= 512 B only");
+    const int64_t rb = (int64_t)ldq * (dtype == MF_F64 ? 8 : 4);
+    if (rb > 512 * kLaMaxG) return set_err(MF_E_UNSUPPORTED, "checkpoint log: ldq * size <= 1 KiB only");
     const int64_t cap = (int64_t)n_cus() * MF_REPLAY_WPC;
     const int g = grid_for_waves(n_pieces < cap ? n_pieces : cap);
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == MF_F32)
-        hipLaunchKernelGGL((log_replay_kernel<float, 1>), dim3(g), dim3(kBlock), 0, st,
-                           (const float *)qlog, (const float *)elog, ldq, n_factors, csr->items,
-                           (const float *)qb, csr->n_items, (float)hp->lr_pu, (float)hp->reg_pu,
-                           perm, ck_pos, piece_beg, n_pieces, (float *)sums);
-    else if (dtype == MF_F64)
-        hipLaunchKernelGGL((log_replay_kernel<double, 1>), dim3(g), dim3(kBlock), 0, st,
-                           (const double *)qlog, (const double *)elog, ldq, n_factors, csr->items,
-                           (const double *)qb, csr->n_items, hp->lr_pu, hp->reg_pu, perm, ck_pos,
-                           piece_beg, n_pieces, (double *)sums);
-    else
-        return set_err(MF_E_ARG, "bad dtype");
-    return check_launch("log_replay_kernel");
+    auto run = [&](auto tag_t) -> int {
+        using T = decltype(tag_t);
+        return dispatch_g<T>(ldq, [&](auto gc) -> int {
+            constexpr int V = decltype(gc)::value;
+            if constexpr (V > kLaMaxG) {
+                return set_err(MF_E_UNSUPPORTED, "checkpoint log: row too long");
+            } else {
+                hipLaunchKernelGGL((log_replay_kernel<T, V>), dim3(g), dim3(kBlock), 0, st,
+                                   (const T *)qlog, (const T *)elog, ldq, n_factors, csr->items,
+                                   (const T *)qb, csr->n_items, (T)hp->lr_pu, (T)hp->reg_pu, perm,
+                                   ck_pos, piece_beg, n_pieces, (T *)sums);
+                return check_launch("log_replay_kernel");
+            }
+        });
+    };
+    if (dtype == MF_F32) return run(float{});
+    if (dtype == MF_F64) return run(double{});
+    return set_err(MF_E_ARG, "bad dtype");
 }
 
 int mf_ckpt_interval(void) { return kCkpt; }

@@ -149,7 +149,7 @@ class MFEngine(ItemSync):
         if ckpt is None:
             ckpt = os.environ.get("SURPRISE_AMD_CKPT", "1") != "0"
         self.ckpt = (self.mode == _lib.MF_MODE_LOG and bool(ckpt) and algo == "svd"
-                     and esz_q <= 512)
+                     and esz_q <= 1024)
         # ... and then splits each chunk's users in two launches on two streams: the heaviest
         # users (>= heavy * the chunk's largest degree: their sequential chains bound the epoch)
         # beside the rest, whose log replay then overlaps the heavy chains
