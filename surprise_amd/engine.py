@@ -406,16 +406,15 @@ class MFEngine(ItemSync):
         self._apply(bufs)
 
     def _delta_buffer(self):
-        """[log sums (log mode)] + [one delta per snapshot table] + [<pu^2> partial (log mode)]"""
+        """[log sums + the <pu^2> partial {sum, count} in its last two elements (log mode)] +
+        [one delta per snapshot table]: log mode all-reduces ONE buffer per chunk."""
         if self._delta is None:
             z = lambda n: self.torch.zeros(n, dtype=self.tdt, device=self.dev)
             bufs = []
             if self.is_log:
-                bufs.append(z(self.n_items * self.ldq))
+                bufs.append(z(self.n_items * self.ldq + 2))
             for tab, snap, ld, _, _ in self._snap_tables():
                 bufs.append(z(self.n_items * ld))
-            if self.is_log:
-                bufs.append(self.work)
             self._delta = bufs
         return self._delta
 
@@ -425,6 +424,7 @@ class MFEngine(ItemSync):
         x = 0
         if self.is_log:
             self._log_fold(bufs[0], False)
+            bufs[0][-2:].copy_(self.work)  # (the statistic rides in the same all-reduce)
             x = 1
         for tab, snap, ld, bias_col, rule in self._snap_tables():
             use_counts = rule != _lib.MF_MERGE_SUM
@@ -442,12 +442,13 @@ class MFEngine(ItemSync):
         c = getattr(self, "_chunk", 0)
         st = self._st()
         x = 0
-        if self.is_log:  # bufs[-1] is the all-reduced sum of squares of pu
+        if self.is_log:  # bufs[0]: the all-reduced sums, then the sum of squares of pu
             count = self._count_rule()
+            self.work.copy_(bufs[0][-2:])
             _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K,
                       self._bias_col, self._ptr(bufs[0]), None, None, None,
                       self._ptr(self._totals()[c]),
-                      ctypes.byref(self._hyper), self._ptr(bufs[-1]),
+                      ctypes.byref(self._hyper), self._ptr(self.work),
                       _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM, None, 1, self.dtype, st)
             x = 1
         for tab, snap, ld, _, _ in self._snap_tables():
