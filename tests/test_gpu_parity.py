@@ -342,3 +342,33 @@ def test_zero_epochs_and_single_rating_users(torch):
     P, f = run_oracle("SVD", params, row_ptr, items, ratings, 3, ts.global_mean)
     a = SVD(**params, dtype="float64", deterministic=True).fit(ts)
     np.testing.assert_allclose(a.pu, f["pu"], atol=1e-9)
+
+
+@pytest.mark.parametrize("K,dtype,chunks", [(20, "float64", 1), (20, "float64", 3),
+                                            (100, "float64", 2), (100, "float32", 1)])
+def test_checkpoint_log_matches_gradient_log(torch, u1, K, dtype, chunks):
+    """The checkpoint log (a user row every mf_ckpt_interval() ratings + err per rating,
+    mf_log_replay rebuilding the gradients, <pu^2> summed inside the replay) against the
+    gradient log (a whole gradient row per rating, mf_log_reduce, mf_sumsq): the same epochs from
+    the same state.  Same arithmetic up to the summation of the statistic and one FMA
+    contraction per rating: fp64 within 1e-10, fp32 within 1e-5."""
+    from surprise_amd import _lib
+    from surprise_amd.engine import MFEngine
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
+                 reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    rng = np.random.RandomState(0)
+    pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
+    out = []
+    for ck in (True, False):
+        eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype=dtype,
+                       mode="log", n_chunks=chunks, ckpt=ck)
+        assert eng.ckpt == ck
+        eng.set_factors(pu0, qi0)
+        eng.run_epochs(4)
+        out.append(eng.get_factors())
+    tol = 1e-10 if dtype == "float64" else 1e-5
+    for k in ("pu", "qi", "bu", "bi"):
+        np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=tol, err_msg=k)
+    assert _lib.load().mf_ckpt_interval() >= 2
