@@ -7,7 +7,7 @@ There is no MovieLens data offline, and uniform random ratings carry no signal
   * r = clip(round(mu + b_u + b_i + <p_u, q_i> + noise), 1, 5) with rank-10 factors
     ~N(0, 0.3), biases ~N(0, 0.5), mu = 3.58, noise ~N(0, 0.9).
 Shapes: ml-100k (943 x 1682, 100,000), ml-1m (6040 x 3706, 1,000,209),
-c4 (2M x 200k, 100M), c5 (10M x 1M, 1B).  The stream is returned in a shuffled
+c4 (2M x 200k, 100M), c5 (10M x 1M, 1B), c5-shard (1.25M x 1M, 125M: c5's per-GPU share).  The stream is returned in a shuffled
 "file order"; raw ids are ints.
 """
 from __future__ import annotations
@@ -20,6 +20,8 @@ SHAPES = {
     "ml-1m": (6040, 3706, 1_000_209),
     "c4": (2_000_000, 200_000, 100_000_000),
     "c5": (10_000_000, 1_000_000, 1_000_000_000),
+    # one rank's shard of c5 on 8 GPUs: 1/8 of the users with their ratings, every item
+    "c5-shard": (1_250_000, 1_000_000, 125_000_000),
 }
 
 

@@ -6,6 +6,7 @@ held-out RMSE (1% of the ratings, seed 0) of the GPU fit next to the fp64 sequen
 (the reference loop restated, oracle/) trained on the same CSR with the same initial factors.
 
     python tools/scale_run.py --shape c4 --factors 128 --epochs 5
+    python tools/scale_run.py --algo svdpp --shape c5-shard --factors 128 --epochs 3 --no-oracle
 """
 import argparse
 import json
@@ -33,8 +34,9 @@ def main():
     p.add_argument("--factors", type=int, default=128)
     p.add_argument("--epochs", type=int, default=5)
     p.add_argument("--holdout", type=float, default=0.01)
-    p.add_argument("--mode", default="log")
+    p.add_argument("--mode", default="auto")
     p.add_argument("--no-oracle", action="store_true")
+    p.add_argument("--algo", default="svd", choices=["svd", "svdpp"])
     a = p.parse_args()
     import torch
     from surprise_amd import synthetic
@@ -58,11 +60,14 @@ def main():
     init = np.random.RandomState(0)
     pu0 = init.normal(0, .1, (U, K))
     qi0 = init.normal(0, .1, (I, K))
-    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
-                 reg_pu=.02, reg_qi=.02, global_mean=gm)
-
-    eng = MFEngine((row_ptr, items, ratings), I, K, hyper=hyper, mode=a.mode)
-    eng.set_factors(pu0, qi0)
+    pp = a.algo == "svdpp"
+    yj0 = init.normal(0, .1, (I, K)) if pp else None
+    lr, reg = (.007, .02) if pp else (.005, .02)  # SVDpp / SVD defaults (mf.pyx:398-407, :140-147)
+    hyper = dict(lr_bu=lr, lr_bi=lr, lr_pu=lr, lr_qi=lr, lr_yj=lr, reg_bu=reg, reg_bi=reg,
+                 reg_pu=reg, reg_qi=reg, reg_yj=reg, global_mean=gm)
+    mode = ("atomic" if pp else "log") if a.mode == "auto" else a.mode
+    eng = MFEngine((row_ptr, items, ratings), I, K, hyper=hyper, mode=mode, algo=a.algo)
+    eng.set_factors(pu0, qi0, yj=yj0)
     torch.cuda.synchronize()
     log("engine ready")
     times = []
@@ -76,16 +81,18 @@ def main():
         times.append(time.perf_counter() - t)
         log("epoch %d: %.2f ms" % (e, times[-1] * 1e3))
     tu_, ti_ = uid[test], iid[test]
-    est, _ = eng.predict(tu_, ti_, gm)
+    est, _ = eng.predict(tu_, ti_, gm, imp=eng.user_implicit() if pp else None)
     est = np.clip(est, 1, 5)
     rmse_gpu = float(np.sqrt(np.mean((r[test] - est) ** 2)))
-    out = {"shape": a.shape, "n_users": U, "n_items": I, "train_ratings": int(len(ratings)),
-           "n_factors": K, "epochs": E, "mode": a.mode,
+    # a reference point that needs no oracle: the RMSE of the global mean on the held-out set
+    out = {"shape": a.shape, "algo": a.algo, "n_users": U, "n_items": I,
+           "train_ratings": int(len(ratings)), "n_factors": K, "epochs": E, "mode": mode,
+           "rmse_global_mean": float(np.sqrt(np.mean((r[test] - gm) ** 2))),
            "epoch_ms": [t * 1e3 for t in times],
            "updates_per_s": len(ratings) / float(np.median(times)),
            "rmse_gpu": rmse_gpu}
     del eng
-    if not a.no_oracle:
+    if not a.no_oracle and not pp:
         import oracle as orc
         hp = orc.hyper(**{k: v for k, v in hyper.items() if k != "global_mean"})
         t = time.perf_counter()
