@@ -1298,6 +1298,9 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
     }
 }
 
+#ifndef MF_EPOCH_WPC
+#define MF_EPOCH_WPC 64  // epoch kernel: default cap on waves per CU
+#endif
 #ifndef MF_REPLAY_U
 #define MF_REPLAY_U 8  // ratings per replay group
 #endif
@@ -1899,7 +1902,11 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
     if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, qlog, dtype)) return rc;
     if (PP && !yj) return set_err(MF_E_ARG, "null yj");
     if (n_sched <= 0) return 0;
-    const int64_t waves = n_waves > 0 ? n_waves : default_waves(n_sched);
+    // default: one wave per user up to MF_EPOCH_WPC waves per CU (then strided): a wave that
+    // finishes its user exits and the dispatcher starts the next one -- measured 5 us faster at
+    // ML-1M than 16 waves/CU taking users in turn (the longest chains start together either way)
+    const int64_t cap = (int64_t)n_cus() * MF_EPOCH_WPC;
+    const int64_t waves = n_waves > 0 ? n_waves : (n_sched < cap ? n_sched : cap);
     auto run = [&](auto tag_t, auto mode_c) -> int {
         using T = decltype(tag_t);
         constexpr int M = decltype(mode_c)::value;

@@ -46,6 +46,8 @@ cases = [("full", order, 0), ("top1", order[:1], 0), ("top16", order[:16], 0),
                     ("top256", order[:256], 0), ("top1024", order[:1024], 0),
                     ("drop-top64", order[64:], 0), ("drop-top256", order[256:], 0),
                     ("full-2048waves", order, 2048), ("full-8192waves", order, 8192)]
+if len(sys.argv) > 3 and sys.argv[3] == "waves":
+    cases = [("full-%dwaves" % w, order, w) for w in (2048, 4096, 6040, 8192, 12288, 16384)]
 if len(sys.argv) > 3 and sys.argv[3] == "fast":
     cases = [c for c in cases if c[0] in ("full", "top1", "drop-top64")]
 for name, s, nw in cases:
