@@ -155,12 +155,14 @@ int mf_ckpt_interval(void);
  *   MF_MERGE_COUNT: w = (1 - (1-eta)^N) / (N eta), N = totals[i] (ratings of item i in the chunk,
  *                   all ranks), eta = lr_bi (1 + reg_bi) in bias_col and lr_qi (<p^2> + reg_qi)
  *                   in factor columns, <p^2> = p2stat[0] / p2stat[1] (mf_sumsq's two doubles).
+ * stat_next (nullable, 2 device doubles, not p2stat): set to {0, 0} -- the next chunk's mf_sumsq
+ * accumulator, cleared here instead of by a separate fill.
  */
 int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
                  const void *sums, const int32_t *item_piece_ptr, const void *sums2,
                  const int32_t *item_piece_ptr2, const int32_t *totals, const mf_hyper_t *hp,
-                 const double *p2stat, int32_t rule, void *delta_out, int32_t apply, int32_t dtype,
-                 void *stream);
+                 const double *p2stat, int32_t rule, void *delta_out, int32_t apply,
+                 double *stat_next, int32_t dtype, void *stream);
 
 /* Merge rules of mf_item_merge. */
 #define MF_MERGE_SUM   0 /* delta = sum_r d_r                                                      */

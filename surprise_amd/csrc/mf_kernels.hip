@@ -1438,8 +1438,9 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     const int32_t *__restrict__ item_piece_ptr2, const int32_t *__restrict__ totals,
     int count_rule, double eta_bias, double lr_fac, double reg_fac, double lr_f, double reg_f,
     double lr_b, double reg_b, const double *__restrict__ p2stat, T *__restrict__ delta_out,
-    int apply)
+    int apply, double *__restrict__ stat_next)
 {
+    if (stat_next && blockIdx.x == 0 && threadIdx.x < 2) stat_next[threadIdx.x] = 0.0;
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -1934,7 +1935,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 800; }
+int mf_version(void) { return 810; }
 
 const char *mf_last_error(void) { return g_err; }
 
@@ -2039,9 +2040,10 @@ int mf_ckpt_interval(void) { return kCkpt; }
 int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
                  const void *sums, const int32_t *item_piece_ptr, const void *sums2,
                  const int32_t *item_piece_ptr2, const int32_t *totals, const mf_hyper_t *hp,
-                 const double *p2stat, int32_t rule, void *delta_out, int32_t apply, int32_t dtype,
-                 void *stream)
+                 const double *p2stat, int32_t rule, void *delta_out, int32_t apply,
+                 double *stat_next, int32_t dtype, void *stream)
 {
+    if (stat_next && stat_next == p2stat) return set_err(MF_E_ARG, "stat_next aliases p2stat");
     if (sums2 && !item_piece_ptr2) return set_err(MF_E_ARG, "sums2 needs item_piece_ptr2");
     if (n_items < 0 || ld < 1 || n_factors < 0 || n_factors > ld || bias_col >= ld)
         return set_err(MF_E_ARG, "bad shape");
@@ -2065,7 +2067,7 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
                                st, (T *)qb, n_items, ld, n_factors, bias_col, (const T *)sums,
                                item_piece_ptr, (const T *)sums2, item_piece_ptr2, totals,
                                count_rule, eta_b, lr_c, reg_c, lr_f,
-                               reg_f, lr_b, reg_b, p2stat, (T *)delta_out, apply);
+                               reg_f, lr_b, reg_b, p2stat, (T *)delta_out, apply, stat_next);
             return check_launch("log_apply_kernel");
         });
     };

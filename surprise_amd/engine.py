@@ -183,7 +183,12 @@ class MFEngine(ItemSync):
             self._totals_local.append(sum(lg.pop("cnt") for lg in lgs).astype(np.int32))
         self.counts = [to_dev(t) for t in self._totals_local]  # this rank's n_r per chunk
         self.totals = None  # set by _prepare(): summed over every rank
-        self.work = torch.zeros(2, dtype=torch.float64, device=dev)  # {sum pu^2, count}
+        # {sum pu^2, count} of the chunk start, double-buffered: chunk t accumulates into slot
+        # t % 2 and its fold clears slot (t + 1) % 2 for the next chunk (no separate fill)
+        self._works = torch.zeros(2, 2, dtype=torch.float64, device=dev)
+        self._wt = 0
+        self._work_cleared = True
+        self.work = self._works[0]
         self.dup_items = int(_has_duplicate_items(row_ptr, items))
 
         # ---- factor tables
@@ -293,7 +298,11 @@ class MFEngine(ItemSync):
         ev = events or {}
         self._chunk = c
         if self.is_log:
-            self.work.zero_()
+            self.work = self._works[self._wt % 2]
+            self._wt += 1
+            if not self._work_cleared:  # (the last chunk was not folded through mf_log_apply)
+                self.work.zero_()
+            self._work_cleared = False
             _lib.call("mf_sumsq", ctypes.c_void_p(self.pu.data_ptr() +
                                                   self.u_lo * self.ld * self.pu.element_size()),
                       self.u_hi - self.u_lo, self.K, self.ld, self._ptr(self.work), self.dtype,
@@ -374,8 +383,13 @@ class MFEngine(ItemSync):
                   self._ptr(hv["ipp"]) if hv is not None else None,
                   self._ptr(self._totals()[c]), ctypes.byref(self._hyper),
                   self._ptr(self.work), _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM,
-                  None if delta_out is None else self._ptr(delta_out), int(apply), self.dtype,
-                  self._st())
+                  None if delta_out is None else self._ptr(delta_out), int(apply),
+                  self._next_work() if apply else None, self.dtype, self._st())
+
+    def _next_work(self):
+        """The next chunk's <pu^2> accumulator, cleared by this chunk's mf_log_apply."""
+        self._work_cleared = True
+        return self._ptr(self._works[self._wt % 2])
 
     def _snap_tables(self):
         """(table, snapshot, ld, bias_col, rule) of the tables merged by snapshot deltas."""
@@ -449,7 +463,8 @@ class MFEngine(ItemSync):
                       self._bias_col, self._ptr(bufs[0]), None, None, None,
                       self._ptr(self._totals()[c]),
                       ctypes.byref(self._hyper), self._ptr(self.work),
-                      _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM, None, 1, self.dtype, st)
+                      _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM, None, 1,
+                      self._next_work(), self.dtype, st)
             x = 1
         for tab, snap, ld, _, _ in self._snap_tables():
             _lib.call("mf_item_apply", self._ptr(tab), self._ptr(snap), self.n_items, ld, 1,

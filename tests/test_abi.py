@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_without_device(lib):
-    assert lib.mf_version() == 800
+    assert lib.mf_version() == 810
     # argument validation happens before any device call
     rc = lib.mf_item_merge(None, None, 10, 16, 10, 10, 1, 0, None, None, None, None, 0, 16,
                            None, None, 1, 0, None)
@@ -41,7 +41,7 @@ def test_version_and_error_without_device(lib):
     assert rc == 1001 and b"null argument" in lib.mf_last_error()
     assert lib.mf_ckpt_interval() in (2, 4, 8, 16)
     rc = lib.mf_log_apply(None, 10, 16, 10, 10, None, None, None, None, None, None, None, 1, None,
-                          1, 0, None)
+                          1, None, 0, None)
     assert rc == 1001 and b"count-aware rule needs" in lib.mf_last_error()
     rc = lib.mf_log_reduce(None, 16, 11, None, None, 5, None, 0, None)
     assert rc == 1001 and b"null argument" in lib.mf_last_error()
