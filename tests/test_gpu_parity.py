@@ -372,3 +372,27 @@ def test_checkpoint_log_matches_gradient_log(torch, u1, K, dtype, chunks):
     for k in ("pu", "qi", "bu", "bi"):
         np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=tol, err_msg=k)
     assert _lib.load().mf_ckpt_interval() >= 2
+
+
+def test_heavy_user_split_matches_single_launch(torch, u1):
+    """The two-stream split (the heaviest users' epoch kernel + replay on a side stream,
+    SURPRISE_AMD_HEAVY; measured slower, off by default) computes the same schedule: per item
+    the two groups' piece sums are added in a fixed order (mf_log_apply's sums2)."""
+    from surprise_amd.engine import MFEngine
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    K = 20
+    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
+                 reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    rng = np.random.RandomState(1)
+    pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
+    out = []
+    for heavy in (0.0, 0.25):
+        eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype="float64",
+                       mode="log", heavy=heavy)
+        assert (eng.logs[0]["heavy"] is not None) == (heavy > 0)
+        eng.set_factors(pu0, qi0)
+        eng.run_epochs(3)
+        out.append(eng.get_factors())
+    for k in ("pu", "qi", "bu", "bi"):
+        np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=1e-10, err_msg=k)
