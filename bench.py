@@ -186,6 +186,11 @@ def main():
                           "algorithmic_bytes_per_update": K_bytes,
                           "updates_per_launch": per_launch_updates,
                           "instrumented_steps": len(recs),
+                          "note": "algorithmic bytes (SURVEY 8(d)) count a gather + scatter of the "
+                                  "user and item rows per rating; the user row stays in registers "
+                                  "and item rows hit L2/MALL, so frac can exceed 1: the epoch "
+                                  "kernel is bound by the heaviest user's sequential chain, "
+                                  "`traffic` is the measured HBM bytes per launch (PMC)",
                           "rest_of_step_ms": elapsed / args.steps * 1e3 / eng.n_chunks
                           - launch_ms}
 
