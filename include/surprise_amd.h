@@ -107,8 +107,22 @@ int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
  */
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
-                   const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves,
+                   const mf_hyper_t *hp, int32_t mode, void *qlog, void *ycbuf, int32_t n_waves,
                    int32_t flags, int32_t dtype, void *stream);
+
+/*
+ * SVD++ deferred y update (MF_MODE_ATOMIC with ycbuf != NULL in mf_svdpp_epoch): the epoch kernel
+ * stores every user's affine-update vector c_u in ycbuf [n_users][ldu] instead of applying
+ * y_j <- A_u y_j + c_u.  This composes, per item j, the maps of the users item_users[x] for x in
+ * the item's pieces (piece p = [piece_beg[p], piece_beg[p+1]), <= 64 entries; the item's pieces
+ * [item_piece_ptr[j], item_piece_ptr[j+1]); users in CSR order), applying them to y_j one user
+ * after the other.  uA [n_users] = A_u = (1 - lr_yj reg_yj)^{|I_u|}; piece_c [n_pieces][ldu] and
+ * piece_A [n_pieces] are scratch.  Race-free and deterministic (a fixed two-level tree).
+ */
+int mf_svdpp_y_fold(void *yj, int32_t ldu, int32_t n_factors, const void *ycbuf, const void *uA,
+                    const int32_t *item_users, const int32_t *piece_beg, int64_t n_pieces,
+                    const int32_t *item_piece_ptr, int32_t n_items, void *piece_c,
+                    void *piece_A, int32_t dtype, void *stream);
 
 /* stat[0] += sum of x[r][c]^2 over r < n_rows, c < n_cols, stat[1] += n_rows * n_cols (x is
  * [n_rows][ld]; stat is two device doubles; both parts add up across ranks).  <pu^2> =

@@ -45,7 +45,9 @@ SIGNATURES = {
     "mf_svd_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32, _i32,
                      ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_svdpp_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp, _i32,
-                       ctypes.POINTER(MfHyper), _i32, _vp, _i32, _i32, _i32, _vp],
+                       ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _i32, _vp],
+    "mf_svdpp_y_fold": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32,
+                        _vp],
     "mf_sumsq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
     "mf_log_reduce": [_vp, _i32, _i32, _vp, _vp, _i64, _vp, _i32, _vp],
     "mf_log_replay": [_vp, _vp, _i32, _i32, ctypes.POINTER(MfCsr), _vp,

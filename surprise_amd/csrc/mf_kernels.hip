@@ -427,8 +427,8 @@ template <typename T, int G, int MODE, bool PP, bool DUPS, int kPF>
 __device__ __forceinline__ void epoch_body(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
-    T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, int K,
-    int biased, Hyper<T> hp, int n_items, int64_t n_waves_req)
+    T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, T *ycbuf,
+    int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -725,6 +725,12 @@ __device__ __forceinline__ void epoch_body(
             vec cacc[G];
 #pragma unroll
             for (int v = 0; v < G; ++v) cacc[v] = (imp[v] - A * imp0[v]) * rs_n;
+            if (ycbuf) {  // deferred: mf_svdpp_y_fold adds every user's c to its y_j after the chunk
+                const rsrc_t c_rs = make_rsrc(ycbuf + (int64_t)u * ldu, (uint32_t)K * sizeof(T));
+#pragma unroll
+                for (int v = 0; v < G; ++v) L::template st<0>(c_rs, cu[v], cacc[v]);
+                return;
+            }
             T cacc1[U];
             to_lane1<G>(cacc, cacc1);
             walk_y([&](T (&g)[kYB][U], uint32_t (&ro)[kYB]) {
@@ -1084,8 +1090,8 @@ __device__ __forceinline__ void epoch_body_la(
         T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, T *elog,\
         int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req
 #define MF_EPOCH_ARGS \
-    row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, K, biased, hp, n_items, \
-        n_waves_req
+    row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, elog, K, biased, hp,    \
+        n_items, n_waves_req
 
 template <typename T, int G, int MODE, bool PP, bool DUPS>
 __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
@@ -1111,9 +1117,12 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, void *stream)
 {
-    // the checkpoint log exists for the lookahead body only: SVD, kLog, one lane group
-    if (elog && (PP || M != kLog || !MF_LA || (int64_t)ldq * sizeof(T) > 512 * kLaMaxG))
+    // elog: SVD: the checkpoint log (the lookahead body: kLog, up to two lane groups);
+    //       SVD++: the deferred y buffer (kAtomic)
+    if (elog && !PP && (M != kLog || !MF_LA || (int64_t)ldq * sizeof(T) > 512 * kLaMaxG))
         return set_err(MF_E_UNSUPPORTED, "checkpoint log: SVD, MF_MODE_LOG, ldq * size <= 1 KiB only");
+    if (elog && PP && M != kAtomic)
+        return set_err(MF_E_UNSUPPORTED, "deferred y: MF_MODE_ATOMIC only");
     return dispatch_g<T>(ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         // (kLog reads a snapshot: a repeated item sees the chunk-start row, no forwarding)
@@ -1747,6 +1756,98 @@ __global__ __launch_bounds__(kBlock) void als_user_kernel(
 
 // ---------------------------------------------------------------- inference
 
+// ---------------------------------------------------------------- SVD++ deferred y update
+//
+// With one wave per user every user of an epoch-chunk gathers the chunk-start y_j anyway; its
+// end-of-user update is the affine map y_j <- A_u y_j + c_u (A_u = (1 - lr_yj reg_yj)^{|I_u|}),
+// which the atomic schedule applies with float atomics in whatever order users finish.
+// Deferred form: the epoch kernel stores c_u (ycbuf[u]); after the chunk the maps of the chunk's
+// users that rated j are composed in CSR (user) order -- race-free, deterministic, no atomics.
+// (Summing the c_u and applying prod A_u once diverges: on a popular item prod A_u ~ e^-80, the
+// early users' c_u must decay with the later users' factors.)  Affine maps compose associatively,
+// (A2, c2) o (A1, c1) = (A2 A1, A2 c1 + c2), so the composition is a two-level tree over the log's
+// pieces (<= 64 ratings of one item): y_piece_kernel composes each piece (one wave, one FMA per
+// user, rows 8 users ahead), y_apply_kernel applies an item's pieces in order.
+template <typename T, int V>
+__global__ __launch_bounds__(kBlock) void y_piece_kernel(
+    int ldu, int K, const T *__restrict__ ycbuf, const T *__restrict__ uA,
+    const int32_t *__restrict__ item_users, const int32_t *__restrict__ piece_beg,
+    int64_t n_pieces, T *__restrict__ pc_c, T *__restrict__ pc_A)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
+        const int b = piece_beg[pc], e = piece_beg[pc + 1];
+        const int my_u = item_users[b + (lane < e - b ? lane : e - b - 1)];  // lane x: user x
+        T cacc[V], Aacc = T(1);
+#pragma unroll
+        for (int v = 0; v < V; ++v) cacc[v] = T(0);
+        constexpr int kU = 8;  // users' rows in flight
+        for (int x = 0; x < e - b; x += kU) {
+            T g[kU][V], A[kU];
+#pragma unroll
+            for (int a = 0; a < kU; ++a) {
+                const bool ok = x + a < e - b;
+                const int64_t u = readlane(my_u, ok ? x + a : 0);
+                A[a] = ok ? uA[u] : T(1);  // (past the piece: the identity map)
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    const int c = lane + kWave * v;
+                    g[a][v] = (ok && c < K) ? ycbuf[u * ldu + c] : T(0);
+                }
+            }
+#pragma unroll
+            for (int a = 0; a < kU; ++a) {
+                Aacc = A[a] * Aacc;
+#pragma unroll
+                for (int v = 0; v < V; ++v) cacc[v] = A[a] * cacc[v] + g[a][v];
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const int c = lane + kWave * v;
+            if (c < ldu) pc_c[pc * ldu + c] = cacc[v];
+        }
+        if (lane == 0) pc_A[pc] = Aacc;
+    }
+}
+
+template <typename T, int V>
+__global__ __launch_bounds__(kBlock) void y_apply_kernel(
+    T *__restrict__ yj, int ldu, int K, const int32_t *__restrict__ item_piece_ptr, int n_items,
+    const T *__restrict__ pc_c, const T *__restrict__ pc_A)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    for (int64_t j = wave; j < n_items; j += n_waves) {
+        const int p0 = item_piece_ptr[j], p1 = item_piece_ptr[j + 1];
+        if (p0 == p1) continue;
+        T y[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const int c = lane + kWave * v;
+            y[v] = c < K ? yj[j * ldu + c] : T(0);
+        }
+        for (int p = p0; p < p1; ++p) {
+            const T A = pc_A[p];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const int c = lane + kWave * v;
+                y[v] = A * y[v] + (c < K ? pc_c[(int64_t)p * ldu + c] : T(0));
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const int c = lane + kWave * v;
+            if (c < K) yj[j * ldu + c] = y[v];
+        }
+    }
+}
+
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void predict_kernel(
     int64_t n, const int32_t *__restrict__ uu, const int32_t *__restrict__ ii,
@@ -1935,7 +2036,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 810; }
+int mf_version(void) { return 820; }
 
 const char *mf_last_error(void) { return g_err; }
 
@@ -1951,10 +2052,10 @@ int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
 
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
-                   const mf_hyper_t *hp, int32_t mode, void *qlog, int32_t n_waves,
+                   const mf_hyper_t *hp, int32_t mode, void *qlog, void *ycbuf, int32_t n_waves,
                    int32_t flags, int32_t dtype, void *stream)
 {
-    return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, nullptr,
+    return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, ycbuf,
                               n_factors, 1, hp, mode, n_waves, flags, dtype, stream);
 }
 
@@ -2036,6 +2137,39 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
 }
 
 int mf_ckpt_interval(void) { return kCkpt; }
+
+int mf_svdpp_y_fold(void *yj, int32_t ldu, int32_t n_factors, const void *ycbuf, const void *uA,
+                    const int32_t *item_users, const int32_t *piece_beg, int64_t n_pieces,
+                    const int32_t *item_piece_ptr, int32_t n_items, void *piece_c,
+                    void *piece_A, int32_t dtype, void *stream)
+{
+    if (n_items < 0 || n_pieces < 0 || ldu < n_factors || n_factors < 0)
+        return set_err(MF_E_ARG, "bad shape");
+    if (n_items == 0 || n_pieces == 0 || n_factors == 0) return 0;
+    if (!yj || !ycbuf || !uA || !item_users || !piece_beg || !item_piece_ptr || !piece_c ||
+        !piece_A)
+        return set_err(MF_E_ARG, "null argument");
+    const int gp = grid_for_waves(default_waves(n_pieces));
+    const int gi = grid_for_waves(default_waves(n_items));
+    hipStream_t st = (hipStream_t)stream;
+    auto run = [&](auto tag_t) -> int {
+        using T = decltype(tag_t);
+        return dispatch_v<T>(ldu, [&](auto vc) -> int {
+            constexpr int V = decltype(vc)::value;
+            hipLaunchKernelGGL((y_piece_kernel<T, V>), dim3(gp), dim3(kBlock), 0, st, ldu,
+                               n_factors, (const T *)ycbuf, (const T *)uA, item_users, piece_beg,
+                               n_pieces, (T *)piece_c, (T *)piece_A);
+            if (int rc = check_launch("y_piece_kernel")) return rc;
+            hipLaunchKernelGGL((y_apply_kernel<T, V>), dim3(gi), dim3(kBlock), 0, st, (T *)yj,
+                               ldu, n_factors, item_piece_ptr, n_items, (const T *)piece_c,
+                               (const T *)piece_A);
+            return check_launch("y_apply_kernel");
+        });
+    };
+    if (dtype == MF_F32) return run(float{});
+    if (dtype == MF_F64) return run(double{});
+    return set_err(MF_E_ARG, "bad dtype");
+}
 
 int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
                  const void *sums, const int32_t *item_piece_ptr, const void *sums2,

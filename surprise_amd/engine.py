@@ -182,6 +182,22 @@ class MFEngine(ItemSync):
             self.logs.append(main)
             self._totals_local.append(sum(lg.pop("cnt") for lg in lgs).astype(np.int32))
         self.counts = [to_dev(t) for t in self._totals_local]  # this rank's n_r per chunk
+        # SVD++ in atomic mode: the end-of-user y update deferred to a per-item fold after each
+        # chunk (mf_svdpp_y_fold; SURPRISE_AMD_YDEFER=0: float atomics at each user's end)
+        self.ydefer = (algo == "svdpp" and self.mode == _lib.MF_MODE_ATOMIC
+                       and not self.deterministic
+                       and os.environ.get("SURPRISE_AMD_YDEFER", "1") != "0")
+        self.ycsc = []
+        if self.ydefer:
+            for us in self.sched:
+                perm, pb, ipp, _ = log_layout(row_ptr, items, us.cpu().numpy(), self.n_items)
+                iusr = (np.searchsorted(row_ptr, perm, side="right") - 1).astype(np.int32)
+                self.ycsc.append(dict(users=to_dev(iusr), pb=to_dev(pb), ipp=to_dev(ipp),
+                                      n_pieces=len(pb) - 1))
+            h = dict(hyper or {})
+            decay = 1.0 - h.get("lr_yj", 0.0) * h.get("reg_yj", 0.0)
+            # A_u = decay^{|I_u|} (the epoch kernel's per-user factor), fp64 on the host
+            self.uA = to_dev(np.power(decay, np.diff(row_ptr).astype(np.float64))).to(self.tdt)
         self.totals = None  # set by _prepare(): summed over every rank
         # {sum pu^2, count} of the chunk start, double-buffered: chunk t accumulates into slot
         # t % 2 and its fold clears slot (t + 1) % 2 for the next chunk (no separate fill)
@@ -197,6 +213,10 @@ class MFEngine(ItemSync):
         self.pu, self.bu = z(U, ld), z(U)
         self.qb = z(I, ldq)
         self.yj = z(I, ld) if algo == "svdpp" else None
+        self.ycbuf = z(U, ld) if self.ydefer else None
+        if self.ydefer:
+            n_pc = max(1, max(y["n_pieces"] for y in self.ycsc))
+            self.ypc_c, self.ypc_A = z(n_pc, ld), z(n_pc)
         # the user rows this rank owns form one range [u_lo, u_hi) (shard_users)
         self.u_lo = int(self.users.min()) if len(self.users) else 0
         self.u_hi = int(self.users.max()) + 1 if len(self.users) else 0
@@ -282,7 +302,8 @@ class MFEngine(ItemSync):
             _lib.call("mf_svdpp_epoch", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
                       self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper),
-                      self.mode, qlog, n_waves, flags, self.dtype, st)
+                      self.mode, qlog, self._ptr(self.ycbuf) if self.ydefer else None,
+                      n_waves, flags, self.dtype, st)
 
     def run_chunk(self, c: int, events=None):
         """Run chunk c: the epoch kernel, preceded in "log" mode by the <pu^2> reduction of the
@@ -327,6 +348,12 @@ class MFEngine(ItemSync):
         self._epoch(s, s.numel(), self.n_waves, 0, st)
         if "end" in ev:
             ev["end"].record(self.stream)
+        if self.ydefer:
+            y = self.ycsc[c]
+            _lib.call("mf_svdpp_y_fold", self._ptr(self.yj), self.ld, self.K,
+                      self._ptr(self.ycbuf), self._ptr(self.uA), self._ptr(y["users"]),
+                      self._ptr(y["pb"]), y["n_pieces"], self._ptr(y["ipp"]), self.n_items,
+                      self._ptr(self.ypc_c), self._ptr(self.ypc_A), self.dtype, st)
         if lg is not None:
             self._reduce_log(lg, self.sums.data_ptr(), st)
         if hv is not None:
