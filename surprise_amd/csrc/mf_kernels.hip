@@ -1121,6 +1121,8 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     //       SVD++: the deferred y buffer (kAtomic)
     if (elog && !PP && (M != kLog || !MF_LA || (int64_t)ldq * sizeof(T) > 512 * kLaMaxG))
         return set_err(MF_E_UNSUPPORTED, "checkpoint log: SVD, MF_MODE_LOG, ldq * size <= 1 KiB only");
+    // (with the kLog snapshot the error stays stale for the whole chunk and the undamped sum of a
+    // popular item's c_u diverges: measured held-out RMSE 1.82 on ML-1M)
     if (elog && PP && M != kAtomic)
         return set_err(MF_E_UNSUPPORTED, "deferred y: MF_MODE_ATOMIC only");
     return dispatch_g<T>(ldq, [&](auto gc) -> int {

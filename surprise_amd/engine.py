@@ -43,6 +43,22 @@ def default_ldq(n_factors: int, dtype: int) -> int:
     return _pad64(n_factors + 1, dtype)
 
 
+def stable_argsort(keys):
+    """np.argsort(keys, kind="stable") for non-negative int keys < 2^32, as LSD radix passes over
+    16-bit digits (numpy radix-sorts 16-bit keys: 5x faster than its int32 merge sort at 1M)."""
+    keys = np.asarray(keys)
+    lo = np.argsort((keys & 0xFFFF).astype(np.uint16), kind="stable")
+    if not len(keys) or int(keys.max()) < (1 << 16):
+        return lo
+    return lo[np.argsort((keys[lo] >> 16).astype(np.uint16), kind="stable")]
+
+
+def position_users(row_ptr):
+    """The user of every CSR position (int32[nnz])."""
+    row_ptr = np.asarray(row_ptr, np.int64)
+    return np.repeat(np.arange(len(row_ptr) - 1, dtype=np.int32), np.diff(row_ptr))
+
+
 def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS):
     """Item grouping of one epoch-chunk's delta-log rows (MF_MODE_LOG).
 
@@ -56,7 +72,7 @@ def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS):
     tot = int(lens.sum())
     ks = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(tot)
     it = np.asarray(items)[ks]
-    perm = ks[np.argsort(it, kind="stable")].astype(np.int32)
+    perm = ks[stable_argsort(it)].astype(np.int32)
     counts = np.bincount(it, minlength=n_items).astype(np.int64)
     offs = np.concatenate([[0], np.cumsum(counts)])
     npc = -(-counts // piece_rows)
@@ -80,12 +96,12 @@ def split_heavy(users, row_ptr, heavy):
     return [users[~h], users[h]]
 
 
-def ckpt_positions(row_ptr, perm, interval):
+def ckpt_positions(row_ptr, perm, interval, pos_user=None):
     """Checkpoint position of every log position (mf_log_replay's ck_pos): for rating k of user
-    u, k - ((k - row_ptr[u]) mod interval)."""
+    u, k - ((k - row_ptr[u]) mod interval).  pos_user: position_users(row_ptr), if at hand."""
     row_ptr = np.asarray(row_ptr, np.int64)
     k = np.asarray(perm, np.int64)
-    u = np.searchsorted(row_ptr, k, side="right") - 1
+    u = (position_users(row_ptr) if pos_user is None else pos_user)[k]
     return (k - ((k - row_ptr[u]) % interval)).astype(np.int32)
 
 
@@ -156,6 +172,8 @@ class MFEngine(ItemSync):
         if heavy is None:
             heavy = float(os.environ.get("SURPRISE_AMD_HEAVY", "0"))
         C = _lib.load().mf_ckpt_interval() if self.ckpt else 0
+        _pu = []
+        pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
         self.side = torch.cuda.Stream(device=dev) if self.ckpt and heavy > 0 else None
         self.sched = []
         self._totals_local = []
@@ -174,7 +192,7 @@ class MFEngine(ItemSync):
                 lg = dict(sched=to_dev(us), perm=to_dev(perm), pb=to_dev(pb), ipp=to_dev(ipp),
                           n_pieces=len(pb) - 1, cnt=cnt)
                 if self.ckpt:
-                    lg["ck"] = to_dev(ckpt_positions(row_ptr, perm, C))
+                    lg["ck"] = to_dev(ckpt_positions(row_ptr, perm, C, pos_user()))
                 lgs.append(lg)
             main = lgs[0]
             main["heavy"] = lgs[1] if len(lgs) > 1 else None
@@ -191,7 +209,7 @@ class MFEngine(ItemSync):
         if self.ydefer:
             for us in self.sched:
                 perm, pb, ipp, _ = log_layout(row_ptr, items, us.cpu().numpy(), self.n_items)
-                iusr = (np.searchsorted(row_ptr, perm, side="right") - 1).astype(np.int32)
+                iusr = pos_user()[perm]
                 self.ycsc.append(dict(users=to_dev(iusr), pb=to_dev(pb), ipp=to_dev(ipp),
                                       n_pieces=len(pb) - 1))
             h = dict(hyper or {})

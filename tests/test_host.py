@@ -246,3 +246,24 @@ def test_nmf_and_baseline_argument_errors():
     algo = BaselineOnly(bsl_options={"method": "wrong_name"})
     with pytest.raises(ValueError, match="Invalid method wrong_name"):
         algo.fit(ts)
+
+
+def test_layout_helpers_match_their_definitions():
+    """engine.stable_argsort = np.argsort(kind="stable") (16-bit radix passes, keys past 2^16
+    included); position_users = the searchsorted definition; log_layout groups by item in
+    increasing CSR position."""
+    from surprise_amd.engine import log_layout, position_users, stable_argsort
+    rng = np.random.RandomState(3)
+    for hi in (1, 7, 3706, 65536, 70000, 1 << 20):
+        keys = rng.randint(0, hi, size=5000).astype(np.int32)
+        np.testing.assert_array_equal(stable_argsort(keys), np.argsort(keys, kind="stable"))
+    assert len(stable_argsort(np.zeros(0, np.int32))) == 0
+    deg = rng.randint(0, 9, size=50)
+    row_ptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    k = np.arange(row_ptr[-1])
+    np.testing.assert_array_equal(position_users(row_ptr),
+                                  np.searchsorted(row_ptr, k, side="right") - 1)
+    items = rng.randint(0, 70000, size=row_ptr[-1]).astype(np.int32)
+    perm, _, _, counts = log_layout(row_ptr, items, np.arange(50), 70000)
+    np.testing.assert_array_equal(perm, np.argsort(items, kind="stable"))
+    np.testing.assert_array_equal(counts, np.bincount(items, minlength=70000))
