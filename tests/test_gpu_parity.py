@@ -396,3 +396,45 @@ def test_heavy_user_split_matches_single_launch(torch, u1):
         out.append(eng.get_factors())
     for k in ("pu", "qi", "bu", "bi"):
         np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=1e-10, err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [20, 100, 130])
+def test_svdpp_y_fold_equals_sequential_composition(torch, K):
+    """mf_svdpp_y_fold (per-piece composition, then each item's pieces in order) equals applying
+    y_j <- A_u y_j + c_u for the item's users one after the other (fp64), on a CSR with items
+    of 0, 1, 64, 65 and ~300 users (several pieces) and K across the lane layouts."""
+    import ctypes
+    from surprise_amd import _lib
+    from surprise_amd.engine import log_layout, position_users
+    rng = np.random.RandomState(5)
+    n_users, n_items = 400, 9
+    pop = np.array([0, 1, 64, 65, 300, 20, 399, 7, 2], np.float64)  # users per item, roughly
+    rows = [np.flatnonzero(rng.rand(n_items) < pop / n_users) for _ in range(n_users)]
+    row_ptr = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
+    items = np.concatenate(rows).astype(np.int32)
+    perm, pb, ipp, cnt = log_layout(row_ptr, items, np.arange(n_users), n_items)
+    assert cnt[0] == 0 and cnt.max() > 64
+    iusr = position_users(row_ptr)[perm]
+    ld = K + (-K % 16)
+    y0 = rng.normal(0, .1, (n_items, ld))
+    c = rng.normal(0, .01, (n_users, ld))
+    A = rng.uniform(.5, 1., n_users)
+    want = y0.copy()
+    for x in range(len(perm)):  # CSR order within every item
+        u, j = iusr[x], items[perm[x]]
+        want[j, :K] = A[u] * want[j, :K] + c[u, :K]
+    dev = "cuda"
+    t = lambda a, dt=torch.float64: torch.tensor(a, dtype=dt, device=dev)
+    y, cb, Ab = t(y0), t(c), t(A)
+    i32 = lambda a: t(np.asarray(a, np.int32), torch.int32)
+    users, pbd, ippd = i32(iusr), i32(pb), i32(ipp)
+    n_pc = len(pb) - 1
+    sc, sa = torch.zeros(n_pc, ld, dtype=torch.float64, device=dev), torch.zeros(n_pc, dtype=torch.float64, device=dev)
+    p = lambda z: ctypes.c_void_p(z.data_ptr())
+    _lib.call("mf_svdpp_y_fold", p(y), ld, K, p(cb), p(Ab), p(users), p(pbd), n_pc, p(ippd),
+              n_items, p(sc), p(sa), _lib.MF_F64, None)
+    torch.cuda.synchronize()
+    got = y.cpu().numpy()
+    np.testing.assert_allclose(got[:, :K], want[:, :K], rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(got[:, K:], y0[:, K:])  # padding columns untouched
