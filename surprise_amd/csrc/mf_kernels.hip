@@ -1770,6 +1770,9 @@ __global__ __launch_bounds__(kBlock) void als_user_kernel(
 // (A2, c2) o (A1, c1) = (A2 A1, A2 c1 + c2), so the composition is a two-level tree over the log's
 // pieces (<= 64 ratings of one item): y_piece_kernel composes each piece (one wave, one FMA per
 // user, rows 8 users ahead), y_apply_kernel applies an item's pieces in order.
+#ifndef MF_YFOLD_U
+#define MF_YFOLD_U 8
+#endif
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void y_piece_kernel(
     int ldu, int K, const T *__restrict__ ycbuf, const T *__restrict__ uA,
@@ -1786,7 +1789,7 @@ __global__ __launch_bounds__(kBlock) void y_piece_kernel(
         T cacc[V], Aacc = T(1);
 #pragma unroll
         for (int v = 0; v < V; ++v) cacc[v] = T(0);
-        constexpr int kU = 8;  // users' rows in flight
+        constexpr int kU = MF_YFOLD_U;  // users' rows in flight
         for (int x = 0; x < e - b; x += kU) {
             T g[kU][V], A[kU];
 #pragma unroll
