@@ -1707,6 +1707,166 @@ __global__ __launch_bounds__(kBlock) void nmf_item_kernel(
     }
 }
 
+// Small rows (NMF's default K=15: a 64-byte row) waste most of a wave in the layouts above and
+// pay a 64-lane reduction per rating.  Segmented layout: the wave is R = 64/S segments of S
+// lanes, E elements per lane (S E >= the row width); segment g takes rating x0 + b R + g, so one
+// step gathers R rows with one load per lane and reduces R dots with log2 S shuffles.  Each
+// segment keeps its own numerator / denominator; the segments are summed once per user / item.
+template <int S, typename T>
+__device__ __forceinline__ T seg_sum(T x) {
+#pragma unroll
+    for (int m = 1; m < S; m <<= 1) x += __shfl_xor(x, m, kWave);
+    return x;
+}
+template <int S, typename T>
+__device__ __forceinline__ T cross_seg_sum(T x) {
+#pragma unroll
+    for (int m = S; m < kWave; m <<= 1) x += __shfl_xor(x, m, kWave);
+    return x;
+}
+
+// unbiased NMF user pass (mf.pyx:697-723 with biased=False: est = dot, the ratings of a user
+// are independent within the epoch)
+template <typename T, int S, int E>
+__global__ __launch_bounds__(kBlock) void nmf_user_seg_kernel(
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
+    const T *__restrict__ ratings, int n_users, const T *__restrict__ pu, T *__restrict__ pu_next,
+    int ldu, const T *__restrict__ qb, int ldq, int K, T reg_pu, T *__restrict__ est_out)
+{
+    constexpr int R = kWave / S, kB = 8;  // R kB ratings' rows in flight per wave
+    const int lane = threadIdx.x & (kWave - 1), seg = lane / S, c0 = (lane % S) * E;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    for (int64_t u = wave; u < n_users; u += n_waves) {
+        const int64_t s = row_ptr[u];
+        const int n = (int)(row_ptr[u + 1] - s);
+        if (n <= 0) continue;
+        T p[E], un[E], ud[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            p[e] = c0 + e < K ? pu[u * ldu + c0 + e] : T(0);
+            un[e] = ud[e] = T(0);
+        }
+        for (int x0 = 0; x0 < n; x0 += R * kB) {
+            T q[kB][E], r[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const int j = x0 + b * R + seg;
+                const bool ok = j < n;
+                const int64_t k = s + (ok ? j : n - 1);
+                const T *qrow = qb + (int64_t)items[k] * ldq;
+                r[b] = ratings[k];
+#pragma unroll
+                for (int e = 0; e < E; ++e) q[b][e] = (ok && c0 + e < ldq) ? qrow[c0 + e] : T(0);
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                T part = T(0);
+#pragma unroll
+                for (int e = 0; e < E; ++e) part += q[b][e] * p[e];
+                const T est = seg_sum<S>(part);  // mf.pyx:703 (unbiased: the dot product)
+#pragma unroll
+                for (int e = 0; e < E; ++e) {   // mf.pyx:712-716 (user side); masked: q = 0
+                    un[e] += q[b][e] * r[b];
+                    ud[e] += q[b][e] * est;
+                }
+                const int j = x0 + b * R + seg;
+                if (j < n && (lane % S) == 0) est_out[s + j] = est;
+            }
+        }
+        const T nreg = (T)n * reg_pu;  // mf.pyx:719-723
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            un[e] = cross_seg_sum<S>(un[e]);
+            ud[e] = cross_seg_sum<S>(ud[e]);
+            const int c = c0 + e;
+            if (seg == 0 && c < ldu)
+                pu_next[u * ldu + c] = c < K ? p[e] * (un[e] / (ud[e] + nreg * p[e])) : T(0);
+        }
+    }
+}
+
+// NMF item pass (mf.pyx:712-716 item side, :726-730), biased or not
+template <typename T, int S, int E, bool BIASED>
+__global__ __launch_bounds__(kBlock) void nmf_item_seg_kernel(
+    const int64_t *__restrict__ csc_ptr, const int64_t *__restrict__ csc_pos,
+    const int32_t *__restrict__ row_user, const T *__restrict__ ratings, const T *__restrict__ est,
+    const T *__restrict__ blog, const T *__restrict__ pu, int ldu, T *__restrict__ qb, int ldq,
+    int K, int n_items, T reg_qi, double eta_b, int count_rule)
+{
+    constexpr int R = kWave / S, kB = 8;
+    const int lane = threadIdx.x & (kWave - 1), seg = lane / S, c0 = (lane % S) * E;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    for (int64_t i = wave; i < n_items; i += n_waves) {
+        const int64_t b0 = csc_ptr[i];
+        const int N = (int)(csc_ptr[i + 1] - b0);
+        T in[E], id[E], bs = T(0);
+#pragma unroll
+        for (int e = 0; e < E; ++e) in[e] = id[e] = T(0);
+        for (int x0 = 0; x0 < N; x0 += R * kB) {
+            T pr[kB][E], r[kB], ev[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const int x = x0 + b * R + seg;
+                const bool ok = x < N;
+                const int64_t k = csc_pos[b0 + (ok ? x : N - 1)];
+                const T *prow = pu + (int64_t)row_user[k] * ldu;
+                r[b] = ratings[k];
+                ev[b] = est[k];
+                if (BIASED && ok && (lane % S) == 0) bs += blog[k];
+#pragma unroll
+                for (int e = 0; e < E; ++e) pr[b][e] = (ok && c0 + e < ldu) ? prow[c0 + e] : T(0);
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b)
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    in[e] += pr[b][e] * r[b];
+                    id[e] += pr[b][e] * ev[b];
+                }
+        }
+        const T nreg = (T)N * reg_qi;
+        T *qrow = qb + i * (int64_t)ldq;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            in[e] = cross_seg_sum<S>(in[e]);
+            id[e] = cross_seg_sum<S>(id[e]);
+            const int c = c0 + e;
+            if (seg == 0 && c < K) {
+                const T qf = qrow[c];
+                qrow[c] = qf * (in[e] / (id[e] + nreg * qf));
+            }
+        }
+        if (BIASED) {
+            const T tot = wave_sum(bs);
+            if (lane == 0) {
+                double w = 1.0;
+                if (count_rule && N > 1) w = -expm1(N * log1p(-eta_b)) / (N * eta_b);
+                qrow[K] += (T)w * tot;
+            }
+        }
+    }
+}
+
+// the segmented layout for rows of <= 32 lanes: f(S, E); 0 when the row is too wide for it
+#ifndef MF_NMF_SEG
+#define MF_NMF_SEG 1
+#endif
+template <typename T, typename F>
+int dispatch_seg(int width, F &&f) {
+    constexpr int E = sizeof(T) == 4 ? 2 : 1;
+    using E_c = std::integral_constant<int, E>;
+    if (!MF_NMF_SEG) return -1;
+    if (width <= 4 * E) return f(std::integral_constant<int, 4>{}, E_c{});
+    if (width <= 8 * E) return f(std::integral_constant<int, 8>{}, E_c{});
+    if (width <= 16 * E) return f(std::integral_constant<int, 16>{}, E_c{});
+    if (width <= 32 * E) return f(std::integral_constant<int, 32>{}, E_c{});
+    return -1;
+}
+
 // ---------------------------------------------------------------- baseline ALS (8(f) 4)
 //
 // baseline_als (optimize_baselines.pyx:14-54): per epoch every item's bias from the current user
@@ -2294,8 +2454,20 @@ int mf_nmf_user_pass(const mf_csr_t *csr, const void *pu, void *pu_next, void *b
     if (csr->n_users <= 0) return 0;
     const int g = grid_for_waves(default_waves(csr->n_users));
     hipStream_t st = (hipStream_t)stream;
+    const int width = ldu > ldq ? ldu : ldq;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
+        if (!biased) {
+            const int rc = dispatch_seg<T>(width, [&](auto sc, auto ec) -> int {
+                constexpr int S = decltype(sc)::value, E = decltype(ec)::value;
+                hipLaunchKernelGGL((nmf_user_seg_kernel<T, S, E>), dim3(g), dim3(kBlock), 0, st,
+                                   csr->row_ptr, csr->items, (const T *)csr->ratings,
+                                   csr->n_users, (const T *)pu, (T *)pu_next, ldu, (const T *)qb,
+                                   ldq, n_factors, (T)hp->reg_pu, (T *)est);
+                return check_launch("nmf_user_seg_kernel");
+            });
+            if (rc >= 0) return rc;
+        }
         return dispatch_g<T>(ldq, [&](auto gc) -> int {
             constexpr int G = decltype(gc)::value;
             auto k = biased ? nmf_user_kernel<T, G, true> : nmf_user_kernel<T, G, false>;
@@ -2328,8 +2500,19 @@ int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32
     const int g = grid_for_waves(default_waves(n_items));
     hipStream_t st = (hipStream_t)stream;
     const double eta_b = hp->lr_bi * (1.0 + hp->reg_bi);
+    const int width = ldu > ldq ? ldu : ldq;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
+        const int rc = dispatch_seg<T>(width, [&](auto sc, auto ec) -> int {
+            constexpr int S = decltype(sc)::value, E = decltype(ec)::value;
+            auto k = biased ? nmf_item_seg_kernel<T, S, E, true> : nmf_item_seg_kernel<T, S, E, false>;
+            hipLaunchKernelGGL(k, dim3(g), dim3(kBlock), 0, st, csc_ptr, csc_pos, row_user,
+                               (const T *)ratings, (const T *)est, (const T *)blog, (const T *)pu,
+                               ldu, (T *)qb, ldq, n_factors, n_items, (T)hp->reg_qi, eta_b,
+                               rule == MF_MERGE_COUNT);
+            return check_launch("nmf_item_seg_kernel");
+        });
+        if (rc >= 0) return rc;
         return dispatch_g<T>(ldq, [&](auto gc) -> int {
             constexpr int G = decltype(gc)::value;
             auto k = biased ? nmf_item_kernel<T, G, true> : nmf_item_kernel<T, G, false>;
