@@ -225,6 +225,11 @@ int mf_item_apply(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
  *   b_i += w * sum of blog (rule MF_MERGE_COUNT: w = (1 - (1-eta)^N) / (N eta),
  *   eta = lr_bi (1 + reg_bi); MF_MERGE_SUM: w = 1).  Call it after the user pass, then swap
  *   pu / pu_next.  pu, pu_next [n_users][ldu]; qb [n_items][ldq] = [q_i | b_i | 0 ...].
+ *   Optional piece form (rows of <= 64 fp32 / 32 fp64 elements; else ignored): every item's CSC
+ *   range cut into pieces of <= 64 ratings, piece p = [piece_beg[p], piece_beg[p+1]) (absolute
+ *   CSC positions, n_pieces+1 entries), the item's pieces [item_piece_ptr[i], item_piece_ptr[i+1]);
+ *   scratch [n_pieces][2 ldq + 1].  The pieces are reduced in parallel and added per item in
+ *   order (deterministic).  piece_beg = NULL: one wave per item.
  */
 int mf_nmf_user_pass(const mf_csr_t *csr, const void *pu, void *pu_next, void *bu, int32_t ldu,
                      const void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
@@ -232,8 +237,9 @@ int mf_nmf_user_pass(const mf_csr_t *csr, const void *pu, void *pu_next, void *b
 int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32_t *row_user,
                      const void *ratings, const void *est, const void *blog, const void *pu,
                      int32_t ldu, void *qb, int32_t ldq, int32_t n_items, int32_t n_factors,
-                     int32_t biased, const mf_hyper_t *hp, int32_t rule, int32_t dtype,
-                     void *stream);
+                     int32_t biased, const mf_hyper_t *hp, int32_t rule,
+                     const int64_t *piece_beg, int64_t n_pieces, const int32_t *item_piece_ptr,
+                     void *scratch, int32_t dtype, void *stream);
 
 /*
  * One epoch of baseline_als (optimize_baselines.pyx:14-54): b_i = sum over ir[i] of

@@ -1851,6 +1851,105 @@ __global__ __launch_bounds__(kBlock) void nmf_item_seg_kernel(
     }
 }
 
+// The one-wave-per-item pass is bound by the most-rated item's chain of dependent gathers
+// (csc_pos -> row_user -> the p_u row, ~6 us per 64 ratings).  Piece form: nmf_item_piece_kernel
+// reduces each <= 64-rating piece of an item's CSC range (one wave, segmented layout) into a
+// scratch row [sum p r | sum p est | sum blog]; nmf_item_fold_kernel adds an item's pieces in
+// order (fixed, deterministic) and takes q_i's step.
+template <typename T, int S, int E, bool BIASED>
+__global__ __launch_bounds__(kBlock) void nmf_item_piece_kernel(
+    const int64_t *__restrict__ csc_pos, const int32_t *__restrict__ row_user,
+    const T *__restrict__ ratings, const T *__restrict__ est, const T *__restrict__ blog,
+    const T *__restrict__ pu, int ldu, int ldq, const int64_t *__restrict__ piece_beg,
+    int64_t n_pieces, T *__restrict__ scratch)
+{
+    constexpr int R = kWave / S, kB = 8;
+    const int lane = threadIdx.x & (kWave - 1), seg = lane / S, c0 = (lane % S) * E;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const int64_t sw = 2 * (int64_t)ldq + 1;
+    for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
+        const int64_t b0 = piece_beg[pc];
+        const int N = (int)(piece_beg[pc + 1] - b0);  // 1 .. 64
+        T in[E], id[E], bs = T(0);
+#pragma unroll
+        for (int e = 0; e < E; ++e) in[e] = id[e] = T(0);
+        for (int x0 = 0; x0 < N; x0 += R * kB) {
+            T pr[kB][E], r[kB], ev[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const int x = x0 + b * R + seg;
+                const bool ok = x < N;
+                const int64_t k = csc_pos[b0 + (ok ? x : N - 1)];
+                const T *prow = pu + (int64_t)row_user[k] * ldu;
+                r[b] = ratings[k];
+                ev[b] = est[k];
+                if (BIASED && ok && (lane % S) == 0) bs += blog[k];
+#pragma unroll
+                for (int e = 0; e < E; ++e) pr[b][e] = (ok && c0 + e < ldu) ? prow[c0 + e] : T(0);
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b)
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    in[e] += pr[b][e] * r[b];
+                    id[e] += pr[b][e] * ev[b];
+                }
+        }
+        T *row = scratch + pc * sw;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            in[e] = cross_seg_sum<S>(in[e]);
+            id[e] = cross_seg_sum<S>(id[e]);
+            const int c = c0 + e;
+            if (seg == 0 && c < ldq) {
+                row[c] = in[e];
+                row[ldq + c] = id[e];
+            }
+        }
+        if (BIASED) {
+            const T tot = wave_sum(bs);
+            if (lane == 0) row[2 * ldq] = tot;
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void nmf_item_fold_kernel(
+    const int64_t *__restrict__ csc_ptr, const int32_t *__restrict__ item_piece_ptr, int n_items,
+    const T *__restrict__ scratch, T *__restrict__ qb, int ldq, int K, T reg_qi, int biased,
+    double eta_b, int count_rule)
+{
+    const int lane = threadIdx.x & (kWave - 1);  // lane = column (ldq <= 64 on this path)
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const int64_t sw = 2 * (int64_t)ldq + 1;
+    for (int64_t i = wave; i < n_items; i += n_waves) {
+        const int N = (int)(csc_ptr[i + 1] - csc_ptr[i]);
+        T in = T(0), id = T(0), bs = T(0);
+        for (int p = item_piece_ptr[i]; p < item_piece_ptr[i + 1]; ++p) {
+            const T *row = scratch + p * sw;
+            if (lane < ldq) {
+                in += row[lane];
+                id += row[ldq + lane];
+            }
+            if (biased) bs += row[2 * ldq];
+        }
+        T *qrow = qb + i * (int64_t)ldq;
+        if (lane < K) {  // mf.pyx:726-730
+            const T qf = qrow[lane];
+            qrow[lane] = qf * (in / (id + (T)N * reg_qi * qf));
+        }
+        if (biased && lane == 0) {
+            double w = 1.0;
+            if (count_rule && N > 1) w = -expm1(N * log1p(-eta_b)) / (N * eta_b);
+            qrow[K] += (T)w * bs;
+        }
+    }
+}
+
 // the segmented layout for rows of <= 32 lanes: f(S, E); 0 when the row is too wide for it
 #ifndef MF_NMF_SEG
 #define MF_NMF_SEG 1
@@ -2201,7 +2300,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 820; }
+int mf_version(void) { return 830; }
 
 const char *mf_last_error(void) { return g_err; }
 
@@ -2487,8 +2586,9 @@ int mf_nmf_user_pass(const mf_csr_t *csr, const void *pu, void *pu_next, void *b
 int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32_t *row_user,
                      const void *ratings, const void *est, const void *blog, const void *pu,
                      int32_t ldu, void *qb, int32_t ldq, int32_t n_items, int32_t n_factors,
-                     int32_t biased, const mf_hyper_t *hp, int32_t rule, int32_t dtype,
-                     void *stream)
+                     int32_t biased, const mf_hyper_t *hp, int32_t rule,
+                     const int64_t *piece_beg, int64_t n_pieces, const int32_t *item_piece_ptr,
+                     void *scratch, int32_t dtype, void *stream)
 {
     if (!csc_ptr || !csc_pos || !row_user || !ratings || !est || !pu || !qb || !hp ||
         (biased && !blog))
@@ -2501,10 +2601,25 @@ int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32
     hipStream_t st = (hipStream_t)stream;
     const double eta_b = hp->lr_bi * (1.0 + hp->reg_bi);
     const int width = ldu > ldq ? ldu : ldq;
+    const bool pieces = piece_beg && item_piece_ptr && scratch && n_pieces > 0;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
         const int rc = dispatch_seg<T>(width, [&](auto sc, auto ec) -> int {
             constexpr int S = decltype(sc)::value, E = decltype(ec)::value;
+            if (pieces) {
+                auto kp = biased ? nmf_item_piece_kernel<T, S, E, true>
+                                 : nmf_item_piece_kernel<T, S, E, false>;
+                hipLaunchKernelGGL(kp, dim3(grid_for_waves(default_waves(n_pieces))), dim3(kBlock),
+                                   0, st, csc_pos, row_user, (const T *)ratings, (const T *)est,
+                                   (const T *)blog, (const T *)pu, ldu, ldq, piece_beg, n_pieces,
+                                   (T *)scratch);
+                if (int e = check_launch("nmf_item_piece_kernel")) return e;
+                hipLaunchKernelGGL(nmf_item_fold_kernel<T>, dim3(g), dim3(kBlock), 0, st, csc_ptr,
+                                   item_piece_ptr, n_items, (const T *)scratch, (T *)qb, ldq,
+                                   n_factors, (T)hp->reg_qi, biased, eta_b,
+                                   rule == MF_MERGE_COUNT);
+                return check_launch("nmf_item_fold_kernel");
+            }
             auto k = biased ? nmf_item_seg_kernel<T, S, E, true> : nmf_item_seg_kernel<T, S, E, false>;
             hipLaunchKernelGGL(k, dim3(g), dim3(kBlock), 0, st, csc_ptr, csc_pos, row_user,
                                (const T *)ratings, (const T *)est, (const T *)blog, (const T *)pu,

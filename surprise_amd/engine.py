@@ -75,12 +75,20 @@ def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS):
     perm = ks[stable_argsort(it)].astype(np.int32)
     counts = np.bincount(it, minlength=n_items).astype(np.int64)
     offs = np.concatenate([[0], np.cumsum(counts)])
+    item_piece_ptr, piece_beg = piece_bounds(offs, counts, piece_rows)
+    return perm, piece_beg.astype(np.int32), item_piece_ptr, counts.astype(np.int32)
+
+
+def piece_bounds(offs, counts, piece_rows=PIECE_ROWS):
+    """Item i's rows [offs[i], offs[i] + counts[i]) cut into pieces of <= piece_rows:
+    (item_piece_ptr int32[n_items+1], piece_beg int64[n_pieces+1], the last = offs[-1])."""
     npc = -(-counts // piece_rows)
     item_piece_ptr = np.concatenate([[0], np.cumsum(npc)]).astype(np.int32)
-    piece_item = np.repeat(np.arange(n_items), npc)
+    piece_item = np.repeat(np.arange(len(counts)), npc)
     local = np.arange(len(piece_item)) - item_piece_ptr[piece_item]
-    piece_beg = np.concatenate([offs[piece_item] + piece_rows * local, [tot]]).astype(np.int32)
-    return perm, piece_beg, item_piece_ptr, counts.astype(np.int32)
+    piece_beg = np.concatenate([offs[piece_item] + piece_rows * local,
+                                [offs[-1]]]).astype(np.int64)
+    return item_piece_ptr, piece_beg
 
 
 def split_heavy(users, row_ptr, heavy):
@@ -608,6 +616,12 @@ class NMFEngine:
         if not self.biased:
             self._hyper.global_mean = 0.0  # mf.pyx:682-683
         self.rule = _lib.MF_MERGE_COUNT if bias_rule == "count" else _lib.MF_MERGE_SUM
+        # the item pass in pieces of <= PIECE_ROWS ratings (mf_nmf_item_pass's piece form)
+        cnt = np.diff(np.asarray(csc_ptr, np.int64))
+        ipp, pb = piece_bounds(np.asarray(csc_ptr, np.int64), cnt)
+        self.piece_beg, self.item_piece_ptr = to_dev(pb), to_dev(ipp)
+        self.n_pieces = len(pb) - 1
+        self.piece_scratch = z(max(self.n_pieces, 1), 2 * self.ldq + 1)
 
     def _ptr(self, t):
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
@@ -630,7 +644,8 @@ class NMFEngine:
                   self._ptr(self.row_user), self._ptr(self.ratings), self._ptr(self.est),
                   self._ptr(self.blog), self._ptr(self.pu), self.ld, self._ptr(self.qb),
                   self.ldq, self.n_items, self.K, int(self.biased), ctypes.byref(self._hyper),
-                  self.rule, self.dtype, st)
+                  self.rule, self._ptr(self.piece_beg), self.n_pieces,
+                  self._ptr(self.item_piece_ptr), self._ptr(self.piece_scratch), self.dtype, st)
         self.pu, self.pu_next = self.pu_next, self.pu
 
     def get_factors(self):
