@@ -230,10 +230,16 @@ int mf_item_apply(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
  *   CSC positions, n_pieces+1 entries), the item's pieces [item_piece_ptr[i], item_piece_ptr[i+1]);
  *   scratch [n_pieces][2 ldq + 1].  The pieces are reduced in parallel and added per item in
  *   order (deterministic).  piece_beg = NULL: one wave per item.
+ *   mf_nmf_user_pass takes the same piece form when unbiased (the biased b_u recursion is a
+ *   chain): the user's CSR range in pieces of <= 64 ratings (absolute CSR positions), the
+ *   user's pieces [user_piece_ptr[u], user_piece_ptr[u+1]), piece_user[p] = its user,
+ *   scratch [n_pieces][2 ldu].  piece_beg = NULL: one wave per user.
  */
 int mf_nmf_user_pass(const mf_csr_t *csr, const void *pu, void *pu_next, void *bu, int32_t ldu,
                      const void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
-                     const mf_hyper_t *hp, void *est, void *blog, int32_t dtype, void *stream);
+                     const mf_hyper_t *hp, void *est, void *blog, const int64_t *piece_beg,
+                     int64_t n_pieces, const int32_t *user_piece_ptr, const int32_t *piece_user,
+                     void *scratch, int32_t dtype, void *stream);
 int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32_t *row_user,
                      const void *ratings, const void *est, const void *blog, const void *pu,
                      int32_t ldu, void *qb, int32_t ldq, int32_t n_items, int32_t n_factors,

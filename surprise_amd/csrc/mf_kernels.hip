@@ -1950,6 +1950,104 @@ __global__ __launch_bounds__(kBlock) void nmf_item_fold_kernel(
     }
 }
 
+// The unbiased user pass in the same piece form (its one-wave-per-user kernel is bound by the
+// most-rated user's chain): nmf_user_piece_kernel takes one <= 64-rating piece of a user's CSR
+// range (its owner piece_user[pc]), writes every rating's estimate and the piece's
+// [sum q r | sum q est] scratch row; nmf_user_fold_kernel adds a user's pieces in order and takes
+// p_u's step into pu_next (mf.pyx:697-723 with biased=False).
+template <typename T, int S, int E>
+__global__ __launch_bounds__(kBlock) void nmf_user_piece_kernel(
+    const int32_t *__restrict__ items, const T *__restrict__ ratings,
+    const T *__restrict__ pu, int ldu, const T *__restrict__ qb, int ldq, int K,
+    const int64_t *__restrict__ piece_beg, const int32_t *__restrict__ piece_user,
+    int64_t n_pieces, T *__restrict__ scratch, T *__restrict__ est_out)
+{
+    constexpr int R = kWave / S, kB = 8;
+    const int lane = threadIdx.x & (kWave - 1), seg = lane / S, c0 = (lane % S) * E;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const int64_t sw = 2 * (int64_t)ldu;
+    for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
+        const int64_t s = piece_beg[pc];
+        const int n = (int)(piece_beg[pc + 1] - s);  // 1 .. 64
+        const int64_t u = piece_user[pc];
+        T p[E], un[E], ud[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            p[e] = c0 + e < K ? pu[u * ldu + c0 + e] : T(0);
+            un[e] = ud[e] = T(0);
+        }
+        for (int x0 = 0; x0 < n; x0 += R * kB) {
+            T q[kB][E], r[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const int j = x0 + b * R + seg;
+                const bool ok = j < n;
+                const int64_t k = s + (ok ? j : n - 1);
+                const T *qrow = qb + (int64_t)items[k] * ldq;
+                r[b] = ratings[k];
+#pragma unroll
+                for (int e = 0; e < E; ++e) q[b][e] = (ok && c0 + e < ldq) ? qrow[c0 + e] : T(0);
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                T part = T(0);
+#pragma unroll
+                for (int e = 0; e < E; ++e) part += q[b][e] * p[e];
+                const T est = seg_sum<S>(part);  // mf.pyx:703
+#pragma unroll
+                for (int e = 0; e < E; ++e) {   // mf.pyx:712-716 (user side); masked: q = 0
+                    un[e] += q[b][e] * r[b];
+                    ud[e] += q[b][e] * est;
+                }
+                const int j = x0 + b * R + seg;
+                if (j < n && (lane % S) == 0) est_out[s + j] = est;
+            }
+        }
+        T *row = scratch + pc * sw;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            un[e] = cross_seg_sum<S>(un[e]);
+            ud[e] = cross_seg_sum<S>(ud[e]);
+            const int c = c0 + e;
+            if (seg == 0 && c < ldu) {
+                row[c] = un[e];
+                row[ldu + c] = ud[e];
+            }
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void nmf_user_fold_kernel(
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ user_piece_ptr, int n_users,
+    const T *__restrict__ scratch, const T *__restrict__ pu, T *__restrict__ pu_next, int ldu,
+    int K, T reg_pu)
+{
+    const int lane = threadIdx.x & (kWave - 1);  // lane = column (ldu <= 64 on this path)
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const int64_t sw = 2 * (int64_t)ldu;
+    for (int64_t u = wave; u < n_users; u += n_waves) {
+        const int n = (int)(row_ptr[u + 1] - row_ptr[u]);
+        if (n <= 0) continue;  // as nmf_user_seg_kernel: no rating, no step
+        T un = T(0), ud = T(0);
+        for (int p = user_piece_ptr[u]; p < user_piece_ptr[u + 1]; ++p) {
+            const T *row = scratch + p * sw;
+            if (lane < ldu) {
+                un += row[lane];
+                ud += row[ldu + lane];
+            }
+        }
+        if (lane < ldu) {  // mf.pyx:719-723
+            const T pf = lane < K ? pu[u * ldu + lane] : T(0);
+            pu_next[u * ldu + lane] = lane < K ? pf * (un / (ud + (T)n * reg_pu * pf)) : T(0);
+        }
+    }
+}
+
 // the segmented layout for rows of <= 32 lanes: f(S, E); 0 when the row is too wide for it
 #ifndef MF_NMF_SEG
 #define MF_NMF_SEG 1
@@ -2300,7 +2398,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 830; }
+int mf_version(void) { return 840; }
 
 const char *mf_last_error(void) { return g_err; }
 
@@ -2543,7 +2641,9 @@ int mf_item_apply(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
 
 int mf_nmf_user_pass(const mf_csr_t *csr, const void *pu, void *pu_next, void *bu, int32_t ldu,
                      const void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
-                     const mf_hyper_t *hp, void *est, void *blog, int32_t dtype, void *stream)
+                     const mf_hyper_t *hp, void *est, void *blog, const int64_t *piece_beg,
+                     int64_t n_pieces, const int32_t *user_piece_ptr, const int32_t *piece_user,
+                     void *scratch, int32_t dtype, void *stream)
 {
     if (!csr || !csr->row_ptr || !csr->items || !csr->ratings) return set_err(MF_E_ARG, "null csr");
     if (!pu || !pu_next || !qb || !hp || !est || (biased && (!bu || !blog)))
@@ -2554,11 +2654,25 @@ int mf_nmf_user_pass(const mf_csr_t *csr, const void *pu, void *pu_next, void *b
     const int g = grid_for_waves(default_waves(csr->n_users));
     hipStream_t st = (hipStream_t)stream;
     const int width = ldu > ldq ? ldu : ldq;
+    const bool pieces = piece_beg && user_piece_ptr && piece_user && scratch && n_pieces > 0;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
         if (!biased) {
             const int rc = dispatch_seg<T>(width, [&](auto sc, auto ec) -> int {
                 constexpr int S = decltype(sc)::value, E = decltype(ec)::value;
+                if (pieces) {
+                    hipLaunchKernelGGL((nmf_user_piece_kernel<T, S, E>),
+                                       dim3(grid_for_waves(default_waves(n_pieces))), dim3(kBlock),
+                                       0, st, csr->items, (const T *)csr->ratings, (const T *)pu,
+                                       ldu, (const T *)qb, ldq, n_factors, piece_beg, piece_user,
+                                       n_pieces, (T *)scratch, (T *)est);
+                    if (int e = check_launch("nmf_user_piece_kernel")) return e;
+                    hipLaunchKernelGGL(nmf_user_fold_kernel<T>, dim3(g), dim3(kBlock), 0, st,
+                                       csr->row_ptr, user_piece_ptr, csr->n_users,
+                                       (const T *)scratch, (const T *)pu, (T *)pu_next, ldu,
+                                       n_factors, (T)hp->reg_pu);
+                    return check_launch("nmf_user_fold_kernel");
+                }
                 hipLaunchKernelGGL((nmf_user_seg_kernel<T, S, E>), dim3(g), dim3(kBlock), 0, st,
                                    csr->row_ptr, csr->items, (const T *)csr->ratings,
                                    csr->n_users, (const T *)pu, (T *)pu_next, ldu, (const T *)qb,

@@ -622,6 +622,14 @@ class NMFEngine:
         self.piece_beg, self.item_piece_ptr = to_dev(pb), to_dev(ipp)
         self.n_pieces = len(pb) - 1
         self.piece_scratch = z(max(self.n_pieces, 1), 2 * self.ldq + 1)
+        # the unbiased user pass in the same piece form over the CSR ranges
+        ucnt = np.diff(row_ptr)
+        upp, upb = piece_bounds(row_ptr, ucnt)
+        self.u_piece_beg, self.user_piece_ptr = to_dev(upb), to_dev(upp)
+        self.u_piece_user = to_dev(np.repeat(np.arange(self.n_users, dtype=np.int32),
+                                             np.diff(upp)))
+        self.u_n_pieces = len(upb) - 1
+        self.u_piece_scratch = z(max(self.u_n_pieces, 1), 2 * self.ld)
 
     def _ptr(self, t):
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
@@ -639,7 +647,9 @@ class NMFEngine:
         _lib.call("mf_nmf_user_pass", ctypes.byref(self._csr), self._ptr(self.pu),
                   self._ptr(self.pu_next), self._ptr(self.bu), self.ld, self._ptr(self.qb),
                   self.ldq, self.K, int(self.biased), ctypes.byref(self._hyper),
-                  self._ptr(self.est), self._ptr(self.blog), self.dtype, st)
+                  self._ptr(self.est), self._ptr(self.blog), self._ptr(self.u_piece_beg),
+                  self.u_n_pieces, self._ptr(self.user_piece_ptr), self._ptr(self.u_piece_user),
+                  self._ptr(self.u_piece_scratch), self.dtype, st)
         _lib.call("mf_nmf_item_pass", self._ptr(self.csc_ptr), self._ptr(self.csc_pos),
                   self._ptr(self.row_user), self._ptr(self.ratings), self._ptr(self.est),
                   self._ptr(self.blog), self._ptr(self.pu), self.ld, self._ptr(self.qb),
