@@ -1915,6 +1915,8 @@ __global__ __launch_bounds__(kBlock) void nmf_item_piece_kernel(
     }
 }
 
+constexpr int kFoldBatch = 8;  // pieces loaded per step of a fold
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void nmf_item_fold_kernel(
     const int64_t *__restrict__ csc_ptr, const int32_t *__restrict__ item_piece_ptr, int n_items,
@@ -1929,13 +1931,26 @@ __global__ __launch_bounds__(kBlock) void nmf_item_fold_kernel(
     for (int64_t i = wave; i < n_items; i += n_waves) {
         const int N = (int)(csc_ptr[i + 1] - csc_ptr[i]);
         T in = T(0), id = T(0), bs = T(0);
-        for (int p = item_piece_ptr[i]; p < item_piece_ptr[i + 1]; ++p) {
-            const T *row = scratch + p * sw;
-            if (lane < ldq) {
-                in += row[lane];
-                id += row[ldq + lane];
+        const int p1 = item_piece_ptr[i + 1];
+        for (int p0 = item_piece_ptr[i]; p0 < p1; p0 += kFoldBatch) {
+            // kFoldBatch pieces' loads in flight, then added in piece order
+            T a[kFoldBatch], d[kFoldBatch], bb[kFoldBatch];
+#pragma unroll
+            for (int b = 0; b < kFoldBatch; ++b) {
+                const bool ok = p0 + b < p1;
+                const T *row = scratch + (int64_t)(ok ? p0 + b : p0) * sw;
+                a[b] = ok && lane < ldq ? row[lane] : T(0);
+                d[b] = ok && lane < ldq ? row[ldq + lane] : T(0);
+                bb[b] = ok && biased ? row[2 * ldq] : T(0);
             }
-            if (biased) bs += row[2 * ldq];
+#pragma unroll
+            for (int b = 0; b < kFoldBatch; ++b) {
+                if (p0 + b < p1) {
+                    in += a[b];
+                    id += d[b];
+                    bs += bb[b];
+                }
+            }
         }
         T *qrow = qb + i * (int64_t)ldq;
         if (lane < K) {  // mf.pyx:726-730
@@ -2034,11 +2049,22 @@ __global__ __launch_bounds__(kBlock) void nmf_user_fold_kernel(
         const int n = (int)(row_ptr[u + 1] - row_ptr[u]);
         if (n <= 0) continue;  // as nmf_user_seg_kernel: no rating, no step
         T un = T(0), ud = T(0);
-        for (int p = user_piece_ptr[u]; p < user_piece_ptr[u + 1]; ++p) {
-            const T *row = scratch + p * sw;
-            if (lane < ldu) {
-                un += row[lane];
-                ud += row[ldu + lane];
+        const int p1 = user_piece_ptr[u + 1];
+        for (int p0 = user_piece_ptr[u]; p0 < p1; p0 += kFoldBatch) {
+            T a[kFoldBatch], d[kFoldBatch];
+#pragma unroll
+            for (int b = 0; b < kFoldBatch; ++b) {
+                const bool ok = p0 + b < p1 && lane < ldu;
+                const T *row = scratch + (int64_t)(p0 + b < p1 ? p0 + b : p0) * sw;
+                a[b] = ok ? row[lane] : T(0);
+                d[b] = ok ? row[ldu + lane] : T(0);
+            }
+#pragma unroll
+            for (int b = 0; b < kFoldBatch; ++b) {
+                if (p0 + b < p1) {
+                    un += a[b];
+                    ud += d[b];
+                }
             }
         }
         if (lane < ldu) {  // mf.pyx:719-723
