@@ -2095,6 +2095,7 @@ int dispatch_seg(int width, F &&f) {
 // baseline_als (optimize_baselines.pyx:14-54): per epoch every item's bias from the current user
 // biases, then every user's bias from the new item biases.  One wave per item / user, lanes
 // over its ratings, one wave sum.
+constexpr int kAlsBatch = 8;  // strides of 64 ratings whose loads are issued together
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void als_item_kernel(
@@ -2110,9 +2111,21 @@ __global__ __launch_bounds__(kBlock) void als_item_kernel(
         const int64_t b = csc_ptr[i];
         const int N = (int)(csc_ptr[i + 1] - b);
         T dev = T(0);
-        for (int x = lane; x < N; x += kWave) {
-            const int64_t k = csc_pos[b + x];
-            dev += ratings[k] - gm - bu[row_user[k]];  // :43-44
+        for (int x0 = lane; x0 < N; x0 += kAlsBatch * kWave) {
+            // kAlsBatch strides' gather chains (csc_pos -> row_user -> bu) in flight, then
+            // added in the lane's x order (the same sums as one stride at a time)
+            int64_t k[kAlsBatch];
+            T t[kAlsBatch];
+#pragma unroll
+            for (int j = 0; j < kAlsBatch; ++j) {
+                const int x = x0 + j * kWave;
+                k[j] = csc_pos[b + (x < N ? x : N - 1)];
+            }
+#pragma unroll
+            for (int j = 0; j < kAlsBatch; ++j) t[j] = ratings[k[j]] - gm - bu[row_user[k[j]]];  // :43-44
+#pragma unroll
+            for (int j = 0; j < kAlsBatch; ++j)
+                if (x0 + j * kWave < N) dev += t[j];
         }
         dev = wave_sum(dev);
         if (lane == 0) bi[i] = dev / (reg_i + (T)N);  // :46
@@ -2133,7 +2146,17 @@ __global__ __launch_bounds__(kBlock) void als_user_kernel(
         const int64_t s = row_ptr[u];
         const int n = (int)(row_ptr[u + 1] - s);
         T dev = T(0);
-        for (int x = lane; x < n; x += kWave) dev += ratings[s + x] - gm - bi[items[s + x]];  // :50-51
+        for (int x0 = lane; x0 < n; x0 += kAlsBatch * kWave) {
+            T t[kAlsBatch];
+#pragma unroll
+            for (int j = 0; j < kAlsBatch; ++j) {
+                const int64_t x = s + (x0 + j * kWave < n ? x0 + j * kWave : n - 1);
+                t[j] = ratings[x] - gm - bi[items[x]];  // :50-51
+            }
+#pragma unroll
+            for (int j = 0; j < kAlsBatch; ++j)
+                if (x0 + j * kWave < n) dev += t[j];
+        }
         dev = wave_sum(dev);
         if (lane == 0) bu[u] = dev / (reg_u + (T)n);  // :52
     }
