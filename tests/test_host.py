@@ -267,3 +267,23 @@ def test_layout_helpers_match_their_definitions():
     perm, _, _, counts = log_layout(row_ptr, items, np.arange(50), 70000)
     np.testing.assert_array_equal(perm, np.argsort(items, kind="stable"))
     np.testing.assert_array_equal(counts, np.bincount(items, minlength=70000))
+
+
+def test_piece_bounds_partition_every_range():
+    """engine.piece_bounds (the NMF / log piece form): each range [offs[i], offs[i]+counts[i])
+    is cut into consecutive pieces of 1..piece_rows rows, owner i's pieces are
+    [ptr[i], ptr[i+1]) in order, empty ranges have none, and the last bound is offs[-1]."""
+    from surprise_amd.engine import piece_bounds
+    rng = np.random.RandomState(5)
+    for rows in (1, 7, 64):
+        counts = rng.choice([0, 1, 63, 64, 65, 200, 1805], size=40)
+        offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        ptr, beg = piece_bounds(offs, counts, rows)
+        assert ptr[0] == 0 and ptr[-1] == len(beg) - 1 and beg[-1] == offs[-1]
+        sizes = np.diff(beg)
+        assert sizes.min() >= 1 and sizes.max() <= rows
+        for i, n in enumerate(counts):
+            b = beg[ptr[i]:ptr[i + 1] + 1]
+            assert ptr[i + 1] - ptr[i] == -(-n // rows)
+            if n:
+                assert b[0] == offs[i] and b[-1] == offs[i + 1]
