@@ -229,7 +229,9 @@ int mf_item_apply(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
  *   range cut into pieces of <= 64 ratings, piece p = [piece_beg[p], piece_beg[p+1]) (absolute
  *   CSC positions, n_pieces+1 entries), the item's pieces [item_piece_ptr[i], item_piece_ptr[i+1]);
  *   scratch [n_pieces][2 ldq + 1].  The pieces are reduced in parallel and added per item in
- *   order (deterministic).  piece_beg = NULL: one wave per item.
+ *   order (deterministic).  piece_beg = NULL: one wave per item.  Optional csc_ratings[nnz] /
+ *   csc_user[nnz] (piece form only; NULL: gathered): ratings[csc_pos[x]] and row_user[csc_pos[x]]
+ *   stored in CSC order, read coalesced.
  *   mf_nmf_user_pass takes the same piece form when unbiased (the biased b_u recursion is a
  *   chain): the user's CSR range in pieces of <= 64 ratings (absolute CSR positions), the
  *   user's pieces [user_piece_ptr[u], user_piece_ptr[u+1]), piece_user[p] = its user,
@@ -245,7 +247,8 @@ int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32
                      int32_t ldu, void *qb, int32_t ldq, int32_t n_items, int32_t n_factors,
                      int32_t biased, const mf_hyper_t *hp, int32_t rule,
                      const int64_t *piece_beg, int64_t n_pieces, const int32_t *item_piece_ptr,
-                     void *scratch, int32_t dtype, void *stream);
+                     void *scratch, const void *csc_ratings, const int32_t *csc_user,
+                     int32_t dtype, void *stream);
 
 /*
  * One epoch of baseline_als (optimize_baselines.pyx:14-54): b_i = sum over ir[i] of

@@ -61,7 +61,8 @@ SIGNATURES = {
     "mf_nmf_user_pass": [ctypes.POINTER(MfCsr), _vp, _vp, _vp, _i32, _vp, _i32, _i32, _i32,
                          ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp],
     "mf_nmf_item_pass": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _i32, _i32, _i32,
-                         ctypes.POINTER(MfHyper), _i32, _vp, _i64, _vp, _vp, _i32, _vp],
+                         ctypes.POINTER(MfHyper), _i32, _vp, _i64, _vp, _vp, _vp, _vp, _i32,
+                         _vp],
     "mf_baseline_als_epoch": [ctypes.POINTER(MfCsr), _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl,
                               _i32, _vp],
     "mf_predict": [_i64, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _dbl, _vp, _vp,

@@ -1861,8 +1861,12 @@ __global__ __launch_bounds__(kBlock) void nmf_item_piece_kernel(
     const int64_t *__restrict__ csc_pos, const int32_t *__restrict__ row_user,
     const T *__restrict__ ratings, const T *__restrict__ est, const T *__restrict__ blog,
     const T *__restrict__ pu, int ldu, int ldq, const int64_t *__restrict__ piece_beg,
-    int64_t n_pieces, T *__restrict__ scratch)
+    int64_t n_pieces, T *__restrict__ scratch, const T *__restrict__ csc_ratings,
+    const int32_t *__restrict__ csc_user)
 {
+    // csc_ratings / csc_user (optional): the ratings and their users already in CSC order, read
+    // coalesced at CSC position b0 + x instead of gathered through k (two fewer 4-byte random
+    // reads per rating, each a whole cache line); est stays gathered
     constexpr int R = kWave / S, kB = 8;
     const int lane = threadIdx.x & (kWave - 1), seg = lane / S, c0 = (lane % S) * E;
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
@@ -1881,9 +1885,10 @@ __global__ __launch_bounds__(kBlock) void nmf_item_piece_kernel(
             for (int b = 0; b < kB; ++b) {
                 const int x = x0 + b * R + seg;
                 const bool ok = x < N;
-                const int64_t k = csc_pos[b0 + (ok ? x : N - 1)];
-                const T *prow = pu + (int64_t)row_user[k] * ldu;
-                r[b] = ratings[k];
+                const int64_t xp = b0 + (ok ? x : N - 1);
+                const int64_t k = csc_pos[xp];
+                const T *prow = pu + (int64_t)(csc_user ? csc_user[xp] : row_user[k]) * ldu;
+                r[b] = csc_ratings ? csc_ratings[xp] : ratings[k];
                 ev[b] = est[k];
                 if (BIASED && ok && (lane % S) == 0) bs += blog[k];
 #pragma unroll
@@ -2447,7 +2452,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 840; }
+int mf_version(void) { return 850; }
 
 const char *mf_last_error(void) { return g_err; }
 
@@ -2751,7 +2756,8 @@ int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32
                      int32_t ldu, void *qb, int32_t ldq, int32_t n_items, int32_t n_factors,
                      int32_t biased, const mf_hyper_t *hp, int32_t rule,
                      const int64_t *piece_beg, int64_t n_pieces, const int32_t *item_piece_ptr,
-                     void *scratch, int32_t dtype, void *stream)
+                     void *scratch, const void *csc_ratings, const int32_t *csc_user,
+                     int32_t dtype, void *stream)
 {
     if (!csc_ptr || !csc_pos || !row_user || !ratings || !est || !pu || !qb || !hp ||
         (biased && !blog))
@@ -2775,7 +2781,7 @@ int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32
                 hipLaunchKernelGGL(kp, dim3(grid_for_waves(default_waves(n_pieces))), dim3(kBlock),
                                    0, st, csc_pos, row_user, (const T *)ratings, (const T *)est,
                                    (const T *)blog, (const T *)pu, ldu, ldq, piece_beg, n_pieces,
-                                   (T *)scratch);
+                                   (T *)scratch, (const T *)csc_ratings, csc_user);
                 if (int e = check_launch("nmf_item_piece_kernel")) return e;
                 hipLaunchKernelGGL(nmf_item_fold_kernel<T>, dim3(g), dim3(kBlock), 0, st, csc_ptr,
                                    item_piece_ptr, n_items, (const T *)scratch, (T *)qb, ldq,

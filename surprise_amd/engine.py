@@ -622,6 +622,9 @@ class NMFEngine:
         self.piece_beg, self.item_piece_ptr = to_dev(pb), to_dev(ipp)
         self.n_pieces = len(pb) - 1
         self.piece_scratch = z(max(self.n_pieces, 1), 2 * self.ldq + 1)
+        # ratings / users in CSC order (static): the item pieces read them coalesced
+        self.csc_ratings = self.ratings[self.csc_pos].contiguous()
+        self.csc_user = self.row_user[self.csc_pos].contiguous()
         # the unbiased user pass in the same piece form over the CSR ranges
         ucnt = np.diff(row_ptr)
         upp, upb = piece_bounds(row_ptr, ucnt)
@@ -655,7 +658,8 @@ class NMFEngine:
                   self._ptr(self.blog), self._ptr(self.pu), self.ld, self._ptr(self.qb),
                   self.ldq, self.n_items, self.K, int(self.biased), ctypes.byref(self._hyper),
                   self.rule, self._ptr(self.piece_beg), self.n_pieces,
-                  self._ptr(self.item_piece_ptr), self._ptr(self.piece_scratch), self.dtype, st)
+                  self._ptr(self.item_piece_ptr), self._ptr(self.piece_scratch),
+                  self._ptr(self.csc_ratings), self._ptr(self.csc_user), self.dtype, st)
         self.pu, self.pu_next = self.pu_next, self.pu
 
     def get_factors(self):
