@@ -253,12 +253,14 @@ int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32
 /*
  * One epoch of baseline_als (optimize_baselines.pyx:14-54): b_i = sum over ir[i] of
  * (r - mu - b_u) / (reg_i + |ir[i]|) for every item, then b_u = sum over ur[u] of
- * (r - mu - b_i) / (reg_u + |ur[u]|) for every user.  csc as for mf_nmf_item_pass.
+ * (r - mu - b_i) / (reg_u + |ur[u]|) for every user.  csc as for mf_nmf_item_pass, and the optional
+ * CSC-ordered csc_ratings / csc_user the same way (NULL: gathered through csc_pos).
  * (baseline_sgd, :57-84, is mf_svd_epoch with n_factors = 0.)
  */
 int mf_baseline_als_epoch(const mf_csr_t *csr, const int64_t *csc_ptr, const int64_t *csc_pos,
                           const int32_t *row_user, void *bu, void *bi, double global_mean,
-                          double reg_u, double reg_i, int32_t dtype, void *stream);
+                          double reg_u, double reg_i, const void *csc_ratings,
+                          const int32_t *csc_user, int32_t dtype, void *stream);
 
 /*
  * Batched SVD.estimate (matrix_factorization.pyx:269-299): for x < n, with u[x] < 0 / i[x] < 0

@@ -64,7 +64,7 @@ SIGNATURES = {
                          ctypes.POINTER(MfHyper), _i32, _vp, _i64, _vp, _vp, _vp, _vp, _i32,
                          _vp],
     "mf_baseline_als_epoch": [ctypes.POINTER(MfCsr), _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl,
-                              _i32, _vp],
+                              _vp, _vp, _i32, _vp],
     "mf_predict": [_i64, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _dbl, _vp, _vp,
                    _i32, _vp],
     "mf_svdpp_user_implicit": [ctypes.POINTER(MfCsr), _vp, _i32, _vp, _i32, _i32, _vp],

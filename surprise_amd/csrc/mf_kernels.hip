@@ -2106,8 +2106,11 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void als_item_kernel(
     const int64_t *__restrict__ csc_ptr, const int64_t *__restrict__ csc_pos,
     const int32_t *__restrict__ row_user, const T *__restrict__ ratings, const T *__restrict__ bu,
-    T *__restrict__ bi, int n_items, T gm, T reg_i)
+    T *__restrict__ bi, int n_items, T gm, T reg_i, const T *__restrict__ csc_ratings,
+    const int32_t *__restrict__ csc_user)
 {
+    // csc_ratings / csc_user (optional): CSC-ordered copies, read coalesced (no csc_pos hop)
+    const bool direct = csc_ratings && csc_user;
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -2119,15 +2122,24 @@ __global__ __launch_bounds__(kBlock) void als_item_kernel(
         for (int x0 = lane; x0 < N; x0 += kAlsBatch * kWave) {
             // kAlsBatch strides' gather chains (csc_pos -> row_user -> bu) in flight, then
             // added in the lane's x order (the same sums as one stride at a time)
-            int64_t k[kAlsBatch];
             T t[kAlsBatch];
+            if (direct) {
 #pragma unroll
-            for (int j = 0; j < kAlsBatch; ++j) {
-                const int x = x0 + j * kWave;
-                k[j] = csc_pos[b + (x < N ? x : N - 1)];
+                for (int j = 0; j < kAlsBatch; ++j) {
+                    const int x = x0 + j * kWave;
+                    const int64_t xp = b + (x < N ? x : N - 1);
+                    t[j] = csc_ratings[xp] - gm - bu[csc_user[xp]];  // :43-44
+                }
+            } else {
+                int64_t k[kAlsBatch];
+#pragma unroll
+                for (int j = 0; j < kAlsBatch; ++j) {
+                    const int x = x0 + j * kWave;
+                    k[j] = csc_pos[b + (x < N ? x : N - 1)];
+                }
+#pragma unroll
+                for (int j = 0; j < kAlsBatch; ++j) t[j] = ratings[k[j]] - gm - bu[row_user[k[j]]];
             }
-#pragma unroll
-            for (int j = 0; j < kAlsBatch; ++j) t[j] = ratings[k[j]] - gm - bu[row_user[k[j]]];  // :43-44
 #pragma unroll
             for (int j = 0; j < kAlsBatch; ++j)
                 if (x0 + j * kWave < N) dev += t[j];
@@ -2452,7 +2464,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 850; }
+int mf_version(void) { return 860; }
 
 const char *mf_last_error(void) { return g_err; }
 
@@ -2814,7 +2826,8 @@ int mf_nmf_item_pass(const int64_t *csc_ptr, const int64_t *csc_pos, const int32
 
 int mf_baseline_als_epoch(const mf_csr_t *csr, const int64_t *csc_ptr, const int64_t *csc_pos,
                           const int32_t *row_user, void *bu, void *bi, double global_mean,
-                          double reg_u, double reg_i, int32_t dtype, void *stream)
+                          double reg_u, double reg_i, const void *csc_ratings,
+                          const int32_t *csc_user, int32_t dtype, void *stream)
 {
     if (!csr || !csr->row_ptr || !csr->items || !csr->ratings) return set_err(MF_E_ARG, "null csr");
     if (!csc_ptr || !csc_pos || !row_user || !bu || !bi) return set_err(MF_E_ARG, "null argument");
@@ -2826,7 +2839,8 @@ int mf_baseline_als_epoch(const mf_csr_t *csr, const int64_t *csc_ptr, const int
         if (csr->n_items > 0) {
             hipLaunchKernelGGL(als_item_kernel<T>, dim3(gi), dim3(kBlock), 0, st, csc_ptr, csc_pos,
                                row_user, (const T *)csr->ratings, (const T *)bu, (T *)bi,
-                               csr->n_items, (T)global_mean, (T)reg_i);
+                               csr->n_items, (T)global_mean, (T)reg_i, (const T *)csc_ratings,
+                               csc_user);
             if (int rc = check_launch("als_item_kernel")) return rc;
         }
         if (csr->n_users > 0) {

@@ -700,6 +700,7 @@ def baseline_als_device(csr, csc, n_items, global_mean, n_epochs, reg_u, reg_i,
     rt = to_dev(np.asarray(ratings, np.float64)).to(tdt)
     cp, cs = to_dev(np.asarray(csc[0], np.int64)), to_dev(np.asarray(csc[1], np.int64))
     ru = to_dev(np.repeat(np.arange(n_users, dtype=np.int32), np.diff(row_ptr)))
+    crt, cru = rt[cs].contiguous(), ru[cs].contiguous()  # CSC-ordered copies (coalesced reads)
     bu = torch.zeros(n_users, dtype=tdt, device=dev)
     bi = torch.zeros(n_items, dtype=tdt, device=dev)
     c = _lib.MfCsr(rp.data_ptr(), it.data_ptr(), rt.data_ptr(), n_users, int(n_items))
@@ -707,6 +708,6 @@ def baseline_als_device(csr, csc, n_items, global_mean, n_epochs, reg_u, reg_i,
     p = lambda x: ctypes.c_void_p(x.data_ptr())
     for _ in range(n_epochs):
         _lib.call("mf_baseline_als_epoch", ctypes.byref(c), p(cp), p(cs), p(ru), p(bu), p(bi),
-                  float(global_mean), float(reg_u), float(reg_i), dt, st)
+                  float(global_mean), float(reg_u), float(reg_i), p(crt), p(cru), dt, st)
     torch.cuda.current_stream(dev).synchronize()
     return bu.to(torch.float64).cpu().numpy(), bi.to(torch.float64).cpu().numpy()

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_without_device(lib):
-    assert lib.mf_version() == 850
+    assert lib.mf_version() == 860
     # argument validation happens before any device call
     rc = lib.mf_item_merge(None, None, 10, 16, 10, 10, 1, 0, None, None, None, None, 0, 16,
                            None, None, 1, 0, None)
