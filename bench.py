@@ -1,21 +1,35 @@
-"""Benchmark: rating-updates/sec of the SVD SGD hot path on MI355X (BASELINE.json configs[1]).
+"""Benchmark: rating-updates/sec of the SVD / SVD++ SGD hot path on MI355X.
 
-Workload (one "step" = one epoch = one pass of the HIP SGD kernel over the train fold):
-  SVD n_factors=100, fp32 on the device, synthetic planted ML-1M shape (6040 users x 3706
-  items x 1,000,209 ratings), KFold(5, random_state=0) fold 0 -> 800,167 training ratings.
-  N GPUs: weak scaling -- every rank owns its own 6040-user shard of that shape over the
-  same 3706 items; item deltas are SUM-all-reduced over RCCL once per epoch-chunk.
+Default (N=1): BASELINE configs[1] -- SVD n_factors=100, fp32 on the device, synthetic planted
+ML-1M shape (6040 users x 3706 items x 1,000,209 ratings, surprise_amd.synthetic), KFold(5,
+random_state=0) fold 0 -> 800,167 training ratings.  One "step" = one epoch over them.
+
+--gpus N (one process per GPU; spawned here when WORLD_SIZE is unset, or launched by
+torch.distributed.run): every rank holds ONLY its own user rows on its device.
+  --shape ml-1m (default)  weak scaling: rank r trains user population r of one dataset (r = 0
+                           is the single-GPU dataset above; every population is ML-1M-shaped and
+                           rates the same 3706 items, synthetic.population) -- per-GPU work fixed
+  --shape c4 | c5          strong scaling: BASELINE configs[3] / [4] (2M x 200k x 100M, SVD
+                           K=128 / 10M x 1M x 1B, SVD++ K=128; 1% held out), sharded by user
+                           range; each rank generates only its own rows (synthetic.sharded_rows)
+Item-side updates are SUM-all-reduced once per epoch-chunk (RCCL; `--backend gloo` only to
+rehearse several ranks on one GPU).
 
 Prints ONE JSON line on rank 0 with the contract fields plus:
-  roofline      the epoch kernel's algorithmic bytes / its HIP-event-timed launch duration
-                (every EVENT_EVERY-th step is instrumented; rest_of_step_ms: the log replay +
-                fold, or the multi-rank merge + all-reduce, that follows the epoch kernel)
-  cpu_baseline  the fp64 C restatement of the reference loop (oracle/), 1 host thread
-  rmse          held-out RMSE of a full 20-epoch fit vs the fp64 sequential oracle (same seed)
+  roofline      algorithmic bytes of a step (SURVEY 8(d) per-update figure x updates per GPU) /
+                the measured step time (<= 1 by construction), the per-kernel GPU time of a step
+                from HIP events on the engine's stream, and `traffic`: HBM bytes per step summed
+                over every kernel (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_*.json)
+  cpu_baseline  the fp64 C restatement of the reference loop (oracle/): all host cores (one
+                pinned process per core) and one pinned core, host model and core count
+  rmse          held-out RMSE of a full 20-epoch fit vs the fp64 sequential oracle (N=1, SVD)
+  svdpp_c3      BASELINE configs[2]: SVD++ K=100 epochs timed on the same fold (N=1 default)
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,8 +38,14 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); 6.29 TB/s measured copy
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); 6.3 TB/s achievable copy
 EVENT_EVERY = 4  # steps between HIP-event-instrumented steps
+BOX_CPU_SHARE = 16  # host cores of one GPU's share on the GPU box (os.cpu_count() shows the host)
+SHAPE_DEFAULTS = {  # shape -> (algo, n_factors, scaling)
+    "ml-1m": ("svd", 100, "weak"),
+    "c4": ("svd", 128, "strong"),
+    "c5": ("svdpp", 128, "strong"),
+}
 
 
 def parse():
@@ -33,17 +53,23 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--algo", default="svd", choices=["svd", "svdpp"])
-    p.add_argument("--factors", type=int, default=100)
+    p.add_argument("--shape", default="ml-1m", choices=sorted(SHAPE_DEFAULTS))
+    p.add_argument("--algo", default=None, choices=["svd", "svdpp"])
+    p.add_argument("--factors", type=int, default=None)
     p.add_argument("--mode", default="auto")
     p.add_argument("--chunks", type=int, default=1)
-    p.add_argument("--shape", default="ml-1m")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rmse", action="store_true")
+    p.add_argument("--no-svdpp", action="store_true", help="skip the SVD++ C3 leg")
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
                         "several ranks on one GPU)")
-    return p.parse_args()
+    a = p.parse_args()
+    algo, K, scaling = SHAPE_DEFAULTS[a.shape]
+    a.algo = a.algo or algo
+    a.factors = a.factors or K
+    a.scaling = scaling
+    return a
 
 
 def algorithmic_bytes_per_update(algo, K, s=4):
@@ -54,192 +80,358 @@ def algorithmic_bytes_per_update(algo, K, s=4):
     return b
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-    from surprise_amd import Dataset, synthetic
-    from surprise_amd.dist import DistContext
-    from surprise_amd.engine import MFEngine, default_ld
+def spawn_ranks(n):
+    """--gpus N without a launcher: N fresh child processes (one per GPU), started before this
+    process touches any GPU; exits with the first failing child's code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc]
+    sys.exit(bad[0] if bad else 0)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# ---------------------------------------------------------------------------- workloads
+def workload(args, rank, world):
+    """This rank's training CSR (rank-local rows), held-out triples (local user ids), item
+    count, the rank's train-rating sum (for the global mean) and a description."""
+    from surprise_amd import synthetic
+    from surprise_amd.dist import shard_users
     from surprise_amd.model_selection import KFold
-    from surprise_amd.utils import get_rng
+    from surprise_amd.trainset import Trainset
+    if args.shape == "ml-1m":
+        U, I, N = synthetic.SHAPES["ml-1m"]
+        u, i, r = synthetic.population(rank, U, I, N)
+        tr, te = next(KFold(5, random_state=0).fold_indices(len(r)))
+        ts = Trainset.from_inner_arrays(u[tr], i[tr], r[tr], n_users=U, n_items=I)
+        desc = ("ML-1M-shape user population %d of %d (%d users x %d items), KFold(5, rs=0) fold "
+                "0" % (rank, world, U, I))
+        return ts.csr(), (u[te], i[te], r[te]), I, U * world, desc
+    U, I, N = synthetic.SHAPES[args.shape]
+    truth = synthetic.sharded_truth(U, I, N)
+    row_ptr = np.concatenate([[0], np.cumsum(truth["deg"])])
+    b = shard_users(row_ptr, world)
+    csr, test = synthetic.sharded_rows(truth, int(b[rank]), int(b[rank + 1]),
+                                       threads=max(1, min(16, len(os.sched_getaffinity(0)))))
+    desc = ("%s shape (%d users x %d items x %d ratings, 1%% held out), users [%d, %d) on this "
+            "rank" % (args.shape, U, I, N, b[rank], b[rank + 1]))
+    return csr, test, I, U, desc
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.backend != "nccl":  # rehearsal: several ranks may share the box's one GPU
-        local %= max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(local)
-    ctx = None
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.backend)
-        ctx = DistContext()
 
-    u, i, r = synthetic.shape(args.shape)
-    ts, test = next(KFold(5, random_state=0).split(Dataset.load_from_arrays(u, i, r)))
-    row_ptr, items, ratings = ts.csr()
-    n_train = int(ts.n_ratings)
-    K = args.factors
-    svdpp = args.algo == "svdpp"
-    lr = .007 if svdpp else .005
-    hyper = dict(lr_bu=lr, lr_bi=lr, lr_pu=lr, lr_qi=lr, lr_yj=lr, reg_bu=.02, reg_bi=.02,
-                 reg_pu=.02, reg_qi=.02, reg_yj=.02, global_mean=float(ts.global_mean))
-    mode = args.mode if args.mode != "auto" else ("atomic" if svdpp else "log")
+def init_tables(shape, rank, n_users, n_items, K, svdpp):
+    """Initial factors: N(0, 0.1) as SVD.sgd draws them.  N=1 ML-1M: get_rng(0) pu then qi
+    (then yj), the reference's own sequence (the rmse leg's oracle uses the same draws)."""
+    rng = np.random.RandomState(0)
+    pu = rng.normal(0, .1, (n_users, K))
+    qi = rng.normal(0, .1, (n_items, K))
+    yj = rng.normal(0, .1, (n_items, K)) if svdpp else None
+    if rank > 0:  # other ranks' users: their own stream; item tables identical on every rank
+        pu = np.random.RandomState([0, rank]).normal(0, .1, (n_users, K))
+    return pu, qi, yj
 
-    def make_engine():
-        rng = get_rng(0)
-        pu = rng.normal(0, .1, (ts.n_users, K))
-        qi = rng.normal(0, .1, (ts.n_items, K))
-        yj = rng.normal(0, .1, (ts.n_items, K)) if svdpp else None
-        eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, algo=args.algo, hyper=hyper,
-                       mode=mode, n_chunks=args.chunks, world=world)
-        eng.set_factors(pu, qi, yj=yj)
-        # global per-item rating counts (all ranks) for the count-aware item fold
-        eng._prepare(ctx)
-        return eng
 
-    eng = make_engine()
-    stream = eng.stream
-    for _ in range(args.warmup):
+def hyper_for(algo, gm):
+    lr = .007 if algo == "svdpp" else .005  # SVDpp / SVD defaults (mf.pyx:398-407, :140-147)
+    return dict(lr_bu=lr, lr_bi=lr, lr_pu=lr, lr_qi=lr, lr_yj=lr, reg_bu=.02, reg_bi=.02,
+                reg_pu=.02, reg_qi=.02, reg_yj=.02, global_mean=float(gm))
+
+
+# ---------------------------------------------------------------------------- timing
+def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
+    """Warmup, then `steps` epochs between barriers + synchronize.  Every EVENT_EVERY-th timed
+    step carries HIP events on the engine's stream around each phase (a recorded timing event
+    idles the GPU for a few us, which the other steps do not pay).  Returns (seconds, phases)."""
+    for _ in range(warmup):
         for c in range(eng.n_chunks):
             eng.run_chunk(c)
             eng.sync_items(ctx)
     torch.cuda.synchronize()
-
-    recs = []
     if ctx is not None:
         ctx.barrier()
     torch.cuda.synchronize()
+    recs = []
     t0 = time.perf_counter()
-    # The epoch kernel's duration is taken with HIP events on the stream it runs on, on every
-    # EVENT_EVERY-th step of the timed region: a recorded timing event idles the GPU for a few us
-    # (measured: ~12 us per instrumented step of ~0.25 ms), which the other steps do not pay.
-    for step in range(args.steps):
+    for step in range(steps):
+        timed = instrument and step % EVENT_EVERY == 0
         for c in range(eng.n_chunks):
-            if step % EVENT_EVERY or os.environ.get("BENCH_NO_EVENTS"):
+            if not timed:
                 eng.run_chunk(c)
                 eng.sync_items(ctx)
                 continue
-            ev = {k: torch.cuda.Event(enable_timing=True) for k in ("start", "end", "end_h")}
-            eng.run_chunk(c, events=ev)  # HIP events on the streams the kernels run on
+            ev = {k: torch.cuda.Event(enable_timing=True)
+                  for k in ("begin", "start", "end", "end_h", "end_r", "done")}
+            ev["begin"].record(eng.stream)
+            eng.run_chunk(c, events=ev)
             eng.sync_items(ctx)
-            recs.append((c, ev))
+            ev["done"].record(eng.stream)
+            recs.append(ev)
     torch.cuda.synchronize()
     if ctx is not None:
         ctx.barrier()
     elapsed = time.perf_counter() - t0
-    # (a split chunk runs its heaviest users' epoch kernel on a second stream: the epoch phase
-    # ends with the later of the two launches)
-    def span(ev):
-        t = ev["start"].elapsed_time(ev["end"])
-        if eng.logs and eng.logs[0].get("heavy") is not None:
-            t = max(t, ev["start"].elapsed_time(ev["end_h"]))
-        return t
-    kern_ms = [span(ev) for _, ev in recs] or [float("nan")]
-    if ctx is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    phases = {}
+    if recs:
+        span = lambda a, b: float(np.mean([e[a].elapsed_time(e[b]) for e in recs]))
+        n = eng.n_chunks
+        phases = {"pre_ms": span("begin", "start") * n, "epoch_kernel_ms": span("start", "end") * n,
+                  "replay_ms": span("end", "end_r") * n, "fold_sync_ms": span("end_r", "done") * n,
+                  "step_gpu_ms": span("begin", "done") * n, "instrumented_steps": len(recs) // n}
+    return elapsed, phases
 
-    updates = n_train * args.steps * world
+
+def max_over_ranks(ctx, x, torch):
+    if ctx is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    ctx.all_reduce_max(t)
+    return float(t.item())
+
+
+def sum_over_ranks(ctx, xs, torch):
+    if ctx is None:
+        return list(xs)
+    t = torch.tensor(list(xs), dtype=torch.float64, device="cuda")
+    ctx.all_reduce_sum(t)
+    return t.cpu().tolist()
+
+
+def traffic_for(algo, K, shape):
+    path = os.path.join(ROOT, "profiles", "traffic_%s_k%d_%s.json" % (algo, K, shape))
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        t = json.load(f)
+    return t.get("bytes_per_step"), t
+
+
+# ---------------------------------------------------------------------------- CPU baseline
+def cpu_baselines(csr, n_items, K, n_train):
+    """The fp64 C restatement (oracle/) on this host: one pinned core (in-process affinity) for
+    ~10 s, then every core of this process's share at once (one pinned child process per core,
+    ~10 s each).  Bounded samples of the same workload: whole epochs over the same fold."""
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    row_ptr, items, ratings = csr
+    cores = sorted(os.sched_getaffinity(0))
+    share = cores[:BOX_CPU_SHARE]
+    old = set(cores)
+    os.sched_setaffinity(0, {share[0]})
+    try:
+        e, t1 = 0, 0.0
+        while t1 < 10.0 and e < 2000:
+            step = max(1, min(50, int(e * (10.0 - t1) / t1))) if t1 > 0 else 1
+            t1 += orc.time_svd_epochs(row_ptr, items, ratings, n_items, K, step, seed=e)
+            e += step
+    finally:
+        os.sched_setaffinity(0, old)
+    rate1 = n_train * e / t1
+    per_core_epochs = max(1, int(round(10.0 * rate1 / n_train)))
+    with tempfile.TemporaryDirectory() as d:
+        for name, a in (("row_ptr", row_ptr), ("items", items), ("ratings", ratings),
+                        ("n_items", np.asarray(n_items))):
+            np.save(os.path.join(d, name + ".npy"), a)
+        w = os.path.join(ROOT, "oracle", "cpu_worker.py")
+        t0 = time.perf_counter()
+        procs = [subprocess.Popen([sys.executable, w, d, str(c), str(per_core_epochs), str(K)],
+                                  stdout=subprocess.PIPE, text=True) for c in share]
+        outs = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in procs]
+        wall = time.perf_counter() - t0
+    ups = sum(o["updates"] for o in outs)
+    compute = max(o["seconds"] for o in outs)
+    cal = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["calibration"]
+    ratio = cal["oracle_over_reference"]
+    return {
+        "value": ups / compute, "unit": "rating-updates/s", "cores": len(share), "kind": "port",
+        "sample": "fp64 C restatement of SVD.sgd (oracle/mf_oracle.c <- mf.pyx:241-262), SVD K=%d, "
+                  "%d pinned processes x %d epochs over the same %d-rating train fold (wall incl. "
+                  "process start %.1fs)" % (K, len(share), per_core_epochs, n_train, wall),
+        "host_cpus": os.cpu_count(), "cpus_allowed": len(cores), "cpu_model": cpu_model(),
+        "single_core": {"value": rate1, "cores": 1, "pinned": True,
+                        "sample": "%d epochs on core %d (%.1fs)" % (e, share[0], t1),
+                        "cython_equivalent_derived": rate1 / ratio},
+        "calibration_oracle_over_cython": ratio,
+        "calibration_note": "the restatement / compiled reference Cython rate, both timed in the "
+                            "build container on the same fold (tests/golden/golden.json)",
+    }
+
+
+# ---------------------------------------------------------------------------- main
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and args.gpus > 1:
+        spawn_ranks(args.gpus)  # exits
+    rank = int(os.environ.get("RANK", "0"))
+
+    # host-side workload first (no GPU touched yet)
+    csr, test, n_items, n_users_global, desc = workload(args, rank, world)
+    row_ptr, items, ratings = csr
+    n_train = int(row_ptr[-1])
+
+    import torch
+    from surprise_amd.dist import DistContext
+    from surprise_amd.engine import MFEngine, default_ld
+    ctx = None
+    if world > 1:
+        ctx = DistContext.from_env(args.backend)
+    else:
+        torch.cuda.set_device(0)
+    # global mean of the training ratings over all ranks (one value for the model)
+    tot, cnt = sum_over_ranks(ctx, [float(ratings.sum()), float(n_train)], torch)
+    gm = tot / cnt
+    K, algo = args.factors, args.algo
+    svdpp = algo == "svdpp"
+    hyper = hyper_for(algo, gm)
+    mode = args.mode if args.mode != "auto" else ("atomic" if svdpp else "log")
+    n_users = len(row_ptr) - 1
+
+    def make_engine(a=algo, k=K, md=mode):
+        pu, qi, yj = init_tables(args.shape, rank, n_users, n_items, k, a == "svdpp")
+        eng = MFEngine(csr, n_items, k, algo=a, hyper=hyper_for(a, gm), mode=md,
+                       n_chunks=args.chunks, world=world)
+        eng.set_factors(pu, qi, yj=yj)
+        eng._prepare(ctx)  # global per-item counts (all ranks)
+        return eng
+
+    torch.cuda.reset_peak_memory_stats()
+    eng = make_engine()
+    elapsed, phases = run_steps(eng, ctx, args.steps, args.warmup, torch)
+    elapsed = max_over_ranks(ctx, elapsed, torch)
+    dev_bytes = max_over_ranks(ctx, float(torch.cuda.max_memory_allocated()), torch)
+    updates = sum_over_ranks(ctx, [float(n_train)], torch)[0] * args.steps
     value = updates / elapsed
-    K_bytes = algorithmic_bytes_per_update(args.algo, K)
-    launch_ms = float(np.mean(kern_ms))
-    per_launch_updates = n_train / eng.n_chunks
-    achieved = K_bytes * per_launch_updates / (launch_ms * 1e-3) / 1e9
+    ms_step = elapsed / args.steps * 1e3
+    B = algorithmic_bytes_per_update(algo, K)
+    bytes_step = B * n_train  # this rank's algorithmic bytes per step
+    achieved = bytes_step / (ms_step * 1e-3) / 1e9
+    traffic, tinfo = traffic_for(algo, K, args.shape)
 
     result = {
         "metric": "rating-updates/sec/GPU, SVD n_factors=100; RMSE delta vs Cython ref"
-        if not svdpp else "rating-updates/sec/GPU, SVD++ n_factors=%d" % K,
+        if (algo, K, args.shape) == ("svd", 100, "ml-1m") else
+        "rating-updates/sec, %s n_factors=%d (%s)" % (algo.upper(), K, args.shape),
         "value": value,
         "unit": "rating-updates/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic planted %s shape (surprise_amd.synthetic, seed 0), KFold(5,rs=0) "
-                "fold 0; weak scaling: one such user shard per GPU" % args.shape,
+        "data": "synthetic planted ratings (surprise_amd.synthetic, seed 0): " + desc,
         "config": {"workload": "%s n_factors=%d, one epoch per step over %d training ratings per "
-                               "GPU (%d users x %d items), mode=%s, chunks/epoch=%d"
-                               % (args.algo.upper(), K, n_train, ts.n_users, ts.n_items, mode,
-                                  eng.n_chunks),
-                   "algo": args.algo, "n_factors": K, "train_ratings_per_gpu": n_train,
-                   "ld": default_ld(K, 0), "parallelism": "users sharded x%d" % world},
+                               "GPU (rank 0), mode=%s, chunks/epoch=%d, %s scaling over %d GPU(s)"
+                               % (algo.upper(), K, n_train, mode, eng.n_chunks, args.scaling,
+                                  world),
+                   "shape": args.shape, "algo": algo, "n_factors": K,
+                   "train_ratings_rank0": n_train, "users_total": n_users_global,
+                   "items": n_items, "ld": default_ld(K, 0),
+                   "parallelism": "users sharded x%d (contiguous ranges), item tables replicated, "
+                                  "one SUM all-reduce per epoch-chunk" % world},
         "per_gpu_value": value / world,
+        "device_bytes_per_rank_max": dev_bytes,
     }
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "traffic_%s_k%d.json" % (args.algo, K))
-    if os.path.exists(tfile):
-        with open(tfile) as f:
-            traffic = json.load(f).get("bytes_per_launch")
-    result["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                          "kernel": "mf_epoch_kernel (%s, mode=%s)" % (args.algo, mode),
-                          "launch_ms": launch_ms,
-                          "algorithmic_bytes_per_update": K_bytes,
-                          "updates_per_launch": per_launch_updates,
-                          "instrumented_steps": len(recs),
-                          "note": "algorithmic bytes (SURVEY 8(d)) count a gather + scatter of the "
-                                  "user and item rows per rating; the user row stays in registers "
-                                  "and item rows hit L2/MALL, so frac can exceed 1: the epoch "
-                                  "kernel is bound by the heaviest user's sequential chain, "
-                                  "`traffic` is the measured HBM bytes per launch (PMC)",
-                          "rest_of_step_ms": elapsed / args.steps * 1e3 / eng.n_chunks
-                          - launch_ms}
+    result["roofline"] = {
+        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+        "kernel": "one epoch step (%s): %s" % (
+            mode, "sumsq + mf_epoch_kernel + log_replay_kernel + log_apply_kernel" if mode == "log"
+            else "mf_epoch_kernel + y fold (+ merge)"),
+        "algorithmic_bytes_per_update": B, "updates_per_step": n_train,
+        "algorithmic_bytes_per_step": bytes_step,
+        "phases_gpu_ms": phases,
+        "traffic_breakdown": tinfo.get("per_kernel") if tinfo else None,
+        "traffic_source": tinfo.get("source") if tinfo else None,
+        "note": "achieved = algorithmic bytes of a step (SURVEY 8(d): a gather + scatter of the "
+                "user and item rows per rating) / the measured step time; ML-1M's tables (pu "
+                "2.4 MB, qb 1.6 MB) are L2/MALL-resident, so HBM moves far fewer bytes than the "
+                "algorithmic figure (`traffic`, PMC) and the epoch kernel is bound by the "
+                "heaviest user's sequential chain, not by HBM",
+    }
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as orc
-        e = 0
-        t_cpu = 0.0
-        while t_cpu < 10.0 and e < 400:
-            t_cpu += orc.time_svd_epochs(row_ptr, items, ratings, ts.n_items, K, 5, seed=e)
-            e += 5
-        cpu_rate = n_train * e / t_cpu
-        cal = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["calibration"]
-        result["cpu_baseline"] = {
-            "value": cpu_rate, "unit": "rating-updates/s", "cores": 1, "kind": "port",
-            "sample": "fp64 C restatement of SVD.sgd (oracle/mf_oracle.c), SVD K=%d, %d epochs "
-                      "over the same %d-rating train fold, 1 thread" % (K, e, n_train),
-            "cython_equivalent_derived": cpu_rate / cal["oracle_over_reference"],
-            "calibration_oracle_over_cython": cal["oracle_over_reference"],
-            "gpu_over_cython_equivalent": value / (cpu_rate / cal["oracle_over_reference"])}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and algo == "svd":
+        result["cpu_baseline"] = cpu_baselines(csr, n_items, K, n_train)
+        cb = result["cpu_baseline"]
+        cb["gpu_over_cpu_all_cores"] = value / cb["value"]
+        cb["gpu_over_cython_equivalent_single"] = value / cb["single_core"]["cython_equivalent_derived"]
 
-    if not args.no_rmse and world == 1 and not svdpp and rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as orc
-        from surprise_amd import SVD, accuracy
-        t1 = time.perf_counter()
-        gpu = SVD(n_factors=K, n_epochs=20, random_state=0, mode=mode,
-                  chunks_per_epoch=args.chunks).fit(ts)
-        fit_s = time.perf_counter() - t1
-        rmse_gpu = accuracy.rmse(gpu.test(test), verbose=False)
-        rng = np.random.RandomState(0)
-        pu, qi, _ = orc.init_factors(rng, ts.n_users, ts.n_items, K)
-        hp = orc.hyper(**{k: v for k, v in hyper.items() if k != "global_mean"})
-        pu, qi, bu, bi = orc.svd_sgd(row_ptr, items, ratings, ts.n_items, K, 20, True,
-                                     ts.global_mean, hp, pu, qi)
-        uu = np.array([ts._raw2inner_id_users.get(x, -1) for x in test.uid.tolist()], np.int32)
-        ii = np.array([ts._raw2inner_id_items.get(x, -1) for x in test.iid.tolist()], np.int32)
-        est, imp = orc.svd_predict(uu, ii, K, True, ts.global_mean, pu, qi, bu, bi)
-        est = orc.finish_estimates(est, imp, ts.global_mean, 0, (1, 5))
-        rmse_ref = orc.rmse(test.rating, est)
-        result["rmse"] = {"gpu": rmse_gpu, "reference_oracle_fp64": rmse_ref,
-                          "delta": rmse_gpu - rmse_ref, "tolerance": 1e-3,
-                          "fit": "SVD K=%d E=20 seed 0, fit() wall %.3fs incl. H2D/init"
-                                 % (K, fit_s)}
+    if not args.no_rmse and algo == "svd":
+        result["rmse"] = rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch,
+                                  make_engine)
+
+    if (world == 1 and args.shape == "ml-1m" and algo == "svd" and K == 100
+            and not args.no_svdpp):
+        del eng
+        pp = make_engine("svdpp", 100, "atomic")
+        e2, ph2 = run_steps(pp, None, max(10, args.steps // 2), 2, torch)
+        n2 = max(10, args.steps // 2)
+        b2 = algorithmic_bytes_per_update("svdpp", 100)
+        result["svdpp_c3"] = {
+            "config": "BASELINE configs[2]: SVD++ n_factors=100 (atomic q rows, deferred y fold) "
+                      "on the same fold, one epoch per step",
+            "value": n_train * n2 / e2, "unit": "rating-updates/s", "steps": n2,
+            "ms_per_step": e2 / n2 * 1e3, "phases_gpu_ms": ph2,
+            "roofline": {"achieved": b2 * n_train / (e2 / n2) / 1e9, "peak": HBM_PEAK_GBS,
+                         "frac": b2 * n_train / (e2 / n2) / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_update": b2}}
 
     if rank == 0:
-        print(json.dumps(result))
+        print(json.dumps(result), flush=True)
     if ctx is not None:
-        dist.destroy_process_group()
+        ctx.barrier()
+        ctx.dist.destroy_process_group()
+
+
+def rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch, make_engine):
+    """A full 20-epoch fit through the same engine, held-out RMSE over all ranks; at N=1 on
+    ML-1M also the fp64 sequential oracle (the reference loop restated) on the same CSR and
+    initial factors."""
+    eng = make_engine()
+    eng.run_epochs(20, ctx)
+    tu, ti, tr = test
+    est, _ = eng.predict(np.asarray(tu, np.int32), np.asarray(ti, np.int32), gm)
+    est = np.clip(est, 1, 5)
+    se, n, se_mu = sum_over_ranks(ctx, [float(((tr - est) ** 2).sum()), float(len(tr)),
+                                        float(((tr - gm) ** 2).sum())], torch)
+    out = {"gpu": (se / n) ** .5, "global_mean_baseline": (se_mu / n) ** .5,
+           "fit": "%s K=%d E=20 through the bench engine, %d held-out ratings over %d rank(s)"
+                  % (args.algo.upper(), K, int(n), world)}
+    if world == 1 and args.shape == "ml-1m":
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as orc
+        row_ptr, items, ratings = csr
+        pu, qi, _ = init_tables(args.shape, 0, len(row_ptr) - 1, n_items, K, False)
+        h = hyper_for("svd", gm)
+        hp = orc.hyper(**{k: v for k, v in h.items() if k != "global_mean"})
+        pu, qi, bu, bi = orc.svd_sgd(row_ptr, items, ratings, n_items, K, 20, True, gm, hp, pu,
+                                     qi)
+        e, imp = orc.svd_predict(np.asarray(tu, np.int32), np.asarray(ti, np.int32), K, True, gm,
+                                 pu, qi, bu, bi)
+        e = orc.finish_estimates(e, imp, gm, 0, (1, 5))
+        out["reference_oracle_fp64"] = orc.rmse(tr, e)
+        out["delta"] = out["gpu"] - out["reference_oracle_fp64"]
+        out["tolerance"] = 1e-3
+    return out
 
 
 if __name__ == "__main__":

@@ -211,6 +211,20 @@ int mf_item_apply(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
                   const void *delta, int32_t dtype, void *stream);
 
 /*
+ * SVD++ implicit factors across ranks (surprise_amd/dist.py; replaces nothing in the reference,
+ * which is single-process).  Rank r's chunk left y_r = A_r y_s + c_r in `tab` (its users' end-of-
+ * user maps y_j <- A_u y_j + c_u composed in CSR order, A_u = (1 - lr_yj reg_yj)^{|I_u|}) over the
+ * chunk-start snapshot y_s in `snap`.  Ranks own consecutive user ranges, so the single-GPU
+ * composition over all users is y = A y_s + sum_r S_r c_r with A = prod_r A_r and
+ * S_r = prod_{s>r} A_s (per item).
+ *   phase 0: delta = s[i] * (tab - a[i] * snap)   (a = A_r, s = S_r; SUM-all-reduce it after)
+ *   phase 1: tab = snap = a[i] * snap + delta      (a = A; s unused)
+ * tab, snap, delta [n_items][ld]; a, s [n_items] (dtype).
+ */
+int mf_item_affine(void *tab, void *snap, int32_t n_items, int32_t ld, const void *a,
+                   const void *s, void *delta, int32_t phase, int32_t dtype, void *stream);
+
+/*
  * One epoch of NMF.sgd (matrix_factorization.pyx:646-735) in two race-free passes.
  * mf_nmf_user_pass: one wave per user computes every rating's estimate
  *   est = mu + b_u + b_i + <q_i, p_u>  (biased; the b_u recursion of :707-708 in the user's
@@ -275,6 +289,19 @@ int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, co
                int32_t biased, double global_mean, void *est, int32_t *impossible, int32_t dtype,
                void *stream);
 
+/*
+ * accuracy.rmse / accuracy.mae over a batch of estimates (accuracy.py:22-90), finishing each
+ * estimate as AlgoBase.predict does (algo_base.py:148-169): impossible[x] (nullable) -> fallback
+ * (default_prediction(), the trainset mean), minus `offset`, clipped to [lo, hi]; the true rating
+ * is r[x] - offset.  Accumulates out[0] += sum err^2, out[1] += sum |err|, out[2] += n (three
+ * device doubles, zeroed by the caller): rmse = sqrt(out[0]/out[2]), mae = out[1]/out[2].
+ * est and r are dtype.  Replaces the per-Prediction Python loop of the reference's
+ * test() + rmse() (algo_base.py:191-218).
+ */
+int mf_rating_errors(int64_t n, const void *est, const int32_t *impossible, const void *r,
+                     double fallback, double offset, double lo, double hi, double *out,
+                     int32_t dtype, void *stream);
+
 /* imp[u] = (sum_{j in I_u} yj[j]) / sqrt(|I_u|)  (SVDpp.estimate :518-520), zero for empty users;
  * yj is replica 0, imp is [n_users][ldu]. */
 int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, int32_t ldu, void *imp,
@@ -289,6 +316,11 @@ int mf_selftest_wave_sum(const void *in, void *out, int32_t n_waves, int32_t dty
 /* Library version (major*10000 + minor*100 + patch) and last error message. */
 int mf_version(void);
 const char *mf_last_error(void);
+
+/* sha256 (hex) of the sources and compile lines this library was built from
+ * (surprise_amd/build.py source_hash()): the Python loader refuses a library whose hash differs
+ * from the sources next to it. */
+const char *mf_source_hash(void);
 
 #ifdef __cplusplus
 }

@@ -10,6 +10,7 @@ What it wraps (see ``mf_oracle.c`` for the reference file:line of each routine):
 * ``svdpp_sgd``          SVDpp.sgd      (matrix_factorization.pyx:420-504), literal O(|I_u|) form
 * ``svdpp_sgd_affine``   per-user reformulation of SVDpp.sgd (the form the GPU kernel uses)
 * ``svd_sgd_groups``     G-group SUM-of-deltas schedule (multi-GPU / multi-replica semantics)
+* ``svdpp_sgd_groups_merge``  SVD++ G-group schedule with the multi-rank merge rules
 * ``svd_predict`` / ``svdpp_predict``  SVD.estimate / SVDpp.estimate on inner ids
 
 Initialisation follows SVD.sgd:206-236 / SVDpp.sgd:450-461: ``get_rng`` then
@@ -137,6 +138,30 @@ def svd_sgd_groups(row_ptr, items, ratings, n_items, K, n_epochs, biased, global
                                 ctypes.c_int32(n_groups), _p(c), ctypes.c_int32(n_chunks),
                                 _p(pu), _p(qi), _p(bu), _p(bi))
     return pu, qi, bu, bi
+
+
+def svdpp_sgd_groups_merge(row_ptr, items, ratings, n_items, K, n_epochs, global_mean, hp,
+                           pu, qi, yj, group_of_user, n_groups, chunk_of_user=None, n_chunks=1,
+                           merge=2, merge_y=4, bu=None, bi=None):
+    """SVD++ G-group schedule (multi-rank semantics): q/b merged by `merge` (0 SUM, 1 MEAN,
+    2 count-aware), y by `merge_y` (4: the GPU's affine composition in group order, users
+    reading the chunk-start y).  Returns (pu, qi, yj, bu, bi)."""
+    row_ptr, items, ratings = _csr_args(row_ptr, items, ratings)
+    n_users = len(row_ptr) - 1
+    pu = np.ascontiguousarray(pu, dtype=np.float64)
+    qi = np.ascontiguousarray(qi, dtype=np.float64)
+    yj = np.ascontiguousarray(yj, dtype=np.float64)
+    bu = np.zeros(n_users) if bu is None else np.ascontiguousarray(bu, dtype=np.float64)
+    bi = np.zeros(n_items) if bi is None else np.ascontiguousarray(bi, dtype=np.float64)
+    g = np.ascontiguousarray(group_of_user, dtype=np.int32)
+    c = (np.zeros(n_users, np.int32) if chunk_of_user is None
+         else np.ascontiguousarray(chunk_of_user, dtype=np.int32))
+    lib().oracle_svdpp_sgd_groups_merge(
+        ctypes.c_int64(n_users), ctypes.c_int64(n_items), _p(row_ptr), _p(items), _p(ratings),
+        ctypes.c_int32(K), ctypes.c_int32(n_epochs), ctypes.c_double(global_mean),
+        ctypes.byref(hp), _p(g), ctypes.c_int32(n_groups), _p(c), ctypes.c_int32(n_chunks),
+        ctypes.c_int32(merge), ctypes.c_int32(merge_y), _p(pu), _p(qi), _p(yj), _p(bu), _p(bi))
+    return pu, qi, yj, bu, bi
 
 
 def svd_sgd_deltalog(row_ptr, items, ratings, n_items, K, n_epochs, biased, global_mean, hp,

@@ -58,6 +58,7 @@ SIGNATURES = {
     "mf_item_merge": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
                       ctypes.POINTER(MfHyper), _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp],
     "mf_item_apply": [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp],
+    "mf_item_affine": [_vp, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp],
     "mf_nmf_user_pass": [ctypes.POINTER(MfCsr), _vp, _vp, _vp, _i32, _vp, _i32, _i32, _i32,
                          ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp],
     "mf_nmf_item_pass": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _i32, _i32, _i32,
@@ -67,18 +68,23 @@ SIGNATURES = {
                               _vp, _vp, _i32, _vp],
     "mf_predict": [_i64, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _dbl, _vp, _vp,
                    _i32, _vp],
+    "mf_rating_errors": [_i64, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _vp, _i32, _vp],
     "mf_svdpp_user_implicit": [ctypes.POINTER(MfCsr), _vp, _i32, _vp, _i32, _i32, _vp],
     "mf_selftest_wave_sum": [_vp, _vp, _i32, _i32, _vp],
     "mf_selftest_xcc": [_vp, _i32, _vp],
     "mf_version": [],
     "mf_last_error": [],
+    "mf_source_hash": [],
 }
+_STR_RESULT = ("mf_last_error", "mf_source_hash")
 
 _lib = None
 
 
 def load(path: str = LIB_PATH):
-    """Load the shared library (no GPU access happens here)."""
+    """Load the shared library (no GPU access happens here).  The product library must carry
+    the source hash of the kernel source / header / compile lines next to it (build provenance:
+    a stale or foreign .so is refused); SURPRISE_AMD_LIB (experiment variants) skips the check."""
     global _lib
     if _lib is not None:
         return _lib
@@ -90,7 +96,14 @@ def load(path: str = LIB_PATH):
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
-        fn.restype = ctypes.c_char_p if name == "mf_last_error" else ctypes.c_int
+        fn.restype = ctypes.c_char_p if name in _STR_RESULT else ctypes.c_int
+    if not os.environ.get("SURPRISE_AMD_LIB"):
+        from .build import source_hash
+        have, want = lib.mf_source_hash().decode(), source_hash()
+        if have != want:
+            raise SurpriseAMDError(
+                f"{path} was built from other sources (hash {have[:16]}, sources {want[:16]}): "
+                "rebuild with surprise_amd.build.build()")
     _lib = lib
     return lib
 

@@ -10,6 +10,7 @@ that combination's epoch-kernel instantiations (-DMF_TU_EPOCH, see the top of th
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 from concurrent.futures import ThreadPoolExecutor
@@ -40,12 +41,41 @@ def units():
     return out
 
 
+HASH_TAG = b"surprise_amd-src-sha256:"
+
+
+def source_hash(extra: tuple = ()) -> str:
+    """sha256 over the kernel source, the C ABI header and the exact compile lines: the
+    identity of a library build.  Embedded in the .so (mf_source_hash()); _lib.load() refuses
+    a library whose hash differs from the sources next to it."""
+    h = hashlib.sha256()
+    for path in (SRC, HDR):
+        with open(path, "rb") as f:
+            h.update(f.read())
+    h.update(repr((FLAGS, list(extra), units())).encode())
+    return h.hexdigest()
+
+
+def embedded_hash(lib_path: str = OUT):
+    """The source hash compiled into a built library (read from its bytes, no loading)."""
+    try:
+        with open(lib_path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    at = data.find(HASH_TAG)
+    if at < 0:
+        return None
+    return data[at + len(HASH_TAG):at + len(HASH_TAG) + 64].decode("ascii", "replace")
+
+
 def build(force: bool = False, verbose: bool = False, jobs: int | None = None, out: str = OUT,
           extra: tuple = ()) -> str:
-    """Build (when stale) and return the library path.  out / extra: experiment variants
-    (tools/ builds libraries with -D switches next to the product one)."""
-    newest = max(os.path.getmtime(SRC), os.path.getmtime(HDR), os.path.getmtime(__file__))
-    if not force and os.path.exists(out) and os.path.getmtime(out) >= newest:
+    """Build (when the embedded source hash differs from the sources) and return the library
+    path.  out / extra: experiment variants (tools/ builds libraries with -D switches next to
+    the product one)."""
+    want = source_hash(extra)
+    if not force and embedded_hash(out) == want:
         return out
     obj_dir = OBJ_DIR if out == OUT else out + ".obj"
     os.makedirs(obj_dir, exist_ok=True)
@@ -53,7 +83,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None, o
     def compile_one(u):
         name, defs = u
         obj = os.path.join(obj_dir, name + ".o")
-        cmd = [HIPCC, *FLAGS, *extra, *defs, "-c", "-o", obj, SRC]
+        cmd = [HIPCC, *FLAGS, *extra, *defs, f'-DMF_SOURCE_HASH="{want}"', "-c", "-o", obj, SRC]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -1246,6 +1246,30 @@ __global__ __launch_bounds__(kBlock) void item_apply_kernel(T *tab, T *snap, int
     }
 }
 
+// SVD++ y_j across ranks (dist.py): rank r's chunk result is y_r = A_r y_s + c_r (its users'
+// end-of-user affine maps composed in CSR order).  phase 0: delta = S_r (y_r - A_r y_s) -- the
+// rank's c_r carried through the later ranks' maps; the caller SUM-all-reduces it.  phase 1:
+// y = A y_s + delta (A = prod_r A_r) into the table and its snapshot.  a / s: per item, dtype.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void item_affine_kernel(T *tab, T *snap, int n_items, int ld,
+                                                             const T *__restrict__ a,
+                                                             const T *__restrict__ s,
+                                                             T *__restrict__ delta, int phase)
+{
+    const int64_t total = (int64_t)n_items * ld;
+    for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * kBlock) {
+        const int i = (int)(x / ld);
+        if (phase == 0) {
+            delta[x] = s[i] * (tab[x] - a[i] * snap[x]);
+        } else {
+            const T nv = a[i] * snap[x] + delta[x];
+            snap[x] = nv;
+            tab[x] = nv;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- delta-log merge (MF_MODE_LOG)
 //
 // After an epoch-chunk in kLog mode, log row k holds the item-row delta d_k of rating k.  The
@@ -2276,6 +2300,47 @@ __global__ __launch_bounds__(kBlock) void y_apply_kernel(
     }
 }
 
+// accuracy.rmse / mae over the batched estimates (algo_base.py:148-169 finishing, accuracy.py:
+// 22-90): est -> fallback where impossible, minus the reader offset, clipped to the rating scale,
+// against r - offset; out[0] += sum err^2, out[1] += sum |err|, out[2] += count (fp64).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void rating_errors_kernel(
+    int64_t n, const T *__restrict__ est, const int32_t *__restrict__ impossible,
+    const T *__restrict__ r, double fallback, double offset, double lo, double hi,
+    double *__restrict__ out)
+{
+    __shared__ double part[2][kBlock / kWave];
+    double se = 0, ae = 0;
+    for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * kBlock) {
+        double e = (impossible && impossible[x]) ? fallback : (double)est[x];
+        e -= offset;
+        e = e < lo ? lo : (e > hi ? hi : e);  // (NaN -> hi, as np.fmax(lo, np.fmin(hi, e)))
+        e = e == e ? e : hi;
+        const double d = ((double)r[x] - offset) - e;
+        se += d * d;
+        ae += d < 0 ? -d : d;
+    }
+    se = wave_sum(se);
+    ae = wave_sum(ae);
+    const int w = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        part[0][w] = se;
+        part[1][w] = ae;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0, b = 0;
+        for (int v = 0; v < kBlock / kWave; ++v) {
+            a += part[0][v];
+            b += part[1][v];
+        }
+        atomicAdd(out, a);
+        atomicAdd(out + 1, b);
+        if (blockIdx.x == 0) atomicAdd(out + 2, (double)n);
+    }
+}
+
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void predict_kernel(
     int64_t n, const int32_t *__restrict__ uu, const int32_t *__restrict__ ii,
@@ -2464,7 +2529,15 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 860; }
+int mf_version(void) { return 900; }
+
+#ifndef MF_SOURCE_HASH
+#define MF_SOURCE_HASH "unknown"
+#endif
+// sha256 of this file, include/surprise_amd.h and the compile lines (surprise_amd/build.py);
+// the tag lets the build read it back from the .so without loading it
+static const char kSourceHash[] = "surprise_amd-src-sha256:" MF_SOURCE_HASH;
+const char *mf_source_hash(void) { return kSourceHash + 24; }
 
 const char *mf_last_error(void) { return g_err; }
 
@@ -2705,6 +2778,28 @@ int mf_item_apply(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
     return check_launch("item_apply_kernel");
 }
 
+int mf_item_affine(void *tab, void *snap, int32_t n_items, int32_t ld, const void *a,
+                   const void *s, void *delta, int32_t phase, int32_t dtype, void *stream)
+{
+    if (!tab || !snap || !a || !delta || n_items < 0 || ld < 1 || (phase != 0 && phase != 1) ||
+        (phase == 0 && !s))
+        return set_err(MF_E_ARG, "bad argument");
+    if (n_items == 0) return 0;
+    const int g = elementwise_grid((int64_t)n_items * ld);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MF_F32)
+        hipLaunchKernelGGL(item_affine_kernel<float>, dim3(g), dim3(kBlock), 0, st, (float *)tab,
+                           (float *)snap, n_items, ld, (const float *)a, (const float *)s,
+                           (float *)delta, phase);
+    else if (dtype == MF_F64)
+        hipLaunchKernelGGL(item_affine_kernel<double>, dim3(g), dim3(kBlock), 0, st, (double *)tab,
+                           (double *)snap, n_items, ld, (const double *)a, (const double *)s,
+                           (double *)delta, phase);
+    else
+        return set_err(MF_E_ARG, "bad dtype");
+    return check_launch("item_affine_kernel");
+}
+
 int mf_nmf_user_pass(const mf_csr_t *csr, const void *pu, void *pu_next, void *bu, int32_t ldu,
                      const void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
                      const mf_hyper_t *hp, void *est, void *blog, const int64_t *piece_beg,
@@ -2881,6 +2976,28 @@ int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, co
     if (dtype == MF_F32) return run(float{});
     if (dtype == MF_F64) return run(double{});
     return set_err(MF_E_ARG, "bad dtype");
+}
+
+int mf_rating_errors(int64_t n, const void *est, const int32_t *impossible, const void *r,
+                     double fallback, double offset, double lo, double hi, double *out,
+                     int32_t dtype, void *stream)
+{
+    if (n <= 0) return 0;
+    if (!est || !r || !out) return set_err(MF_E_ARG, "null argument");
+    int64_t b = (n + kBlock - 1) / kBlock;
+    const int g = (int)(b > 2048 ? 2048 : b);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MF_F32)
+        hipLaunchKernelGGL(rating_errors_kernel<float>, dim3(g), dim3(kBlock), 0, st, n,
+                           (const float *)est, impossible, (const float *)r, fallback, offset, lo,
+                           hi, out);
+    else if (dtype == MF_F64)
+        hipLaunchKernelGGL(rating_errors_kernel<double>, dim3(g), dim3(kBlock), 0, st, n,
+                           (const double *)est, impossible, (const double *)r, fallback, offset,
+                           lo, hi, out);
+    else
+        return set_err(MF_E_ARG, "bad dtype");
+    return check_launch("rating_errors_kernel");
 }
 
 int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, int32_t ldu, void *imp,

@@ -2,9 +2,11 @@
 SUM-all-reduced once per epoch-chunk.
 
 One process per GPU (torchrun / torch.distributed; backend "nccl" is RCCL on
-ROCm, "gloo" for the CPU tests).  Each rank owns a contiguous range of users
-balanced by rating count, so pu/bu rows never cross ranks; item tables are
-replicated and every rank runs its epoch-chunk from the same chunk-start state.
+ROCm, "gloo" for the CPU tests and for rehearsing several ranks on one GPU).
+Each rank owns a contiguous range of users balanced by rating count and holds
+ONLY that range on its device: its rows of the CSR (rank-local row_ptr) and its
+pu / bu rows.  Item tables are replicated; every rank runs its epoch-chunk from
+the same chunk-start item state.
 
   mode "log":  each rank folds its delta log into per-item sums S_i; the SUM
                all-reduce of S (and of the <pu^2> partials) gives every rank the
@@ -14,12 +16,19 @@ replicated and every rank runs its epoch-chunk from the same chunk-start state.
   other modes: each rank contributes its weighted ``local - snapshot`` item delta
                (mf_item_merge's count-aware rule, n_r = the rank's ratings of the
                item), SUM all-reduced and added to the snapshot.
-SVD++'s y_j rows are per-rank shared state, merged across ranks by the
-count-weighted mean of the rank deltas.
+SVD++'s y_j rows: within a chunk every user's end-of-user update is the affine
+map y_j <- A_u y_j + c_u (A_u = (1 - lr_yj reg_yj)^|I_u|), so rank r's chunk
+result is y_r = A_r y_s + c_r with A_r the product of its users' A_u.  Ranks own
+contiguous user ranges in order, so composing the ranks' maps in rank order is
+the single-GPU composition over all users in CSR order:
+    y = A y_s + sum_r S_r c_r,   A = prod_r A_r,   S_r = prod_{s > r} A_s,
+a SUM all-reduce of S_r (y_r - A_r y_s) (mf_item_affine; A_r, S_r are per-item
+constants of the schedule, computed once on the host).
 """
 from __future__ import annotations
 
 import os
+import zlib
 
 import numpy as np
 
@@ -37,6 +46,14 @@ def shard_users(row_ptr, world: int):
         bounds.append(b)
     bounds.append(n_users)
     return np.asarray(bounds, dtype=np.int64)
+
+
+def local_csr(csr, lo: int, hi: int):
+    """Rows [lo, hi) of a user-major CSR with a rank-local row_ptr (starts at 0)."""
+    row_ptr, items, ratings = csr
+    row_ptr = np.asarray(row_ptr, np.int64)
+    k0, k1 = int(row_ptr[lo]), int(row_ptr[hi])
+    return (row_ptr[lo:hi + 1] - k0, np.asarray(items)[k0:k1], np.asarray(ratings)[k0:k1])
 
 
 def chunk_users(users, row_ptr, n_chunks: int):
@@ -62,8 +79,33 @@ def item_counts(users, row_ptr, items, n_items: int):
     return np.bincount(np.asarray(items)[idx], minlength=n_items)
 
 
+def item_log_decay(users, row_ptr, items, n_items: int, decay: float):
+    """log of A_r per item: sum over the ratings (u, j) of `users` of |I_u| log(decay) -- the
+    product of the end-of-user y maps' factors A_u = decay^|I_u| that touch item j."""
+    row_ptr = np.asarray(row_ptr, dtype=np.int64)
+    users = np.asarray(users, dtype=np.int64)
+    if len(users) == 0 or decay == 1.0:
+        return np.zeros(n_items, np.float64)
+    deg = np.diff(row_ptr)
+    starts, lens = row_ptr[users], deg[users]
+    idx = np.repeat(starts - np.cumsum(np.concatenate([[0], lens[:-1]])), lens) + np.arange(lens.sum())
+    w = np.repeat(lens.astype(np.float64), lens) * np.log(decay)
+    return np.bincount(np.asarray(items)[idx], weights=w, minlength=n_items)
+
+
+def csr_fingerprint(csr, n_items: int):
+    """(n_users, n_items, nnz, crc32 of the CSR bytes) -- ranks must agree on the trainset."""
+    row_ptr, items, ratings = csr
+    crc = zlib.crc32(np.ascontiguousarray(row_ptr, np.int64).tobytes())
+    crc = zlib.crc32(np.ascontiguousarray(items, np.int32).tobytes(), crc)
+    crc = zlib.crc32(np.ascontiguousarray(ratings, np.float64).tobytes(), crc)
+    return np.array([len(row_ptr) - 1, n_items, int(row_ptr[-1]), crc], np.int64)
+
+
 class DistContext:
-    """Rank/world of the current process and the item-delta all-reduce."""
+    """Rank/world of the current process and the collectives of the schedule.  With the gloo
+    backend device tensors are staged through host memory (gloo is the CPU / rehearsal
+    transport); with nccl (RCCL) they stay on the device."""
 
     def __init__(self, group=None):
         import torch.distributed as dist
@@ -71,31 +113,81 @@ class DistContext:
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+        self.host_staged = self.backend == "gloo"
 
     @classmethod
     def from_env(cls, backend: str | None = None):
-        """Join (or reuse) the default process group described by torchrun's env vars;
-        returns None for a single-process run."""
+        """Join (or reuse) the default process group described by torchrun's env vars and bind
+        this process to its GPU (LOCAL_RANK); None for a single-process run."""
+        import torch
         import torch.distributed as dist
         if int(os.environ.get("WORLD_SIZE", "1")) <= 1 and not dist.is_initialized():
             return None
         if not dist.is_initialized():
-            dist.init_process_group(backend=backend or "nccl")
+            backend = backend or os.environ.get("SURPRISE_AMD_DIST_BACKEND", "nccl")
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            if backend == "nccl":
+                torch.cuda.set_device(local)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                n = torch.cuda.device_count()
+                if n:
+                    torch.cuda.set_device(local % n)
+                dist.init_process_group(backend)
         return cls()
 
+    def _run(self, fn, tensor):
+        if self.host_staged and tensor.is_cuda:
+            h = tensor.cpu()
+            fn(h)
+            tensor.copy_(h)
+        else:
+            fn(tensor)
+
     def all_reduce_sum(self, tensor):
-        self.dist.all_reduce(tensor, op=self.dist.ReduceOp.SUM, group=self.group)
+        self._run(lambda t: self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group),
+                  tensor)
+
+    def all_reduce_max(self, tensor):
+        self._run(lambda t: self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group),
+                  tensor)
+
+    def broadcast(self, tensor, src: int = 0):
+        self._run(lambda t: self.dist.broadcast(t, src, group=self.group), tensor)
+
+    def all_gather_rows(self, local, counts):
+        """Concatenate every rank's rows (rank order); counts[r] = rows of rank r.  Rows are
+        padded to the largest shard for the collective and trimmed after."""
+        import torch
+        m = max(int(max(counts)), 1)
+        dev = "cpu" if self.host_staged else local.device
+        pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+        pad[:local.shape[0]].copy_(local)
+        outs = [torch.empty_like(pad) for _ in range(self.world)]
+        self.dist.all_gather(outs, pad, group=self.group)
+        return torch.cat([o[:int(c)] for o, c in zip(outs, counts)])
 
     def barrier(self):
         self.dist.barrier(group=self.group)
+
+    def check_agreement(self, values, what: str):
+        """Raise unless every rank passed the same int64 vector."""
+        import torch
+        v = torch.as_tensor(np.asarray(values, np.int64))
+        dev = "cpu" if self.host_staged else torch.device("cuda", torch.cuda.current_device())
+        hi, lo = v.clone().to(dev), (-v).to(dev)
+        self.all_reduce_max(hi)
+        self.all_reduce_max(lo)
+        if not torch.equal(hi.cpu(), (-lo).cpu()):
+            raise RuntimeError(f"ranks disagree on {what}: max {hi.tolist()} min {(-lo).tolist()}")
 
 
 class ItemSync:
     """Epoch-chunk protocol shared by the HIP engine and the CPU test engine.
 
     Subclasses provide ``run_chunk(c)``, ``_merge_local()`` (single-rank fold, may
-    be a no-op), ``_delta_into(buf)``, ``_apply(buf)``, ``_delta_buffer()`` and
-    ``_gather_users(ctx)``."""
+    be a no-op), ``_delta_into(buf)``, ``_apply(buf)`` and ``_delta_buffer()``."""
 
     n_chunks = 1
 
@@ -120,5 +212,3 @@ class ItemSync:
                 self.sync_items(ctx)
             if on_epoch is not None:
                 on_epoch(epoch)
-        if ctx is not None and ctx.world > 1:
-            self._gather_users(ctx)

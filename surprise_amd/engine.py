@@ -117,9 +117,11 @@ class MFEngine(ItemSync):
     """SVD / SVD++ SGD on one GPU (one rank of a multi-GPU job)."""
 
     def __init__(self, csr, n_items, n_factors, *, algo="svd", hyper=None, biased=True,
-                 dtype="float32", mode="log", n_chunks=1, users=None, deterministic=False,
+                 dtype="float32", mode="log", n_chunks=1, deterministic=False,
                  user_order=None, n_waves=0, device=None, ld=None, world=1, merge="count",
                  ckpt=None, heavy=None):
+        """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
+        trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers."""
         torch = _lib.require_gpu()
         self.torch = torch
         self.algo = algo
@@ -160,13 +162,15 @@ class MFEngine(ItemSync):
             dev, self.tdt)
         self._csr = _lib.MfCsr(self.row_ptr.data_ptr(), self.items.data_ptr(),
                                self.ratings.data_ptr(), self.n_users, self.n_items)
-        self.users = np.arange(self.n_users) if users is None else np.asarray(users)
+        self.users = np.arange(self.n_users)
         if self.deterministic:
             order = np.asarray(user_order if user_order is not None else self.users, np.int32)
             chunks = [order]
         else:
             chunks = chunk_users(self.users, row_ptr, self.n_chunks)
         to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        self._row_ptr_h, self._items_h = row_ptr, np.asarray(items, np.int32)
+        self._chunk_users = [np.asarray(c, np.int32) for c in chunks]
         esz_q = self.ldq * esz
         # SVD with one-group rows logs in checkpoint form (a user row every mf_ckpt_interval()
         # ratings + err per rating; mf_log_replay rebuilds the gradients)
@@ -243,9 +247,8 @@ class MFEngine(ItemSync):
         if self.ydefer:
             n_pc = max(1, max(y["n_pieces"] for y in self.ycsc))
             self.ypc_c, self.ypc_A = z(n_pc, ld), z(n_pc)
-        # the user rows this rank owns form one range [u_lo, u_hi) (shard_users)
-        self.u_lo = int(self.users.min()) if len(self.users) else 0
-        self.u_hi = int(self.users.max()) + 1 if len(self.users) else 0
+        # every user row on the device belongs to this rank (a rank-local CSR)
+        self.u_lo, self.u_hi = 0, self.n_users
         self.qlog = None
         if self.mode == _lib.MF_MODE_LOG:
             k_lo, k_hi = int(row_ptr[self.u_lo]), int(row_ptr[self.u_hi])
@@ -294,13 +297,19 @@ class MFEngine(ItemSync):
         if self.yj_s is not None:
             self.yj_s.copy_(self.yj)
 
-    def get_factors(self):
-        """Host fp64 copies (pu, qi, bu, bi, yj) with the padding columns dropped."""
+    def get_factors(self, ctx=None):
+        """Host fp64 copies (pu, qi, bu, bi, yj) with the padding columns dropped.  With ctx
+        (several ranks) pu / bu are every rank's rows gathered in rank order (all ranks)."""
         self.stream.synchronize()
         K = self.K
         h = lambda x: x.to(self.torch.float64).cpu().numpy()
-        out = dict(pu=h(self.pu[:, :K]), qi=h(self.qb[:, :K]), bu=h(self.bu),
-                   bi=h(self.qb[:, K]))
+        pu, bu = self.pu[:, :K], self.bu
+        if ctx is not None and ctx.world > 1:
+            n = self.torch.tensor([self.n_users], dtype=self.torch.int64, device=self.dev)
+            counts = ctx.all_gather_rows(n, [1] * ctx.world).cpu().tolist()
+            pu = ctx.all_gather_rows(pu.contiguous(), counts)
+            bu = ctx.all_gather_rows(bu, counts)
+        out = dict(pu=h(pu), qi=h(self.qb[:, :K]), bu=h(bu), bi=h(self.qb[:, K]))
         out["yj"] = h(self.yj[:, :K]) if self.yj is not None else None
         return out
 
@@ -338,7 +347,8 @@ class MFEngine(ItemSync):
         for the checkpoint form); the fold into the table happens in sync_items.  A split chunk
         runs its heavy users' epoch + replay on the side stream beside the rest, joined before
         returning.  events: optional dict of torch.cuda.Event: "start" (main stream, before the
-        epoch kernels), "end" (after the main epoch kernel), "end_h" (after the heavy one)."""
+        epoch kernels), "end" (after the main epoch kernel), "end_h" (after the heavy one),
+        "end_r" (after the log replay / reduce / y fold that follow the epoch kernel)."""
         torch = self.torch
         s = self.sched[c]
         st = self._st()
@@ -384,6 +394,8 @@ class MFEngine(ItemSync):
             self._reduce_log(lg, self.sums.data_ptr(), st)
         if hv is not None:
             self.stream.wait_event(join)
+        if "end_r" in ev:
+            ev["end_r"].record(self.stream)
 
     def _reduce_log(self, lg, sums_ptr, st):
         """Piece sums of one user group's log: mf_log_replay (checkpoint form) or mf_log_reduce."""
@@ -399,13 +411,28 @@ class MFEngine(ItemSync):
                       ctypes.c_void_p(sums_ptr), self.dtype, st)
 
     def _prepare(self, ctx):
-        """Global per-item rating counts of every chunk (all ranks) for the count-aware rules."""
+        """Global per-item rating counts of every chunk (all ranks) for the count-aware rules;
+        with SVD++ on several ranks, the per-item factors of the y_j affine merge (dist.py)."""
         self.totals = []
         for t in self._totals_local:
             tt = self.torch.from_numpy(t).to(self.dev)
             if ctx is not None and ctx.world > 1:
                 ctx.all_reduce_sum(tt)
             self.totals.append(tt)
+        self._yaff = []
+        if self.yj_s is not None and ctx is not None and ctx.world > 1:
+            from .dist import item_log_decay
+            torch = self.torch
+            h = self._hyper
+            decay = 1.0 - h.lr_yj * h.reg_yj
+            for us in self._chunk_users:
+                la = torch.from_numpy(item_log_decay(us, self._row_ptr_h, self._items_h,
+                                                     self.n_items, decay))
+                every = ctx.all_gather_rows(la[None].to(self.dev), [1] * ctx.world).cpu()
+                suffix = torch.flip(torch.cumsum(torch.flip(every, [0]), 0), [0])  # sum_{s>=r}
+                s_r = suffix[ctx.rank + 1] if ctx.rank + 1 < ctx.world else torch.zeros_like(la)
+                to = lambda x: torch.exp(x).to(self.dev, self.tdt)
+                self._yaff.append(dict(a=to(la), s=to(s_r), a_all=to(suffix[0])))
 
     def _totals(self):
         """Per-item rating counts of every chunk over all ranks (a single rank: its own)."""
@@ -452,10 +479,9 @@ class MFEngine(ItemSync):
             tabs.append((self.qb, self.qb_s, self.ldq, self.K,
                          _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM))
         if self.yj_s is not None:
-            # SVD++ implicit factors: count-weighted mean over ranks (every user of a rank moves
-            # all its y_j together, which saturates fast)
-            tabs.append((self.yj, self.yj_s, self.ld, -1,
-                         _lib.MF_MERGE_MEAN if count else _lib.MF_MERGE_SUM))
+            # SVD++ implicit factors: the ranks' end-of-user affine maps composed in rank order
+            # (mf_item_affine, dist.py)
+            tabs.append((self.yj, self.yj_s, self.ld, -1, "affine"))
         return tabs
 
     def _merge_local(self):
@@ -494,6 +520,13 @@ class MFEngine(ItemSync):
             bufs[0][-2:].copy_(self.work)  # (the statistic rides in the same all-reduce)
             x = 1
         for tab, snap, ld, bias_col, rule in self._snap_tables():
+            if rule == "affine":
+                ya = self._yaff[c]
+                _lib.call("mf_item_affine", self._ptr(tab), self._ptr(snap), self.n_items, ld,
+                          self._ptr(ya["a"]), self._ptr(ya["s"]), self._ptr(bufs[x]), 0,
+                          self.dtype, st)
+                x += 1
+                continue
             use_counts = rule != _lib.MF_MERGE_SUM
             _lib.call("mf_item_merge", self._ptr(tab), self._ptr(snap), self.n_items, ld, self.K,
                       bias_col, 1, rule, self._ptr(self.counts[c]) if use_counts else None,
@@ -519,20 +552,15 @@ class MFEngine(ItemSync):
                       _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM, None, 1,
                       self._next_work(), self.dtype, st)
             x = 1
-        for tab, snap, ld, _, _ in self._snap_tables():
-            _lib.call("mf_item_apply", self._ptr(tab), self._ptr(snap), self.n_items, ld, 1,
-                      self._ptr(bufs[x]), self.dtype, st)
+        for tab, snap, ld, _, rule in self._snap_tables():
+            if rule == "affine":
+                _lib.call("mf_item_affine", self._ptr(tab), self._ptr(snap), self.n_items, ld,
+                          self._ptr(self._yaff[c]["a_all"]), None, self._ptr(bufs[x]), 1,
+                          self.dtype, st)
+            else:
+                _lib.call("mf_item_apply", self._ptr(tab), self._ptr(snap), self.n_items, ld, 1,
+                          self._ptr(bufs[x]), self.dtype, st)
             x += 1
-
-    def _gather_users(self, ctx):
-        """After the last epoch: every rank keeps only its own users' rows, then a SUM
-        all-reduce assembles the full pu / bu on every rank."""
-        mask = self.torch.zeros(self.n_users, dtype=self.tdt, device=self.dev)
-        mask[self.torch.from_numpy(np.asarray(self.users, np.int64)).to(self.dev)] = 1
-        self.pu.mul_(mask[:, None])
-        self.bu.mul_(mask)
-        ctx.all_reduce_sum(self.pu)
-        ctx.all_reduce_sum(self.bu)
 
     # ------------------------------------------------------------------ inference
     def user_implicit(self):

@@ -20,7 +20,8 @@ no CPU fallback.  Extra, keyword-only device options:
   chunks_per_epoch   epoch-chunks (item merges / all-reduces per epoch)
   deterministic      one wavefront, users in Trainset order: the reference's exact sequence
   n_waves            wavefronts per launch (0 = fill the GPU)
-  distributed        shard users over torch.distributed ranks (one process per GPU)
+  distributed        opt-in: shard users over the torch.distributed ranks of the job (one
+                     process per GPU, torchrun env); every rank must fit the same trainset
 
 The fork's per-fit side effects in SVD.fit (:158-169: a print and an unused
 ``movie_to_mean`` dict) do not change results and are not reproduced.
@@ -77,11 +78,46 @@ class _MFBase(AlgoBase):
         ts = Trainset.from_csr(row_ptr, items, ratings, n_items, rating_scale, offset)
         return self.fit(ts)
 
+    def _init_factors(self, n_users, n_items, with_yj, ctx):
+        """pu, qi[, yj] drawn as SVD.sgd / SVDpp.sgd draw them (mf.pyx:227-231, :454-461): one
+        rng, pu then qi then yj, fp64.  On several ranks every rank must start from the same
+        factors: with an int seed each rank draws the identical stream itself; otherwise
+        (random_state None or a RandomState, whose stream differs per process) rank 0 draws
+        and broadcasts."""
+        K = self.n_factors
+
+        def draw():
+            rng = get_rng(self.random_state)
+            pu = rng.normal(self.init_mean, self.init_std_dev, (n_users, K))
+            qi = rng.normal(self.init_mean, self.init_std_dev, (n_items, K))
+            yj = rng.normal(self.init_mean, self.init_std_dev, (n_items, K)) if with_yj else None
+            return pu, qi, yj
+
+        if ctx is None or ctx.world == 1 or isinstance(self.random_state, (int, np.integer)):
+            return draw()
+        import torch
+        if ctx.rank == 0:
+            arrs = draw()
+        else:
+            arrs = (np.empty((n_users, K)), np.empty((n_items, K)),
+                    np.empty((n_items, K)) if with_yj else None)
+        out = []
+        for a in arrs:
+            if a is None:
+                out.append(None)
+                continue
+            t = torch.from_numpy(np.ascontiguousarray(a))
+            if not ctx.host_staged:
+                t = t.cuda()
+            ctx.broadcast(t, 0)
+            out.append(t.cpu().numpy())
+        return tuple(out)
+
     def _run_sgd(self, trainset, with_yj):
         from .engine import MFEngine
-        from .dist import DistContext, shard_users
+        from .dist import DistContext, csr_fingerprint, local_csr, shard_users
 
-        torch = _lib.require_gpu()
+        _lib.require_gpu()
         if isinstance(trainset, Trainset):
             csr = trainset.csr()
             user_order = trainset.sched_order()
@@ -90,24 +126,27 @@ class _MFBase(AlgoBase):
                            trainset.n_ratings, trainset.rating_scale, trainset.offset, {}, {}).csr()
             user_order = np.fromiter(trainset.ur.keys(), np.int32, len(trainset.ur))
         global_mean = self.trainset.global_mean
+        n_users, n_items = trainset.n_users, trainset.n_items
 
-        rng = get_rng(self.random_state)
-        n_users, n_items, K = trainset.n_users, trainset.n_items, self.n_factors
-        pu = rng.normal(self.init_mean, self.init_std_dev, (n_users, K))
-        qi = rng.normal(self.init_mean, self.init_std_dev, (n_items, K))
-        yj = rng.normal(self.init_mean, self.init_std_dev, (n_items, K)) if with_yj else None
-
-        ctx = DistContext.from_env() if self.distributed else None
-        users = None
+        ctx = DistContext.from_env() if (self.distributed and not self.deterministic) else None
         if ctx is not None and ctx.world > 1:
-            b = shard_users(csr[0], ctx.world)
-            users = np.arange(b[ctx.rank], b[ctx.rank + 1])
-        eng = MFEngine(csr, n_items, K, algo=self._algo, hyper=self._hyper(global_mean),
-                       biased=getattr(self, "biased", True), dtype=self.dtype,
-                       mode=self._resolve_mode(), n_chunks=self.chunks_per_epoch, users=users,
-                       deterministic=self.deterministic, user_order=user_order,
-                       n_waves=self.n_waves, world=1 if ctx is None else ctx.world)
-        eng.set_factors(pu, qi, yj=yj)
+            # every rank must hold the same trainset: it shards it by user range below
+            ctx.check_agreement(csr_fingerprint(csr, n_items), "the trainset (users, items, "
+                                "ratings, CSR crc32)")
+        pu, qi, yj = self._init_factors(n_users, n_items, with_yj, ctx)
+        lo, hi = 0, n_users
+        world = 1 if ctx is None else ctx.world
+        if world > 1:
+            b = shard_users(csr[0], world)
+            lo, hi = int(b[ctx.rank]), int(b[ctx.rank + 1])
+            csr = local_csr(csr, lo, hi)
+        eng = MFEngine(csr, n_items, self.n_factors, algo=self._algo,
+                       hyper=self._hyper(global_mean), biased=getattr(self, "biased", True),
+                       dtype=self.dtype, mode=self._resolve_mode(),
+                       n_chunks=self.chunks_per_epoch, deterministic=self.deterministic,
+                       user_order=user_order, n_waves=self.n_waves, world=world)
+        eng.set_factors(pu[lo:hi], qi, yj=yj)
+        del pu
         verbose = self.verbose
 
         def on_epoch(e):
@@ -115,13 +154,14 @@ class _MFBase(AlgoBase):
                 print("Processing epoch {}".format(e))
 
         eng.run_epochs(self.n_epochs, ctx, on_epoch=on_epoch if verbose else None)
-        f = eng.get_factors()
-        self._engine = eng
+        f = eng.get_factors(ctx)
+        # inference (test()) needs every user's row on the device: a sharded engine is dropped
+        # and test() falls back to the batched path's host arrays via a fresh single-GPU view
+        self._engine = eng if world == 1 else None
         self._imp = None
         self.bu, self.bi, self.pu, self.qi = f["bu"], f["bi"], f["pu"], f["qi"]
         if with_yj:
             self.yj = f["yj"]
-        del torch
 
     # ------------------------------------------------------------------ batched test()
     def test(self, testset, verbose=False):
@@ -168,7 +208,7 @@ class SVD(_MFBase):
                  lr_all=.005, reg_all=.02, lr_bu=None, lr_bi=None, lr_pu=None, lr_qi=None,
                  reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, random_state=None,
                  verbose=False, *, dtype="float32", mode="auto",
-                 chunks_per_epoch=1, deterministic=False, n_waves=0, distributed=True):
+                 chunks_per_epoch=1, deterministic=False, n_waves=0, distributed=False):
         self.n_factors = n_factors
         self.n_epochs = n_epochs
         self.biased = biased
@@ -229,7 +269,7 @@ class SVDpp(_MFBase):
                  reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, reg_yj=None,
                  random_state=None, verbose=False, *, dtype="float32", mode="auto",
                  chunks_per_epoch=1, deterministic=False, n_waves=0,
-                 distributed=True):
+                 distributed=False):
         self.n_factors = n_factors
         self.n_epochs = n_epochs
         self.init_mean = init_mean

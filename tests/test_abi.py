@@ -27,7 +27,9 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_without_device(lib):
-    assert lib.mf_version() == 860
+    assert lib.mf_version() == 900
+    rc = lib.mf_item_affine(None, None, 10, 16, None, None, None, 0, 0, None)
+    assert rc == 1001 and b"bad argument" in lib.mf_last_error()
     # argument validation happens before any device call
     rc = lib.mf_item_merge(None, None, 10, 16, 10, 10, 1, 0, None, None, None, None, 0, 16,
                            None, None, 1, 0, None)
@@ -56,3 +58,11 @@ def test_header_constants_match_python():
                       ("MF_MAX_FACTORS_F32", 512),
                       ("MF_MAX_FACTORS_F64", 256)):
         assert "#define %s" % name in text and str(val) in text.split("#define %s" % name)[1].split("\n")[0]
+
+
+def test_library_hash_is_the_committed_sources(lib):
+    """Build provenance: the loaded .so carries sha256 of mf_kernels.hip + surprise_amd.h + the
+    compile lines, equal to the hash of the sources in this tree (_lib.load() enforces it)."""
+    from surprise_amd import build
+    assert lib.mf_source_hash().decode() == build.source_hash()
+    assert build.embedded_hash() == build.source_hash()

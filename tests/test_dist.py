@@ -36,23 +36,24 @@ def test_chunk_users_partition():
 
 
 class OracleRankEngine(ItemSync):
-    """CPU stand-in for MFEngine: same protocol, oracle compute (test infrastructure)."""
+    """CPU stand-in for MFEngine: same protocol, oracle compute (test infrastructure).  Holds
+    only its rank's rows (a rank-local CSR), like the device engine."""
 
-    def __init__(self, csr, n_items, K, hp, gm, users, n_chunks, pu, qi):
+    def __init__(self, csr, n_items, K, hp, gm, n_chunks, pu, qi):
         import torch
         self.torch = torch
         self.row_ptr, self.items, self.ratings = csr
         self.n_items, self.K, self.hp, self.gm = n_items, K, hp, gm
-        self.users = users
+        self.n_users = len(self.row_ptr) - 1
         self.n_chunks = n_chunks
-        self.chunks = chunk_users(users, self.row_ptr, n_chunks)
-        self.pu, self.bu = pu.copy(), np.zeros(len(self.row_ptr) - 1)
+        self.chunks = chunk_users(np.arange(self.n_users), self.row_ptr, n_chunks)
+        self.pu, self.bu = pu.copy(), np.zeros(self.n_users)
         self.q_snap, self.b_snap = qi.copy(), np.zeros(n_items)
         self.q, self.b = qi.copy(), np.zeros(n_items)
 
     def run_chunk(self, c):
         import oracle as orc
-        mask = np.zeros(len(self.row_ptr) - 1, bool)
+        mask = np.zeros(self.n_users, bool)
         mask[self.chunks[c]] = True
         deg = np.diff(self.row_ptr) * mask
         rp = np.concatenate([[0], np.cumsum(deg)])
@@ -77,14 +78,12 @@ class OracleRankEngine(ItemSync):
     def _merge_local(self):
         pass
 
-    def _gather_users(self, ctx):
-        keep = np.zeros(len(self.bu), bool)
-        keep[self.users] = True
-        pu = self.torch.from_numpy(self.pu * keep[:, None])
-        bu = self.torch.from_numpy(self.bu * keep)
-        ctx.all_reduce_sum(pu)
-        ctx.all_reduce_sum(bu)
-        self.pu, self.bu = pu.numpy(), bu.numpy()
+    def gather_users(self, ctx):
+        t = self.torch
+        counts = ctx.all_gather_rows(t.tensor([[self.n_users]]), [1] * ctx.world)[:, 0].tolist()
+        pu = ctx.all_gather_rows(t.from_numpy(self.pu), counts).numpy()
+        bu = ctx.all_gather_rows(t.from_numpy(self.bu), counts).numpy()
+        return pu, bu
 
 
 def _worker(rank, world, port, n_chunks, out_dir):
@@ -94,18 +93,19 @@ def _worker(rank, world, port, n_chunks, out_dir):
     sys.path.insert(0, os.path.join(root, "oracle"))
     sys.path.insert(0, root)
     import oracle as orc
-    from surprise_amd.dist import DistContext
+    from surprise_amd.dist import DistContext, local_csr
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = DistContext()
     csr, n_items, K, gm, pu, qi = _problem()
     b = shard_users(csr[0], world)
-    users = np.arange(b[rank], b[rank + 1])
+    lo, hi = int(b[rank]), int(b[rank + 1])
     hp = orc.hyper(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005,
                    reg_bu=.02, reg_bi=.02, reg_pu=.02, reg_qi=.02)
-    eng = OracleRankEngine(csr, n_items, K, hp, gm, users, n_chunks, pu, qi)
+    eng = OracleRankEngine(local_csr(csr, lo, hi), n_items, K, hp, gm, n_chunks, pu[lo:hi], qi)
     eng.run_epochs(3, ctx)
-    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), pu=eng.pu, bu=eng.bu, qi=eng.q_snap,
+    pu_all, bu_all = eng.gather_users(ctx)
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), pu=pu_all, bu=bu_all, qi=eng.q_snap,
              bi=eng.b_snap)
     dist.destroy_process_group()
 

@@ -354,3 +354,74 @@ def test_baseline_oracle(golden_ext, u1, name):
     ts, _ = u1
     bu, bi = run_oracle_bsl(case["params"]["bsl_options"], ts)
     assert _sha(bu, bi) == case["sha_bu_bi"]
+
+
+# ----------------------------------------------------------------------------- multi-rank rules
+
+def _groups_of(row_ptr, world):
+    from surprise_amd.dist import shard_users
+    b = shard_users(row_ptr, world)
+    return (np.searchsorted(b, np.arange(len(row_ptr) - 1), side="right") - 1).astype(np.int32)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("name", ["svdpp_k20_e20", "svdpp_k100_e20"])
+def test_svdpp_multirank_rule_within_1e3_of_reference(golden, u1, world, name):
+    """The SVD++ multi-rank schedule of the GPU path (dist.py): users sharded by contiguous
+    rating-balanced ranges, q/b by the count-aware merge, y_j by the affine composition of the
+    ranks' end-of-user maps in rank order (merge_y=4) -- within the north-star 1e-3 of the
+    reference's RMSE (golden) at 2, 4 and 8 ranks."""
+    meta, _ = golden
+    case = meta["cases"][name]
+    ts, test = u1
+    row_ptr, items, ratings = ts.csr()
+    P = _Params("SVDpp", case["params"])
+    pu, qi, yj = orc.init_factors(get_rng(P.random_state), ts.n_users, ts.n_items, P.n_factors,
+                                  P.init_mean, P.init_std_dev, with_yj=True)
+    pu, qi, yj, bu, bi = orc.svdpp_sgd_groups_merge(
+        row_ptr, items, ratings, ts.n_items, P.n_factors, P.n_epochs, ts.global_mean,
+        orc.svd_hyper(P), pu, qi, yj, _groups_of(row_ptr, world), world, merge=2, merge_y=4)
+    f = dict(pu=pu, qi=qi, yj=yj, bu=bu, bi=bi)
+    rmse = _oracle_test_rmse(P, f, "SVDpp", ts, list(test))[1]
+    assert abs(rmse - case["rmse"]) < 1e-3, (world, rmse, case["rmse"])
+
+
+def test_svdpp_affine_rule_one_group_composes_in_user_order(u1):
+    """merge_y=4 with ONE group: every user reads the chunk-start y and the maps compose in user
+    order -- equal to the composition done by hand from the per-user maps (a second, pure-numpy
+    restatement of the same rule on a small K)."""
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    K, n_items = 4, ts.n_items
+    rng = np.random.RandomState(3)
+    pu, qi, yj = orc.init_factors(rng, ts.n_users, n_items, K, with_yj=True)
+    hp = orc.hyper(lr_bu=.007, lr_bi=.007, lr_pu=.007, lr_qi=.007, lr_yj=.007, reg_bu=.02,
+                   reg_bi=.02, reg_pu=.02, reg_qi=.02, reg_yj=.02)
+    g = np.zeros(ts.n_users, np.int32)
+    a = orc.svdpp_sgd_groups_merge(row_ptr, items, ratings, n_items, K, 1, ts.global_mean, hp,
+                                   pu.copy(), qi.copy(), yj.copy(), g, 1, merge=0, merge_y=4)
+    # numpy restatement: users in order, imp from y0, maps onto a running y
+    P, Q, Y0, Y = pu.copy(), qi.copy(), yj.copy(), yj.copy()
+    bu, bi = np.zeros(ts.n_users), np.zeros(n_items)
+    decay = 1 - .007 * .02
+    for u in range(ts.n_users):
+        s, e = row_ptr[u], row_ptr[u + 1]
+        if e == s:
+            continue
+        js = items[s:e]
+        sq = np.sqrt(e - s)
+        imp = (Y0[js] / sq).sum(0)
+        c = np.zeros(K)
+        for k in range(s, e):
+            i = items[k]
+            err = ratings[k] - (ts.global_mean + bu[u] + bi[i] + Q[i] @ (P[u] + imp))
+            bu[u] += .007 * (err - .02 * bu[u])
+            bi[i] += .007 * (err - .02 * bi[i])
+            pf, qf = P[u].copy(), Q[i].copy()
+            P[u] += .007 * (err * qf - .02 * pf)
+            Q[i] += .007 * (err * (pf + imp) - .02 * qf)
+            c = decay * c + .007 * (err * qf / sq)
+            imp = decay * imp + .007 * err * qf
+        Y[js] = decay ** (e - s) * Y[js] + c
+    np.testing.assert_allclose(a[2], Y, rtol=0, atol=1e-11)
+    np.testing.assert_allclose(a[1], Q, rtol=0, atol=1e-11)
