@@ -61,6 +61,13 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rmse", action="store_true")
     p.add_argument("--no-svdpp", action="store_true", help="skip the SVD++ C3 leg")
+    p.add_argument("--users", type=int, default=0,
+                   help="c4 / c5: train only the first N users of the shape (a user-prefix "
+                        "subsample that keeps every item; 0 = all)")
+    p.add_argument("--rmse-epochs", type=int, default=20)
+    p.add_argument("--oracle", action="store_true",
+                   help="c4 / c5 at N=1: also train the fp64 sequential oracle on the same CSR "
+                        "and initial factors in the rmse leg (single host thread)")
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -126,18 +133,36 @@ def workload(args, rank, world):
         return ts.csr(), (u[te], i[te], r[te]), I, U * world, desc
     U, I, N = synthetic.SHAPES[args.shape]
     truth = synthetic.sharded_truth(U, I, N)
-    row_ptr = np.concatenate([[0], np.cumsum(truth["deg"])])
+    n_users = min(args.users, U) if args.users else U
+    row_ptr = np.concatenate([[0], np.cumsum(truth["deg"][:n_users])])
     b = shard_users(row_ptr, world)
     csr, test = synthetic.sharded_rows(truth, int(b[rank]), int(b[rank + 1]),
                                        threads=max(1, min(16, len(os.sched_getaffinity(0)))))
-    desc = ("%s shape (%d users x %d items x %d ratings, 1%% held out), users [%d, %d) on this "
-            "rank" % (args.shape, U, I, N, b[rank], b[rank + 1]))
-    return csr, test, I, U, desc
+    desc = ("%s shape (%d users x %d items x %d ratings, 1%% held out)%s, users [%d, %d) on this "
+            "rank" % (args.shape, U, I, N, ", first %d users" % n_users if n_users < U else "",
+                      b[rank], b[rank + 1]))
+    workload.user_lo = int(b[rank])
+    return csr, test, I, n_users, desc
 
 
-def init_tables(shape, rank, n_users, n_items, K, svdpp):
-    """Initial factors: N(0, 0.1) as SVD.sgd draws them.  N=1 ML-1M: get_rng(0) pu then qi
-    (then yj), the reference's own sequence (the rmse leg's oracle uses the same draws)."""
+def init_tables(shape, rank, n_users, n_items, K, svdpp, user_lo=0):
+    """Initial factors: N(0, 0.1) as SVD.sgd draws them.  ML-1M: get_rng(0) pu then qi (then
+    yj), the reference's own sequence (the rmse leg's oracle uses the same draws); other
+    populations' users draw from their own stream.  c4 / c5: per user block (the generator's
+    blocks), so that a user's initial row does not depend on the number of ranks."""
+    if shape != "ml-1m":
+        from surprise_amd.synthetic import BLOCK_USERS
+        rng = np.random.RandomState([0, 6])
+        qi = rng.normal(0, .1, (n_items, K))
+        yj = rng.normal(0, .1, (n_items, K)) if svdpp else None
+        hi = user_lo + n_users
+        rows = []
+        for b in range(user_lo // BLOCK_USERS, -(-hi // BLOCK_USERS)):
+            b0 = b * BLOCK_USERS
+            blk = np.random.RandomState([0, 5, b]).normal(0, .1, (BLOCK_USERS, K))
+            rows.append(blk[max(user_lo - b0, 0):min(hi - b0, BLOCK_USERS)])
+        pu = np.concatenate(rows) if rows else np.zeros((0, K))
+        return pu, qi, yj
     rng = np.random.RandomState(0)
     pu = rng.normal(0, .1, (n_users, K))
     qi = rng.normal(0, .1, (n_items, K))
@@ -304,7 +329,8 @@ def main():
     n_users = len(row_ptr) - 1
 
     def make_engine(a=algo, k=K, md=mode):
-        pu, qi, yj = init_tables(args.shape, rank, n_users, n_items, k, a == "svdpp")
+        pu, qi, yj = init_tables(args.shape, rank, n_users, n_items, k, a == "svdpp",
+                                 getattr(workload, "user_lo", 0))
         eng = MFEngine(csr, n_items, k, algo=a, hyper=hyper_for(a, gm), mode=md,
                        n_chunks=args.chunks, world=world)
         eng.set_factors(pu, qi, yj=yj)
@@ -375,7 +401,7 @@ def main():
         cb["gpu_over_cpu_all_cores"] = value / cb["value"]
         cb["gpu_over_cython_equivalent_single"] = value / cb["single_core"]["cython_equivalent_derived"]
 
-    if not args.no_rmse and algo == "svd":
+    if not args.no_rmse:
         result["rmse"] = rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch,
                                   make_engine)
 
@@ -403,30 +429,42 @@ def main():
 
 
 def rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch, make_engine):
-    """A full 20-epoch fit through the same engine, held-out RMSE over all ranks; at N=1 on
-    ML-1M also the fp64 sequential oracle (the reference loop restated) on the same CSR and
-    initial factors."""
+    """A full fit (--rmse-epochs, 20 by default) through the same engine, held-out RMSE over all
+    ranks; at N=1 on ML-1M (or with --oracle) also the fp64 sequential oracle -- the reference
+    loop restated (SVD: mf.pyx:241-262; SVD++: its exact per-user form of :463-498) -- on the
+    same CSR and initial factors."""
+    E = args.rmse_epochs
     eng = make_engine()
-    eng.run_epochs(20, ctx)
+    eng.run_epochs(E, ctx)
     tu, ti, tr = test
-    est, _ = eng.predict(np.asarray(tu, np.int32), np.asarray(ti, np.int32), gm)
+    tu, ti = np.asarray(tu, np.int32), np.asarray(ti, np.int32)
+    svdpp = args.algo == "svdpp"
+    est, _ = eng.predict(tu, ti, gm, imp=eng.user_implicit() if svdpp else None)
     est = np.clip(est, 1, 5)
     se, n, se_mu = sum_over_ranks(ctx, [float(((tr - est) ** 2).sum()), float(len(tr)),
                                         float(((tr - gm) ** 2).sum())], torch)
     out = {"gpu": (se / n) ** .5, "global_mean_baseline": (se_mu / n) ** .5,
-           "fit": "%s K=%d E=20 through the bench engine, %d held-out ratings over %d rank(s)"
-                  % (args.algo.upper(), K, int(n), world)}
-    if world == 1 and args.shape == "ml-1m":
+           "fit": "%s K=%d E=%d (%s) through the bench engine, %d held-out ratings over %d "
+                  "rank(s)" % (args.algo.upper(), K, E, mode, int(n), world)}
+    del eng
+    if world == 1 and (args.shape == "ml-1m" or args.oracle):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as orc
         row_ptr, items, ratings = csr
-        pu, qi, _ = init_tables(args.shape, 0, len(row_ptr) - 1, n_items, K, False)
-        h = hyper_for("svd", gm)
+        pu, qi, yj = init_tables(args.shape, 0, len(row_ptr) - 1, n_items, K, svdpp)
+        h = hyper_for(args.algo, gm)
         hp = orc.hyper(**{k: v for k, v in h.items() if k != "global_mean"})
-        pu, qi, bu, bi = orc.svd_sgd(row_ptr, items, ratings, n_items, K, 20, True, gm, hp, pu,
-                                     qi)
-        e, imp = orc.svd_predict(np.asarray(tu, np.int32), np.asarray(ti, np.int32), K, True, gm,
-                                 pu, qi, bu, bi)
+        t0 = time.perf_counter()
+        if svdpp:
+            pu, qi, yj, bu, bi = orc.svdpp_sgd(row_ptr, items, ratings, n_items, K, E, gm, hp, pu,
+                                               qi, yj, affine=True)
+            e = orc.svdpp_predict(tu, ti, row_ptr, items, K, gm, pu, qi, yj, bu, bi)
+            imp = np.zeros(len(tu), bool)
+        else:
+            pu, qi, bu, bi = orc.svd_sgd(row_ptr, items, ratings, n_items, K, E, True, gm, hp,
+                                         pu, qi)
+            e, imp = orc.svd_predict(tu, ti, K, True, gm, pu, qi, bu, bi)
+        out["oracle_seconds"] = time.perf_counter() - t0
         e = orc.finish_estimates(e, imp, gm, 0, (1, 5))
         out["reference_oracle_fp64"] = orc.rmse(tr, e)
         out["delta"] = out["gpu"] - out["reference_oracle_fp64"]

@@ -26,6 +26,7 @@ from . import _lib
 from .dist import ItemSync, chunk_users, item_counts
 
 PIECE_ROWS = 64  # log rows summed by one wave of mf_log_reduce
+SVDPP_WAVES_PER_CU = int(os.environ.get("SURPRISE_AMD_SVDPP_WPC", "4"))
 
 
 def _pad64(n: int, dtype: int) -> int:
@@ -113,13 +114,101 @@ def ckpt_positions(row_ptr, perm, interval, pos_user=None):
     return (k - ((k - row_ptr[u]) % interval)).astype(np.int32)
 
 
-class MFEngine(ItemSync):
+class Predictor:
+    """Batched inference on device tables (pu, bu, qb = [q | b], yj): the estimate of
+    SVD / SVDpp / NMF for many (u, i) pairs in one launch (mf_predict) and accuracy.rmse / mae
+    as one device reduction (mf_rating_errors).  Needs: torch, dev, stream, dtype, tdt, pu, bu,
+    qb, ld, ldq, K, biased (+ yj and _csr for SVD++'s implicit term)."""
+
+    def _ptr(self, t):
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+    def user_implicit(self):
+        """imp[u] = sum_{j in I_u} yj[j] / sqrt|I_u| on device (SVDpp.estimate :518-520)."""
+        imp = self.torch.zeros(self.n_users, self.ld, dtype=self.tdt, device=self.dev)
+        _lib.call("mf_svdpp_user_implicit", ctypes.byref(self._csr), self._ptr(self.yj),
+                  self.ld, self._ptr(imp), self.K, self.dtype,
+                  ctypes.c_void_p(self.stream.cuda_stream))
+        return imp
+
+    def _predict_dev(self, u, i, global_mean, imp=None):
+        t = self.torch
+        n = len(u)
+        du = t.from_numpy(np.ascontiguousarray(u, np.int32)).to(self.dev)
+        di = t.from_numpy(np.ascontiguousarray(i, np.int32)).to(self.dev)
+        est = t.zeros(n, dtype=self.tdt, device=self.dev)
+        bad = t.zeros(n, dtype=t.int32, device=self.dev)
+        _lib.call("mf_predict", n, self._ptr(du), self._ptr(di), self._ptr(self.pu),
+                  self._ptr(self.bu), self.ld, self._ptr(self.qb), self.ldq,
+                  None if imp is None else self._ptr(imp), self.K, int(self.biased),
+                  float(global_mean), self._ptr(est), self._ptr(bad), self.dtype,
+                  ctypes.c_void_p(self.stream.cuda_stream))
+        return est, bad
+
+    def predict(self, u, i, global_mean, imp=None):
+        """Batched estimate on inner ids (-1 = unknown) -> (est fp64, impossible bool)."""
+        est, bad = self._predict_dev(u, i, global_mean, imp)
+        self.stream.synchronize()
+        return est.to(self.torch.float64).cpu().numpy(), bad.cpu().numpy().astype(bool)
+
+    def rating_errors(self, u, i, r, global_mean, imp=None, fallback=None, offset=0.0,
+                      rating_scale=(1, 5)):
+        """(rmse, mae, n) of the estimates against r (test() + accuracy.rmse / mae, finished as
+        AlgoBase.predict does) -- estimates and errors never leave the device."""
+        t = self.torch
+        est, bad = self._predict_dev(u, i, global_mean, imp)
+        dr = t.from_numpy(np.ascontiguousarray(r, np.float64)).to(self.dev, self.tdt)
+        out = t.zeros(3, dtype=t.float64, device=self.dev)
+        fb = float(global_mean if fallback is None else fallback)
+        _lib.call("mf_rating_errors", len(u), self._ptr(est), self._ptr(bad), self._ptr(dr), fb,
+                  float(offset), float(rating_scale[0]), float(rating_scale[1]), self._ptr(out),
+                  self.dtype, ctypes.c_void_p(self.stream.cuda_stream))
+        se, ae, n = out.cpu().tolist()
+        return (se / n) ** .5 if n else float("nan"), ae / n if n else float("nan"), int(n)
+
+
+class PredictTables(Predictor):
+    """Device copies of a fitted model's host arrays for batched inference (a model whose training
+    engine is gone: fitted on several ranks, or unpickled on a GPU host)."""
+
+    def __init__(self, pu, qi, bu, bi, *, yj=None, csr=None, biased=True, dtype="float32"):
+        torch = _lib.require_gpu()
+        self.torch = torch
+        self.dev = torch.device("cuda", torch.cuda.current_device())
+        self.stream = torch.cuda.current_stream(self.dev)
+        self.dtype = _lib.MF_F64 if str(dtype) in ("float64", "f64", "double") else _lib.MF_F32
+        self.tdt = torch.float64 if self.dtype == _lib.MF_F64 else torch.float32
+        pu, qi = np.asarray(pu, np.float64), np.asarray(qi, np.float64)
+        self.K = int(qi.shape[1])
+        self.ld = default_ld(self.K, self.dtype) if self.K else 16
+        self.ldq = default_ldq(self.K, self.dtype)
+        self.n_users, self.n_items = len(pu), len(qi)
+        self.biased = bool(biased)
+        z = lambda *shape: torch.zeros(*shape, dtype=self.tdt, device=self.dev)
+        put = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(self.dev, self.tdt)
+        self.pu, self.qb = z(self.n_users, self.ld), z(self.n_items, self.ldq)
+        self.pu[:, :self.K] = put(pu)
+        self.qb[:, :self.K] = put(qi)
+        self.qb[:, self.K] = put(bi)
+        self.bu = put(bu)
+        self.yj = None
+        if yj is not None:
+            self.yj = z(self.n_items, self.ld)
+            self.yj[:, :self.K] = put(yj)
+            row_ptr, items, _ = csr
+            self.row_ptr = torch.from_numpy(np.ascontiguousarray(row_ptr, np.int64)).to(self.dev)
+            self.items = torch.from_numpy(np.ascontiguousarray(items, np.int32)).to(self.dev)
+            self._csr = _lib.MfCsr(self.row_ptr.data_ptr(), self.items.data_ptr(), 0,
+                                   self.n_users, self.n_items)
+
+
+class MFEngine(ItemSync, Predictor):
     """SVD / SVD++ SGD on one GPU (one rank of a multi-GPU job)."""
 
     def __init__(self, csr, n_items, n_factors, *, algo="svd", hyper=None, biased=True,
                  dtype="float32", mode="log", n_chunks=1, deterministic=False,
                  user_order=None, n_waves=0, device=None, ld=None, world=1, merge="count",
-                 ckpt=None, heavy=None):
+                 ckpt=None, heavy=None, chunk_order=None):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers."""
         torch = _lib.require_gpu()
@@ -146,7 +235,17 @@ class MFEngine(ItemSync):
             mode, n_chunks, n_waves = "plain", 1, 1
         self.mode = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
         self.n_chunks = max(1, int(n_chunks))
+        if chunk_order is None:
+            chunk_order = os.environ.get("SURPRISE_AMD_CHUNK_ORDER", "deal")
         self.n_waves = int(n_waves)
+        if self.n_waves <= 0 and algo == "svdpp" and not self.deterministic:
+            # SVD++ with shared item rows: at most SVDPP_WAVES_PER_CU users in flight per CU.
+            # Users that start later then see the q rows (float atomics) of the users before
+            # them, as the reference's sequential order does; with every ML-1M user in flight at
+            # once the whole epoch reads the epoch-start q and the held-out RMSE drifts +3e-3 ..
+            # +5e-3 from the reference at E=20, vs -7e-5 at 4 per CU, same epoch time
+            props = torch.cuda.get_device_properties(torch.cuda.current_device())
+            self.n_waves = SVDPP_WAVES_PER_CU * props.multi_processor_count
         self.world = int(world)
         self.merge_rule = merge
         self.stream = torch.cuda.current_stream(self.dev)
@@ -167,7 +266,7 @@ class MFEngine(ItemSync):
             order = np.asarray(user_order if user_order is not None else self.users, np.int32)
             chunks = [order]
         else:
-            chunks = chunk_users(self.users, row_ptr, self.n_chunks)
+            chunks = chunk_users(self.users, row_ptr, self.n_chunks, chunk_order)
         to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
         self._row_ptr_h, self._items_h = row_ptr, np.asarray(items, np.int32)
         self._chunk_users = [np.asarray(c, np.int32) for c in chunks]
@@ -562,32 +661,6 @@ class MFEngine(ItemSync):
                           self._ptr(bufs[x]), self.dtype, st)
             x += 1
 
-    # ------------------------------------------------------------------ inference
-    def user_implicit(self):
-        """imp[u] = sum_{j in I_u} yj[j] / sqrt|I_u| on device (SVDpp.estimate :518-520)."""
-        imp = self.torch.zeros(self.n_users, self.ld, dtype=self.tdt, device=self.dev)
-        _lib.call("mf_svdpp_user_implicit", ctypes.byref(self._csr), self._ptr(self.yj),
-                  self.ld, self._ptr(imp), self.K, self.dtype,
-                  ctypes.c_void_p(self.stream.cuda_stream))
-        return imp
-
-    def predict(self, u, i, global_mean, imp=None):
-        """Batched estimate on inner ids (-1 = unknown) -> (est fp64, impossible bool)."""
-        t = self.torch
-        n = len(u)
-        du = t.from_numpy(np.ascontiguousarray(u, np.int32)).to(self.dev)
-        di = t.from_numpy(np.ascontiguousarray(i, np.int32)).to(self.dev)
-        est = t.zeros(n, dtype=self.tdt, device=self.dev)
-        bad = t.zeros(n, dtype=t.int32, device=self.dev)
-        _lib.call("mf_predict", n, self._ptr(du), self._ptr(di), self._ptr(self.pu),
-                  self._ptr(self.bu), self.ld, self._ptr(self.qb), self.ldq,
-                  None if imp is None else self._ptr(imp), self.K, int(self.biased),
-                  float(global_mean), self._ptr(est), self._ptr(bad), self.dtype,
-                  ctypes.c_void_p(self.stream.cuda_stream))
-        self.stream.synchronize()
-        return est.to(t.float64).cpu().numpy(), bad.cpu().numpy().astype(bool)
-
-
 def _has_duplicate_items(row_ptr, items) -> bool:
     """True if some user lists the same item twice (the kernels then forward rows in registers)."""
     row_ptr = np.asarray(row_ptr, np.int64)
@@ -598,7 +671,7 @@ def _has_duplicate_items(row_ptr, items) -> bool:
     return len(np.unique(key)) != len(key)
 
 
-class NMFEngine:
+class NMFEngine(Predictor):
     """NMF.sgd on one GPU (matrix_factorization.pyx:646-735): per epoch mf_nmf_user_pass then
     mf_nmf_item_pass, then the user-factor buffers swap.  Layout as MFEngine: pu / pu_next
     T[U, ldu], qb T[I, ldq] = [q_i | b_i | 0..], bu T[U]; per rating est T[nnz] (and the item-bias
@@ -696,21 +769,6 @@ class NMFEngine:
         h = lambda x: x.to(self.torch.float64).cpu().numpy()
         return dict(pu=h(self.pu[:, :K]), qi=h(self.qb[:, :K]), bu=h(self.bu),
                     bi=h(self.qb[:, K]))
-
-    def predict(self, u, i, global_mean):
-        """Batched estimate (the SVD formula, mf.pyx:737-759) -> (est fp64, impossible bool)."""
-        t = self.torch
-        n = len(u)
-        du = t.from_numpy(np.ascontiguousarray(u, np.int32)).to(self.dev)
-        di = t.from_numpy(np.ascontiguousarray(i, np.int32)).to(self.dev)
-        est = t.zeros(n, dtype=self.tdt, device=self.dev)
-        bad = t.zeros(n, dtype=t.int32, device=self.dev)
-        _lib.call("mf_predict", n, self._ptr(du), self._ptr(di), self._ptr(self.pu),
-                  self._ptr(self.bu), self.ld, self._ptr(self.qb), self.ldq, None, self.K,
-                  int(self.biased), float(global_mean), self._ptr(est), self._ptr(bad),
-                  self.dtype, ctypes.c_void_p(self.stream.cuda_stream))
-        self.stream.synchronize()
-        return est.to(t.float64).cpu().numpy(), bad.cpu().numpy().astype(bool)
 
 
 def baseline_als_device(csr, csc, n_items, global_mean, n_epochs, reg_u, reg_i,

@@ -164,39 +164,109 @@ class _MFBase(AlgoBase):
             self.yj = f["yj"]
 
     # ------------------------------------------------------------------ batched test()
+    def _device_model(self):
+        """The device tables inference runs on: the training engine, or (model fitted on several
+        ranks / unpickled on a GPU host) device copies of the fitted arrays.  None without a
+        GPU: then test() is the reference's per-prediction estimate()."""
+        if self._engine is not None:
+            return self._engine
+        if getattr(self, "pu", None) is None:
+            return None
+        try:
+            _lib.require_gpu()
+        except _lib.SurpriseAMDError:
+            return None
+        from .engine import PredictTables
+        ts = _as_trainset(self.trainset)
+        self._engine = PredictTables(self.pu, self.qi, self.bu, self.bi,
+                                     yj=getattr(self, "yj", None) if self._algo == "svdpp" else None,
+                                     csr=ts.csr() if self._algo == "svdpp" else None,
+                                     biased=getattr(self, "biased", True), dtype=self.dtype)
+        self._imp = None
+        return self._engine
+
+    def _columns(self, testset):
+        """(raw uids, raw iids, r_ui_trans) columns of a testset (list of triples or array)."""
+        if isinstance(testset, np.ndarray):
+            testset = testset.tolist()
+        rows = testset if isinstance(testset, list) else list(testset)
+        if not rows:
+            return [], [], np.zeros(0)
+        ru, ri, r = zip(*rows)
+        return list(ru), list(ri), np.asarray(r, np.float64)
+
+    def _inner_columns(self, ruids, riids):
+        """Vectorised raw -> inner id mapping (-1 = unknown, the 'UKN__' case of
+        algo_base.py:137-144)."""
+        ts = _as_trainset(self.trainset)
+        return (_map_ids(ruids, ts._raw2inner_id_users), _map_ids(riids, ts._raw2inner_id_items))
+
     def test(self, testset, verbose=False):
-        """AlgoBase.test (algo_base.py:191-218) with the estimates computed in one
-        batched HIP launch when the model is on the device; after unpickling (no
-        device state) it falls back to per-prediction estimate(), the reference's
-        own numpy path."""
-        if self._engine is None or verbose:
+        """AlgoBase.test (algo_base.py:191-218): the ids are mapped with one vectorised lookup
+        and all estimates come from one batched HIP launch; the returned Predictions are the
+        reference's (same est, offset, clip, was_impossible details).  Without a GPU (an
+        unpickled model on a CPU host) it is the reference's per-prediction estimate()."""
+        eng = None if verbose else self._device_model()
+        if eng is None:
             return AlgoBase.test(self, testset, verbose)
-        iterate_on = testset.tolist() if isinstance(testset, np.ndarray) else testset
-        rows = list(iterate_on)
-        ts = self.trainset
-        u = np.empty(len(rows), np.int32)
-        i = np.empty(len(rows), np.int32)
-        for x, (ruid, riid, _) in enumerate(rows):
-            try:
-                u[x] = ts.to_inner_uid(ruid)
-            except ValueError:
-                u[x] = -1
-            try:
-                i[x] = ts.to_inner_iid(riid)
-            except ValueError:
-                i[x] = -1
+        ruids, riids, r = self._columns(testset)
+        if not len(r):
+            return []
+        u, i = self._inner_columns(ruids, riids)
         est, impossible = self._predict_inner(u, i)
+        ts = self.trainset
         est = np.where(impossible, self.default_prediction(), est) - ts.offset
         lo, hi = ts.rating_scale
         est = np.fmax(lo, np.fmin(hi, est))  # algo_base.py:166-169 (NaN -> upper bound)
-        out = []
         reason = "User and item are unkown."
-        for x, (ruid, riid, r) in enumerate(rows):
-            d = {"was_impossible": bool(impossible[x])}
-            if impossible[x]:
-                d["reason"] = reason
-            out.append(Prediction(ruid, riid, r - ts.offset, float(est[x]), d))
-        return out
+        ok, bad = {"was_impossible": False}, {"was_impossible": True, "reason": reason}
+        return [Prediction(a, b, c, e, dict(bad) if x else dict(ok))
+                for a, b, c, e, x in zip(ruids, riids, (r - ts.offset).tolist(), est.tolist(),
+                                         impossible.tolist())]
+
+    def test_metrics(self, testset):
+        """(rmse, mae) of the model on a testset -- accuracy.rmse(algo.test(testset)) and
+        accuracy.mae(...) without building Prediction objects: ids mapped in one vectorised
+        lookup, estimates and the error reduction on the device (mf_predict +
+        mf_rating_errors).  No reference counterpart; equal to the reference pipeline's values
+        (tests/test_gpu_parity.py)."""
+        eng = self._device_model()
+        if eng is None:
+            from . import accuracy
+            preds = AlgoBase.test(self, testset)
+            return accuracy.rmse(preds, verbose=False), accuracy.mae(preds, verbose=False)
+        ruids, riids, r = self._columns(testset)
+        u, i = self._inner_columns(ruids, riids)
+        ts = self.trainset
+        gm, imp = self._predict_args()
+        rmse, mae, _ = eng.rating_errors(u, i, r, gm, imp=imp, fallback=self.default_prediction(),
+                                         offset=ts.offset, rating_scale=ts.rating_scale)
+        return rmse, mae
+
+    def _predict_args(self):
+        return (self.trainset.global_mean if getattr(self, "biased", True) else 0.0), None
+
+    def _predict_inner(self, u, i):
+        gm, imp = self._predict_args()
+        return self._device_model().predict(u, i, gm, imp=imp)
+
+
+def _map_ids(raw, mapping):
+    """raw ids -> inner ids through a Trainset's raw2inner map, vectorised (-1 if absent)."""
+    from .trainset import _IdentityIds
+    if isinstance(mapping, _IdentityIds):
+        a = np.asarray(raw)
+        if a.dtype.kind in "iu":
+            out = a.astype(np.int64)
+            return np.where((out >= 0) & (out < mapping.n), out, -1).astype(np.int32)
+        return np.array([mapping[x] if x in mapping else -1 for x in raw], np.int32)
+    import pandas as pd
+    m = pd.Series(mapping, dtype="int64") if len(mapping) else pd.Series([], dtype="int64")
+    idx = m.index.get_indexer(pd.Index(list(raw)))
+    out = np.full(len(idx), -1, np.int32)
+    hit = idx >= 0
+    out[hit] = m.to_numpy()[idx[hit]]
+    return out
 
 
 class SVD(_MFBase):
@@ -255,10 +325,6 @@ class SVD(_MFBase):
                 raise PredictionImpossible("User and item are unkown.")
         return est
 
-    def _predict_inner(self, u, i):
-        return self._engine.predict(u, i, self.trainset.global_mean if self.biased else 0.0)
-
-
 class SVDpp(_MFBase):
     """SVD++ trained on the GPU in the exact per-user affine form (mf.pyx:302-522)."""
 
@@ -311,10 +377,10 @@ class SVDpp(_MFBase):
             est += np.dot(self.qi[i], self.pu[u] + u_impl_feedback)
         return est
 
-    def _predict_inner(self, u, i):
+    def _predict_args(self):
         if self._imp is None:
-            self._imp = self._engine.user_implicit()
-        return self._engine.predict(u, i, self.trainset.global_mean, imp=self._imp)
+            self._imp = self._device_model().user_implicit()
+        return self.trainset.global_mean, self._imp
 
 
 def _as_trainset(trainset):
@@ -391,5 +457,4 @@ class NMF(_MFBase):
         """mf.pyx:737-759 (host numpy fp64, per call)."""
         return SVD.estimate(self, u, i)
 
-    def _predict_inner(self, u, i):
-        return self._engine.predict(u, i, self.trainset.global_mean if self.biased else 0.0)
+

@@ -247,7 +247,8 @@ def test_pickle_round_trip(torch, u1, tmp_path):
     preds2, algo2 = dump.load(f)
     assert algo2._engine is None
     assert preds == preds2
-    preds3 = algo2.test(test)  # reference numpy estimate path
+    preds3 = algo2.test(test)  # device tables rebuilt from the unpickled arrays
+    assert algo2._engine is not None
     np.testing.assert_allclose([p.est for p in preds3], [p.est for p in preds], atol=1e-5)
     s = pickle.dumps(SVD(n_factors=3))  # unfitted: __init__ touches no GPU state
     assert pickle.loads(s).n_factors == 3
@@ -289,11 +290,12 @@ def test_c2_ml1m_svd_k100_e20_rmse_within_1e3(torch, ml1m, mode):
 
 @pytest.mark.slow
 def test_c3_ml1m_svdpp_k100_rmse_within_1e3(torch, ml1m):
-    """BASELINE configs[2]: SVD++ n_factors=100 on the ML-1M shape (5 epochs here: the
-    literal-form oracle is O(|I_u|^2); the affine-form oracle is the fp64 reference)."""
+    """BASELINE configs[2]: SVD++ n_factors=100 on the ML-1M shape at the reference's default 20
+    epochs (mf.pyx:389-411); the oracle is the exact per-user affine form of SVDpp.sgd in fp64
+    (pinned bit-for-bit to the literal form on u1, tests/test_oracle_golden.py)."""
     from surprise_amd import SVDpp
     ts, test = ml1m
-    params = dict(n_factors=100, n_epochs=5, random_state=0)
+    params = dict(n_factors=100, n_epochs=20, random_state=0)
     ref = _oracle_rmse("SVDpp", params, ts, test, affine=True)
     got = _rmse(SVDpp(**params).fit(ts).test(test))
     assert abs(got - ref) < RMSE_TOL, (got, ref)
@@ -438,3 +440,25 @@ def test_svdpp_y_fold_equals_sequential_composition(torch, K):
     got = y.cpu().numpy()
     np.testing.assert_allclose(got[:, :K], want[:, :K], rtol=0, atol=1e-12)
     np.testing.assert_array_equal(got[:, K:], y0[:, K:])  # padding columns untouched
+
+
+def test_test_metrics_equal_reference_pipeline(torch, u1):
+    """test_metrics(): ids mapped vectorised, estimates + error reduction on the device (no
+    Prediction objects) -- equal to accuracy.rmse / mae over the reference-style per-call
+    predictions (AlgoBase.test -> estimate), unknown ids included."""
+    from surprise_amd import NMF, SVD, SVDpp, accuracy
+    from surprise_amd.algo_base import AlgoBase
+    ts, test = u1
+    test = list(test) + [("no-such-user", "1", 4.0), ("1", "no-such-item", 2.0)]
+    for algo in (SVD(n_factors=30, n_epochs=3, random_state=0, dtype="float64"),
+                 SVD(n_factors=30, n_epochs=3, biased=False, random_state=0, dtype="float64"),
+                 SVDpp(n_factors=12, n_epochs=2, random_state=0, dtype="float64"),
+                 NMF(n_factors=8, n_epochs=3, random_state=0, dtype="float64")):
+        algo.fit(ts)
+        slow = AlgoBase.test(algo, test)
+        rmse, mae = algo.test_metrics(test)
+        assert abs(rmse - accuracy.rmse(slow, verbose=False)) < 1e-12
+        assert abs(mae - accuracy.mae(slow, verbose=False)) < 1e-12
+        fast = algo.test(test)
+        assert [p.details for p in fast] == [p.details for p in slow]
+        np.testing.assert_allclose([p.est for p in fast], [p.est for p in slow], atol=1e-12)

@@ -25,27 +25,30 @@ rng = np.random.RandomState(0)
 eng.set_factors(rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K)),
                 yj=rng.normal(0, .1, (ts.n_items, K)) if algo == "svdpp" else None)
 full = eng.sched[0].clone()
+W0 = eng.n_waves  # the engine's default wave count (SVD++: capped per CU)
 deg = np.diff(rp)
 order = full.cpu().numpy()
 
 
-def t_sched(s, n_waves=0, reps=10):
+def t_sched(s, n_waves=None, reps=10):
     eng.sched[0] = torch.from_numpy(np.ascontiguousarray(s, np.int32)).cuda()
-    eng.n_waves = n_waves
+    eng.n_waves = W0 if n_waves is None else n_waves
     ts_ = []
     for _ in range(reps + 2):
         ev = {k: torch.cuda.Event(enable_timing=True) for k in ("start", "end")}
         eng.run_chunk(0, events=ev)
+        eng.sync_items(None)
         torch.cuda.synchronize()
         ts_.append(ev["start"].elapsed_time(ev["end"]))
     return float(np.median(ts_[2:])) * 1e3
 
 
 print("algo", algo, "mode", mode, "K", K, "max deg", deg.max(), "ratings", deg.sum())
-cases = [("full", order, 0), ("top1", order[:1], 0), ("top16", order[:16], 0),
-                    ("top256", order[:256], 0), ("top1024", order[:1024], 0),
-                    ("drop-top64", order[64:], 0), ("drop-top256", order[256:], 0),
-                    ("full-2048waves", order, 2048), ("full-8192waves", order, 8192)]
+cases = [("full", order, None), ("top1", order[:1], None), ("top16", order[:16], None),
+         ("top256", order[:256], None), ("top1024", order[:1024], None),
+         ("drop-top64", order[64:], None), ("drop-top256", order[256:], None),
+         ("drop-top1024", order[1024:], None),
+         ("full-2048waves", order, 2048), ("full-8192waves", order, 8192)]
 if len(sys.argv) > 3 and sys.argv[3] == "waves":
     cases = [("full-%dwaves" % w, order, w) for w in (2048, 4096, 6040, 8192, 12288, 16384)]
 if len(sys.argv) > 3 and sys.argv[3] == "fast":

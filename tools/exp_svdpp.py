@@ -1,5 +1,6 @@
-"""Experiment: SVD++ item-side schedules with the deferred y fold -- held-out RMSE delta vs the
-fp64 affine-form oracle (BASELINE configs[2] shape, K=100, 5 epochs) and the epoch time."""
+"""Experiment: SVD++ item-side schedules on BASELINE configs[2]'s shape (K=100, E=20) -- held-out
+RMSE delta vs the fp64 affine-form oracle and the fit time.
+    python tools/exp_svdpp.py [epochs] [mode:chunks:ydefer:order,...]"""
 import os
 import sys
 import time
@@ -12,23 +13,40 @@ from surprise_amd import SVDpp, accuracy  # noqa: E402
 
 
 def main():
+    E = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     ts, test = synth("ml-1m")
-    params = dict(n_factors=100, n_epochs=5, random_state=0)
+    params = dict(n_factors=100, n_epochs=E, random_state=0)
     ref = oracle_rmse("SVDpp", params, ts, test, affine=True)
-    print("oracle rmse %.5f" % ref, flush=True)
-    for mode, chunks, ydefer in (("atomic", 1, "1"), ("atomic", 1, "0"), ("log", 1, "1"),
-                                 ("log", 4, "1"), ("log", 1, "0"), ("log", 4, "0")):
+    print("oracle rmse %.5f (E=%d)" % (ref, E), flush=True)
+    variants = [v.split(":") for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else
+                ["atomic:1:1:deal", "atomic:2:1:band", "atomic:4:1:band", "atomic:2:0:band",
+                 "atomic:4:0:band", "log:2:0:band", "log:4:0:band", "log:8:0:band"])]
+    for v in variants:
+        mode, chunks, ydefer, order = v[:4]
+        waves = int(v[4]) if len(v) > 4 else 0
+        chunks = int(chunks)
         os.environ["SURPRISE_AMD_YDEFER"] = ydefer
-        algo = SVDpp(**params, mode=mode, chunks_per_epoch=chunks)
+        os.environ["SURPRISE_AMD_CHUNK_ORDER"] = order
+        algo = SVDpp(**params, mode=mode, chunks_per_epoch=chunks, n_waves=waves)
         algo.fit(ts)  # warm (build + first launches)
         torch.cuda.synchronize()
         t = time.perf_counter()
-        algo = SVDpp(**params, mode=mode, chunks_per_epoch=chunks).fit(ts)
+        algo = SVDpp(**params, mode=mode, chunks_per_epoch=chunks, n_waves=waves).fit(ts)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t) / params["n_epochs"] * 1e3
         got = accuracy.rmse(algo.test(test), verbose=False)
-        print("mode %-6s chunks %d ydefer %s: rmse %.5f delta %+.5f  fit %.3f ms/epoch (incl. setup)"
-              % (mode, chunks, ydefer, got, got - ref, dt), flush=True)
+        eng = algo._engine
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(10):
+            for c in range(eng.n_chunks):
+                eng.run_chunk(c)
+                eng.sync_items(None)
+        torch.cuda.synchronize()
+        ep = (time.perf_counter() - t) / 10 * 1e3
+        print("mode %-6s chunks %d ydefer %s order %s waves %d: rmse %.5f delta %+.5f  epoch "
+              "%.3f ms (fit %.3f ms/epoch incl. setup)" % (mode, chunks, ydefer, order, waves, got,
+                                                          got - ref, ep, dt), flush=True)
 
 
 if __name__ == "__main__":

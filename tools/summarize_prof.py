@@ -1,4 +1,5 @@
-"""Summarise rocprofv3 outputs of tools/profile.sh into profiles/<tag>_*.{csv,json}."""
+"""Summarise rocprofv3 outputs of tools/profile.sh into profiles/<tag>_*.{csv,json} and
+profiles/traffic_<algo>_k<K>_<shape>.json (HBM bytes of ONE step, every kernel of the step)."""
 import csv
 import glob
 import json
@@ -11,11 +12,19 @@ tag = sys.argv[1]
 out = os.path.join(ROOT, "gpurun_out")
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
+EPOCH = "mf_epoch_kernel"
 
 
 def find(pattern):
     hits = sorted(glob.glob(os.path.join(out, pattern), recursive=True))
     return hits[0] if hits else None
+
+
+def short(name):
+    """kernel name without template arguments / parameter list"""
+    n = name.split("(")[0]
+    n = n.split("<")[0]
+    return n.replace("void ", "").split("::")[-1].strip()
 
 
 summary = {"tag": tag}
@@ -26,7 +35,7 @@ if stats:
         rows = list(csv.DictReader(f))
     summary["kernel_stats"] = [{k: r[k] for k in r if k in ("Name", "Calls", "TotalDurationNs",
                                                            "AverageNs", "Percentage", "MinNs",
-                                                           "MaxNs")} for r in rows[:12]]
+                                                           "MaxNs")} for r in rows[:16]]
 bench = os.path.join(out, "prof_%s_bench.log" % tag)
 if os.path.exists(bench):
     lines = [l for l in open(bench) if l.startswith("{")]
@@ -43,8 +52,7 @@ def pmc(kind, counter):
         for r in csv.DictReader(f):
             if r.get("Counter_Name") != counter:
                 continue
-            name = r.get("Kernel_Name", "")
-            vals.setdefault(name, []).append(float(r["Counter_Value"]))
+            vals.setdefault(short(r.get("Kernel_Name", "")), []).append(float(r["Counter_Value"]))
     return {k: {"dispatches": len(v), "mean_per_dispatch": sum(v) / len(v)} for k, v in vals.items()}
 
 
@@ -52,23 +60,31 @@ fetch = pmc("fetch", "FETCH_SIZE")
 write = pmc("write", "WRITE_SIZE")
 summary["FETCH_SIZE_kib"] = fetch
 summary["WRITE_SIZE_kib"] = write
-# HBM-side bytes per epoch-kernel launch, corrected as MI355X_MICROARCH.md (HBM) prescribes:
-# FETCH_SIZE tallies 128-B read requests at 64 B on gfx950 -> x2; WRITE_SIZE is exact.
-# Calibrated on our own access pattern: log_reduce_kernel reads a known 404 B/rating from
-# 448-B-strided rows (4 x 128-B lines each), and 2 x FETCH_SIZE matches that line count.
+# HBM-side bytes, corrected as MI355X_MICROARCH.md (HBM) prescribes: FETCH_SIZE tallies 128-B read
+# requests at 64 B on gfx950 -> x2; WRITE_SIZE is exact.  One step = the dispatches of every
+# kernel per epoch-kernel dispatch (the PMC runs time warmup + steps epochs and nothing else).
 bench_line = summary.get("bench_line_under_profiler")
-if fetch and write and bench_line and "mf_epoch_kernel" in fetch and "mf_epoch_kernel" in write:
-    fb = 2 * fetch["mf_epoch_kernel"]["mean_per_dispatch"] * 1024
-    wb = write["mf_epoch_kernel"]["mean_per_dispatch"] * 1024
+if fetch and write and bench_line and EPOCH in fetch and EPOCH in write:
+    per = {}
+    n_epoch = fetch[EPOCH]["dispatches"]
+    for k in sorted(set(fetch) & set(write)):
+        d = fetch[k]["dispatches"] / n_epoch  # dispatches per step
+        fb = 2 * fetch[k]["mean_per_dispatch"] * 1024 * d
+        wb = write[k]["mean_per_dispatch"] * 1024 * d
+        per[k] = {"dispatches_per_step": d, "read_bytes": fb, "write_bytes": wb,
+                  "bytes_per_step": fb + wb}
+    total = sum(v["bytes_per_step"] for v in per.values())
     cfg = bench_line["config"]
-    n_up = bench_line["roofline"]["updates_per_launch"]
-    traffic = {"kernel": "mf_epoch_kernel", "bytes_per_launch": fb + wb, "read_bytes": fb,
-               "write_bytes": wb, "bytes_per_update": (fb + wb) / n_up,
+    n_up = bench_line["roofline"]["updates_per_step"]
+    traffic = {"bytes_per_step": total, "bytes_per_update": total / n_up,
                "algorithmic_bytes_per_update": bench_line["roofline"]["algorithmic_bytes_per_update"],
-               "source": "profiles/%s_summary.json (2 x FETCH_SIZE + WRITE_SIZE, separate passes)" % tag,
+               "per_kernel": per,
+               "source": "profiles/%s_summary.json (2 x FETCH_SIZE + WRITE_SIZE, separate --pmc "
+                         "passes, every kernel of the step)" % tag,
                "workload": cfg["workload"]}
     summary["traffic"] = traffic
-    with open(os.path.join(prof, "traffic_%s_k%d.json" % (cfg["algo"], cfg["n_factors"])), "w") as f:
+    name = "traffic_%s_k%d_%s.json" % (cfg["algo"], cfg["n_factors"], cfg.get("shape", "ml-1m"))
+    with open(os.path.join(prof, name), "w") as f:
         json.dump(traffic, f, indent=1)
 with open(os.path.join(prof, "%s_summary.json" % tag), "w") as f:
     json.dump(summary, f, indent=1)
