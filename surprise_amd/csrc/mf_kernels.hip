@@ -93,6 +93,18 @@ struct Hyper {
     T lr_bu, lr_bi, lr_pu, lr_qi, lr_yj, reg_bu, reg_bi, reg_pu, reg_qi, reg_yj, gm;
 };
 
+// x^n by repeated squaring (n >= 0)
+template <typename T>
+__device__ __forceinline__ T pow_int(T x, int n) {
+    T r = T(1);
+    while (n) {
+        if (n & 1) r *= x;
+        x *= x;
+        n >>= 1;
+    }
+    return r;
+}
+
 template <typename T>
 Hyper<T> cast_hyper(const mf_hyper_t *h) {
     Hyper<T> o;
@@ -1080,6 +1092,303 @@ __device__ __forceinline__ void epoch_body_la(
     for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w]);
 }
 
+#ifndef MF_PP_LA
+#define MF_PP_LA 1  // SVD++ (atomic q rows, deferred y): the lookahead body below
+#endif
+
+// ---- SVD++ rating loop in lookahead form (kAtomic, deferred y, G <= 2, no repeated items)
+//
+// SVDpp.sgd per rating (mf.pyx:478-498) in the exact per-user affine form: with m_k = u_impl
+// before rating k (m_0 = sum_{j in I_u} y_j / sqrt|I_u|, one gather at the user's start) and
+// s_k = p_k + m_k (column K: the constant 1 of the bias),
+//   err_k = r_k - c_k - <q_k, s_k>,  p_{k+1} = ap o p_k + err_k lrp o q_k,
+//   m_{k+1} = dc o m_k + err_k lry o q_k  (dc = 1 - lr_yj reg_yj, lry = lr_yj: every y_j of the
+//   user takes the same step, so u_impl moves by lr_yj err q_k),
+//   q_k += err_k lrq o s_k + nrq o q_k  (float atomics on the shared row, bias in column K).
+// One rating back, s_k = B_{k-1} + err_{k-1} D_{k-1} with B = ap o p + dc o m and
+// D = (lrp + lry) o q, so err_k = (r_k - c0_{k-1}) - X_k - err_{k-1} (Y_k + lr_bu) with
+// X_k = <q_k, B_{k-1}>, Y_k = <q_k, D_{k-1}>: the recursion of epoch_body_la, whose reductions run
+// a rating ahead of their use.  The q atomics of a bank are issued one bank late, after the next
+// bank's row gathers (a row's vmcnt wait then never covers an atomic younger than a whole bank:
+// an atomic stays counted for thousands of cycles under load).  The y update is deferred:
+// c_u = (m_n - dc^n m_0) / sqrt|I_u| goes to ycbuf (mf_svdpp_y_fold applies it after the chunk).
+template <typename T, int G>
+__device__ __forceinline__ void epoch_body_pp_la(
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
+    const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
+    T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *ycbuf, int K,
+    Hyper<T> hp, int n_items, int64_t n_waves_req)
+{
+    using L = Lane8<T>;
+    using vec = typename L::vec;
+    constexpr int W = L::W;
+    constexpr int kB = G == 1 ? MF_LA_BANK : MF_LA_BANK_G2;
+    constexpr int U = Lane1<T, G>::U;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t grid_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
+    if (wave >= n_waves) return;
+
+    const uint32_t qrow = (uint32_t)ldq * sizeof(T), yrow = (uint32_t)ldu * sizeof(T);
+    const uint32_t q_oob = (uint32_t)n_items * qrow, y_oob = (uint32_t)n_items * yrow;
+    uint32_t cq[G], cu[G], cq1[U], cy1[U];
+    vec one[G], lrp[G], ap[G], lry[G], lrpy[G], lrq[G], nrq[G];
+    const T dc = T(1) - hp.lr_yj * hp.reg_yj;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = lane + kWave * u;
+        cq1[u] = c < ldq ? (uint32_t)c * sizeof(T) : q_oob;
+        cy1[u] = c < ldu ? (uint32_t)c * sizeof(T) : y_oob;
+    }
+#pragma unroll
+    for (int v = 0; v < G; ++v) {
+        const int c0 = (lane + kWave * v) * W;
+        const uint32_t b = (uint32_t)c0 * sizeof(T);
+        cq[v] = c0 < ldq ? b : q_oob;
+        cu[v] = c0 < ldu ? b : y_oob;  // >= the pu / ycbuf records (K elements) too: dropped
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            const int c = c0 + e;
+            const bool fac = c < K, bias = c == K;
+            const T lq = fac ? hp.lr_qi : (bias ? hp.lr_bi : T(0));
+            const T rq = fac ? hp.reg_qi : (bias ? hp.reg_bi : T(0));
+            L::set(one[v], e, bias ? T(1) : T(0));
+            L::set(lrp[v], e, fac ? hp.lr_pu : T(0));
+            L::set(ap[v], e, fac ? T(1) - hp.lr_pu * hp.reg_pu : T(1));
+            L::set(lry[v], e, fac ? hp.lr_yj : T(0));
+            L::set(lrpy[v], e, fac ? hp.lr_pu + hp.lr_yj : T(0));
+            L::set(lrq[v], e, lq);
+            L::set(nrq[v], e, -lq * rq);
+        }
+    }
+    const T lr_bu = hp.lr_bu;
+    const T abu = T(1) - lr_bu * hp.reg_bu;
+    const T kb = hp.gm * (T(1) - abu);
+    const rsrc_t q_rs = make_rsrc(qb, q_oob);
+    const rsrc_t y_rs = make_rsrc(yj, y_oob);
+    const int prio_len = (int)(row_ptr[sched[0] + 1] - row_ptr[sched[0]]);
+
+    auto do_user = [&](const int u) {
+        const int64_t s = row_ptr[u];
+        const int n = (int)(row_ptr[u + 1] - s);
+        if (n <= 0) return;
+        if (n * 2 > prio_len) __builtin_amdgcn_s_setprio(3);
+        else if (n * 4 > prio_len) __builtin_amdgcn_s_setprio(2);
+        else if (n * 8 > prio_len) __builtin_amdgcn_s_setprio(1);
+        const int32_t *__restrict__ it = items + s;
+        const T *__restrict__ rt = ratings + s;
+        const rsrc_t p_rs = make_rsrc(pu + (int64_t)u * ldu, (uint32_t)K * sizeof(T));
+        const rsrc_t b_rs = make_rsrc(bu + u, sizeof(T));
+        const T rs_n = T(1) / sqrt(T(n));  // mf.pyx:470-476
+
+        vec p0[G];
+#pragma unroll
+        for (int v = 0; v < G; ++v) p0[v] = L::template ld<0>(p_rs, cu[v]) + one[v];
+        const T bu0 = Buf<T>::template ld<0>(b_rs, 0);
+
+        // u_impl at the user's start: the y_j rows (chunk-start values: the fold is deferred)
+        // gathered 32 at a time in the Lane1 view, 64 item ids per vector load
+        vec m0[G];
+        {
+            constexpr int kYB = 32;
+            T acc1[U];
+#pragma unroll
+            for (int uu = 0; uu < U; ++uu) acc1[uu] = T(0);
+            for (int x0 = 0; x0 < n; x0 += kWave) {
+                const int gid = it[x0 + lane < n ? x0 + lane : n - 1];
+                const int cnt = n - x0 < kWave ? n - x0 : kWave;
+                for (int x = 0; x < cnt; x += kYB) {
+                    T g[kYB][U];
+#pragma unroll
+                    for (int a = 0; a < kYB; ++a) {
+                        const uint32_t ro = (uint32_t)readlane(gid, x + a < kWave ? x + a : kWave - 1) *
+                                                yrow + (x + a < cnt ? 0u : y_oob);
+#pragma unroll
+                        for (int uu = 0; uu < U; ++uu) g[a][uu] = Buf<T>::template ld<0>(y_rs, ro + cy1[uu]);
+                    }
+#pragma unroll
+                    for (int a = 0; a < kYB; ++a)
+#pragma unroll
+                        for (int uu = 0; uu < U; ++uu) acc1[uu] += g[a][uu] * rs_n;
+                }
+            }
+            to_lane8<G>(acc1, m0);
+        }
+
+        auto grp_load = [&](int j0, uint32_t &go, T &gr) {
+            int j = j0 + (lane & (kB - 1));
+            j = j < n ? j : n - 1;
+            go = (uint32_t)it[j] * qrow;
+            gr = rt[j];
+        };
+        vec bank[2][kB][G];
+        T br[2][kB];
+        uint32_t bo[2][kB];
+        vec dl[kB][G];      // the q deltas of the current bank (issued one bank late)
+        uint32_t dlo[kB];   // their row offsets (masked ratings: past the table)
+        uint32_t go_n1, go_n2;
+        T gr_n1, gr_n2;
+        auto fill = [&](const int bk, const uint32_t go, const T gr) {
+#pragma unroll
+            for (int d = 0; d < kB; ++d) {
+                const uint32_t off = readlane((int)go, d);
+                bo[bk][d] = off;
+                br[bk][d] = readlane(gr, d);
+#pragma unroll
+                for (int v = 0; v < G; ++v) bank[bk][d][v] = L::template lds<kSc1>(q_rs, cq[v], off);
+            }
+        };
+        auto flush = [&]() {  // the float atomics of the previous bank's ratings
+#pragma unroll
+            for (int d = 0; d < kB; ++d) {
+                T d1[U];
+                to_lane1<G>(dl[d], d1);
+#if defined(MF_EXP_ATOM_SPREAD)  // timing experiment only (wrong results): no two waves on a row
+                const uint32_t ao = (uint32_t)((wave * 131 + d) % n_items) * qrow;
+#else
+                const uint32_t ao = dlo[d];
+#endif
+#if defined(MF_EXP_GLOBAL_ATOM)  // timing experiment: global_atomic_add_f32 instead of buffer
+#pragma unroll
+                for (int uu = 0; uu < U; ++uu) {
+                    const uint32_t o = ao + cq1[uu];
+                    if (o < q_oob)
+                        __hip_atomic_fetch_add((T *)((char *)qb + o), d1[uu], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                }
+#elif !defined(MF_EXP_NO_QATOM)
+#pragma unroll
+                for (int uu = 0; uu < U; ++uu) atom_add1(q_rs, qb, q_oob, cq1[uu], ao, d1[uu]);
+#endif
+            }
+        };
+        {
+            uint32_t go0;
+            T gr0;
+            grp_load(0, go0, gr0);
+            grp_load(kB, go_n1, gr_n1);
+            asm volatile("" ::"v"(go0), "v"(gr0), "v"(go_n1), "v"(gr_n1));
+            __builtin_amdgcn_sched_barrier(0);
+            fill(0, go0, gr0);
+        }
+        // state entering rating k: err_p = err_{k-1}, c0_p = c0_{k-1}, Pp = ap o p_{k-1},
+        // Mp = dc o m_{k-1}, Dpp = lrp o q_{k-1}, Dmp = lry o q_{k-1}, X = X_k, Yb = Y_k + lr_bu
+        // (k = 0: err_{-1} = 0, c0_{-1} = c_0, Pp = p_0, Mp = m_0, X_0 = <q_0, p_0 + m_0>)
+        T err_p = T(0), c0_p = hp.gm + bu0, X, Yb = T(0);
+        vec Pp[G], Mp[G], Dpp[G], Dmp[G];
+        {
+            vec part = L::splat(T(0));
+#pragma unroll
+            for (int v = 0; v < G; ++v) {
+                Pp[v] = p0[v];
+                Mp[v] = m0[v];
+                Dpp[v] = L::splat(T(0));
+                Dmp[v] = L::splat(T(0));
+                part += bank[0][0][v] * (p0[v] + m0[v]);
+            }
+            X = wave_sum_u(L::hsum(part));
+        }
+        auto step = [&](auto full_c, auto bank_c, const int j0, const int d) {
+            constexpr bool FULL = decltype(full_c)::value;
+            constexpr int bk = decltype(bank_c)::value;
+            const int k = j0 + d;
+            const bool valid = FULL || k < n;
+            vec (&qn)[G] = d + 1 < kB ? bank[bk][d + 1] : bank[bk ^ 1][0];
+#pragma unroll
+            for (int v = 0; v < G; ++v) asm volatile("" : "+v"(qn[v])::"memory");
+            const T err = (br[bk][d] - c0_p) - X - err_p * Yb;  // mf.pyx:483
+            const T c0 = abu * (lr_bu * err_p + c0_p) + kb;     // mf.pyx:486, one rating late
+            vec P[G], M[G], Dp[G], Dm[G], px = L::splat(T(0)), py = L::splat(T(0));
+#pragma unroll
+            for (int v = 0; v < G; ++v) {
+                const vec q = bank[bk][d][v];
+                const vec pk = Pp[v] + err_p * Dpp[v];  // p_k, m_k (one rating late)
+                const vec mk = Mp[v] + err_p * Dmp[v];
+                const vec sk = pk + mk;                 // puf + u_impl (mf.pyx:491-493)
+                P[v] = ap[v] * pk;
+                M[v] = dc * mk;
+                Dp[v] = lrp[v] * q;
+                Dm[v] = lry[v] * q;
+                px += qn[v] * (P[v] + M[v]);
+                py += qn[v] * (lrpy[v] * q);
+                dl[d][v] = err * (lrq[v] * sk) + nrq[v] * q;  // mf.pyx:489, :492
+            }
+            dlo[d] = valid ? bo[bk][d] : bo[bk][d] + q_oob;
+            T Xn, Yn;
+            wave_sum2_u(L::hsum(px), L::hsum(py), Xn, Yn);  // X_{k+1}, Y_{k+1}
+            err_p = valid ? err : err_p;
+            c0_p = valid ? c0 : c0_p;
+            X = valid ? Xn : X;
+            Yb = valid ? Yn + lr_bu : Yb;
+#pragma unroll
+            for (int v = 0; v < G; ++v) {
+                Pp[v] = valid ? P[v] : Pp[v];
+                Mp[v] = valid ? M[v] : Mp[v];
+                Dpp[v] = valid ? Dp[v] : Dpp[v];
+                Dmp[v] = valid ? Dm[v] : Dmp[v];
+            }
+        };
+        int j0 = 0;
+        auto full_bank = [&](auto bank_c, auto first_c) {
+            constexpr int bk = decltype(bank_c)::value;
+            grp_load(j0 + 2 * kB, go_n2, gr_n2);
+            asm volatile("" ::: "memory");  // issue order: ids, rows, then the atomics
+            fill(bk ^ 1, go_n1, gr_n1);
+            asm volatile("" ::: "memory");
+            if (!decltype(first_c)::value) flush();
+            go_n1 = go_n2;
+            gr_n1 = gr_n2;
+#pragma unroll
+            for (int d = 0; d < kB; ++d) step(std::true_type{}, bank_c, j0, d);
+            j0 += kB;
+        };
+        auto tail_bank = [&](auto bank_c) {
+            if (j0 > 0) flush();
+#pragma unroll
+            for (int d = 0; d < kB; ++d) step(std::false_type{}, bank_c, j0, d);
+            flush();
+        };
+        using B0 = std::integral_constant<int, 0>;
+        using B1 = std::integral_constant<int, 1>;
+        if (n >= kB) {
+            full_bank(B0{}, std::true_type{});
+            while (j0 + 2 * kB <= n) {
+                full_bank(B1{}, std::false_type{});
+                full_bank(B0{}, std::false_type{});
+            }
+            if (j0 + kB <= n) {
+                full_bank(B1{}, std::false_type{});
+                if (j0 < n) tail_bank(B0{});
+                else flush();
+            } else if (j0 < n) {
+                tail_bank(B1{});
+            } else {
+                flush();
+            }
+        } else {
+            tail_bank(B0{});
+        }
+        // after rating n-1: p_n, m_n (u_impl), c_n
+        vec cacc[G];
+        const T A = pow_int(dc, n);
+#pragma unroll
+        for (int v = 0; v < G; ++v) {
+            L::template st<0>(p_rs, cu[v], Pp[v] + err_p * Dpp[v]);
+            cacc[v] = ((Mp[v] + err_p * Dmp[v]) - A * m0[v]) * rs_n;
+        }
+        const T bu_u = lr_bu * err_p + c0_p - hp.gm;
+        Buf<T>::template st<0>(b_rs, lane == 0 ? 0u : (uint32_t)sizeof(T), bu_u);
+        const rsrc_t c_rs = make_rsrc(ycbuf + (int64_t)u * ldu, (uint32_t)K * sizeof(T));
+#pragma unroll
+        for (int v = 0; v < G; ++v) L::template st<0>(c_rs, cu[v], cacc[v]);
+        __builtin_amdgcn_s_setprio(0);
+    };
+
+    for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w]);
+}
+
 #ifndef MF_LA
 #define MF_LA 1
 #endif
@@ -1096,6 +1405,13 @@ __device__ __forceinline__ void epoch_body_la(
 template <typename T, int G, int MODE, bool PP, bool DUPS>
 __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
 {
+    if constexpr (MODE == kAtomic && PP && !DUPS && G <= kLaMaxG && MF_PP_LA) {
+        if (elog) {  // deferred y (elog = ycbuf)
+            epoch_body_pp_la<T, G>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
+                                   yj, elog, K, hp, n_items, n_waves_req);
+            return;
+        }
+    }
     if constexpr (MODE == kLog && !PP && G <= kLaMaxG && MF_LA) {
         if (elog)
             epoch_body_la<T, G, true>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,

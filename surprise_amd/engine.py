@@ -39,9 +39,13 @@ def default_ld(n_factors: int, dtype: int) -> int:
     return _pad64(n_factors, dtype)
 
 
+ITEM_ROW_ALIGN = int(os.environ.get("SURPRISE_AMD_QALIGN", "64"))  # bytes (timing experiments)
+
+
 def default_ldq(n_factors: int, dtype: int) -> int:
     """Item row length: n_factors + the item bias column, padded to a 64-byte multiple."""
-    return _pad64(n_factors + 1, dtype)
+    per = ITEM_ROW_ALIGN // (4 if dtype == _lib.MF_F32 else 8)
+    return -(-(n_factors + 1) // per) * per
 
 
 def stable_argsort(keys):
