@@ -17,8 +17,8 @@
  *   - factor tables are row-major.  User rows pu[u] and implicit rows yj[j] have leading
  *     dimension ldu >= n_factors; item rows have ldq >= n_factors + 1 and hold the item bias in
  *     column n_factors: qb[i] = [q_i | b_i | 0 ...].  Padding columns must be zero and stay zero;
- *   - item tables (qb, yj) must be < 715 MB (32-bit buffer offsets, three of which must add
- *     below 2^31);
+ *   - item tables (qb, yj) must be < 2 GiB - 4 KiB (32-bit buffer offsets: a masked lane's
+ *     offset is the row's offset plus the table size);
  *   - `dtype` selects the arithmetic type of every floating array: MF_F32 or MF_F64.
  */
 #ifndef SURPRISE_AMD_H

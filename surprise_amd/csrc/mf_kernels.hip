@@ -204,9 +204,11 @@ __device__ __forceinline__ int xcc_id() {
 // prefetches of the next kPF ratings in flight behind counted vmcnt waits.
 
 using rsrc_t = __amdgpu_buffer_rsrc_t;
-// Offsets stay below 2^31 (the check misbehaves on offsets with bit 31 set, measured): a masked
-// offset is a real offset plus the table size, so tables must be < 2^31 / 3 bytes (kMaxTable).
-constexpr uint64_t kMaxTable = 0x7FFFFFFFull / 3;
+// Range check, measured on gfx950 (tools/probe_buffer_range.hip): a lane's access is dropped iff
+// voffset + soffset >= num_records, the sum taken without 32-bit wrap-around, for any
+// num_records up to 0xFFFFFFFF.  A masked offset is a real offset plus the table size, computed
+// in 32 bits here, so tables must stay below 2^31 bytes (kMaxTable, less one 4 KiB row).
+constexpr uint64_t kMaxTable = 0x80000000ull - 4096;
 constexpr int kSc1 = 16;                // gfx950 cache policy: sc1 (bypass the CU's L1)
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void *p, uint32_t bytes) {
@@ -1731,10 +1733,16 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
             for (int y = 0; y < kU; ++y) {  // (x past cnt: lane cnt-1's rating, weight 0)
                 const int x = x0 + y < kWave ? x0 + y : kWave - 1;
                 const T *row = ckpt + (int64_t)readlane(c_l, x) * ldq;
+#if defined(MF_REPLAY_CK_AUX)  // timing experiment: checkpoint rows with a cache policy
+                const rsrc_t ck_rs = make_rsrc(row, qrow);
+#pragma unroll
+                for (int v = 0; v < G; ++v) p[y][v] = L::template ld<MF_REPLAY_CK_AUX>(ck_rs, cq[v]);
+#else
 #pragma unroll
                 for (int v = 0; v < G; ++v)  // (non-temporal: keep L2 for the item rows)
                     p[y][v] = MF_REPLAY_NT ? __builtin_nontemporal_load((const vec *)(row + cc[v]))
                                            : *(const vec *)(row + cc[v]);
+#endif
 #pragma unroll
                 for (int m = 0; m < kR; ++m) {
                     const uint32_t off = readlane((int)qo_l[m], x);
@@ -2799,7 +2807,7 @@ int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const v
     const size_t esz = dtype == MF_F32 ? 4 : 8;
     if ((uint64_t)c->n_items * (uint64_t)ldq * esz >= kMaxTable ||
         (uint64_t)c->n_items * (uint64_t)ldu * esz >= kMaxTable)
-        return set_err(MF_E_UNSUPPORTED, "item table >= 715 MB (32-bit buffer offsets)");
+        return set_err(MF_E_UNSUPPORTED, "item table >= 2 GiB (32-bit buffer offsets)");
     return 0;
 }
 

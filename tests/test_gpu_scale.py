@@ -79,3 +79,127 @@ def test_c5_two_ranks_within_1e3_of_one(torch, c5_one):
     r2 = _bench("--shape", "c5", "--users", C5_USERS, "--gpus", "2", "--backend", "gloo")
     assert r2["n_gpus"] == 2
     assert abs(r2["rmse"]["gpu"] - c5_one["rmse"]["gpu"]) < 1e-3, (r2["rmse"], c5_one["rmse"])
+
+
+# ------------------------------------------------------------------ item tables above 715 MB
+# (the round-1 limit; now < 2 GiB, tools/probe_buffer_range.hip): 3,000 rated items spread over
+# a table of ~800k rows, so gathers, stores and atomics reach offsets far past 715 MB.  Unrated
+# rows never change, so the oracle runs on the compacted problem (rated items renumbered).
+
+def _big_table_case(n_items, K, seed=11):
+    import numpy as np
+    rng = np.random.RandomState(seed)
+    n_users, M = 1500, 3000
+    ids = np.sort(rng.choice(n_items - 2, M - 2, replace=False))
+    ids = np.concatenate([ids, [n_items - 2, n_items - 1]]).astype(np.int32)  # the last rows
+    rows = [np.sort(rng.choice(M, rng.randint(5, 160), replace=False)) for _ in range(n_users)]
+    row_ptr = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
+    local = np.concatenate(rows).astype(np.int32)
+    ratings = rng.randint(1, 6, len(local)).astype(np.float64)
+    pu0 = rng.normal(0, .1, (n_users, K))
+    qc0 = rng.normal(0, .1, (M, K))
+    yc0 = rng.normal(0, .1, (M, K))
+    return ids, row_ptr, local, ratings, pu0, qc0, yc0
+
+
+def _scatter_rows(ids, rows, n_items):
+    import numpy as np
+    full = np.zeros((n_items, rows.shape[1]))
+    full[ids] = rows
+    return full
+
+
+HYPER = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, lr_yj=.005, reg_bu=.02,
+             reg_bi=.02, reg_pu=.02, reg_qi=.02, reg_yj=.02)
+
+
+@pytest.mark.parametrize("dtype,K,n_items", [("float32", 240, 800_000),
+                                             ("float64", 100, 1_100_000)])
+def test_svd_log_item_table_above_715mb(torch, dtype, K, n_items):
+    """SVD, default log schedule: fp32 K=240 (1 KiB rows: the lookahead body + checkpoint
+    replay, 819 MB table) and fp64 K=100 (915 MB, the direct body's gradient log) against the
+    delta-log oracle on the compacted problem."""
+    import numpy as np
+    import oracle as orc
+    from surprise_amd.engine import MFEngine
+    ids, row_ptr, local, ratings, pu0, qc0, _ = _big_table_case(n_items, K)
+    gm = float(ratings.mean())
+    eng = MFEngine((row_ptr, ids[local], ratings), n_items, K, hyper=dict(HYPER, global_mean=gm),
+                   dtype=dtype, mode="log")
+    assert eng.qb.numel() * eng.qb.element_size() > 715 * 2 ** 20
+    eng.set_factors(pu0, _scatter_rows(ids, qc0, n_items))
+    eng.run_epochs(2)
+    got = eng.get_factors()
+    hp = orc.hyper(**HYPER)
+    pu, qc, bu, bc = orc.svd_sgd_deltalog(row_ptr, local, ratings, len(ids), K, 2, True, gm, hp,
+                                          pu0.copy(), qc0.copy())
+    tol = 1e-9 if dtype == "float64" else 2e-5
+    np.testing.assert_allclose(got["pu"], pu, rtol=0, atol=tol)
+    np.testing.assert_allclose(got["qi"][ids], qc, rtol=0, atol=tol)
+    np.testing.assert_allclose(got["bi"][ids], bc, rtol=0, atol=tol)
+    np.testing.assert_allclose(got["bu"], bu, rtol=0, atol=tol)
+    untouched = np.setdiff1d(np.arange(0, n_items, 9973), ids)
+    assert not got["qi"][untouched].any() and not got["bi"][untouched].any()
+
+
+def _svdpp_train_rmse(row_ptr, local, ratings, gm, pu, q, y, bu, b):
+    import numpy as np
+    n = np.diff(row_ptr)
+    users = np.repeat(np.arange(len(n)), n)
+    imp = np.add.reduceat(y[local], row_ptr[:-1], axis=0) / np.sqrt(n)[:, None]
+    est = gm + bu[users] + b[local] + np.einsum("ij,ij->i", q[local], (pu + imp)[users])
+    return float(np.sqrt(np.mean((ratings - est) ** 2)))
+
+
+def test_svdpp_deterministic_item_tables_above_715mb(torch):
+    """SVD++ in the reference's sequential order (one wavefront, plain stores), fp64 K=100:
+    qb and yj of 915 MB each; factors within 1e-9 of the sequential oracle's."""
+    import numpy as np
+    import oracle as orc
+    from surprise_amd.engine import MFEngine
+    n_items, K = 1_100_000, 100
+    ids, row_ptr, local, ratings, pu0, qc0, yc0 = _big_table_case(n_items, K, seed=12)
+    gm = float(ratings.mean())
+    eng = MFEngine((row_ptr, ids[local], ratings), n_items, K, algo="svdpp",
+                   hyper=dict(HYPER, global_mean=gm), dtype="float64", deterministic=True)
+    assert eng.yj.numel() * eng.yj.element_size() > 715 * 2 ** 20
+    eng.set_factors(pu0, _scatter_rows(ids, qc0, n_items), yj=_scatter_rows(ids, yc0, n_items))
+    eng.run_epochs(2)
+    got = eng.get_factors()
+    pu, qc, yc, bu, bc = orc.svdpp_sgd(row_ptr, local, ratings, len(ids), K, 2, gm,
+                                       orc.hyper(**HYPER), pu0.copy(), qc0.copy(), yc0.copy())
+    for name, a, b in (("pu", got["pu"], pu), ("qi", got["qi"][ids], qc),
+                       ("yj", got["yj"][ids], yc), ("bu", got["bu"], bu), ("bi", got["bi"][ids], bc)):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-9, err_msg=name)
+    untouched = np.setdiff1d(np.arange(0, n_items, 9973), ids)
+    assert not got["qi"][untouched].any() and not got["yj"][untouched].any()
+
+
+def test_svdpp_atomic_item_tables_above_715mb(torch):
+    """SVD++ (float atomics on q, deferred y fold), fp32 K=240: qb 819 MB and yj 780 MB.  The
+    parallel schedule is timing-dependent, so the big-table run is held to the same engine on
+    the compacted table (3,000 rows): training RMSE within 2e-4 after 2 epochs."""
+    import numpy as np
+    from surprise_amd.engine import MFEngine
+    n_items, K = 800_000, 240
+    ids, row_ptr, local, ratings, pu0, qc0, yc0 = _big_table_case(n_items, K, seed=12)
+    gm = float(ratings.mean())
+    out = []
+    for big in (True, False):
+        n = n_items if big else len(ids)
+        eng = MFEngine((row_ptr, (ids[local] if big else local), ratings), n, K, algo="svdpp",
+                       hyper=dict(HYPER, global_mean=gm), dtype="float32", mode="atomic")
+        if big:
+            assert eng.yj.numel() * eng.yj.element_size() > 715 * 2 ** 20
+            eng.set_factors(pu0, _scatter_rows(ids, qc0, n), yj=_scatter_rows(ids, yc0, n))
+        else:
+            eng.set_factors(pu0, qc0, yj=yc0)
+        eng.run_epochs(2)
+        f = eng.get_factors()
+        sel = ids if big else slice(None)
+        out.append(_svdpp_train_rmse(row_ptr, local, ratings, gm, f["pu"], f["qi"][sel],
+                                     f["yj"][sel], f["bu"], f["bi"][sel]))
+        if big:
+            untouched = np.setdiff1d(np.arange(0, n_items, 9973), ids)
+            assert not f["qi"][untouched].any() and not f["yj"][untouched].any()
+    assert abs(out[0] - out[1]) < 2e-4, out
