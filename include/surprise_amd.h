@@ -93,6 +93,10 @@ typedef struct mf_csr {
  *               forwarding in MF_MODE_PLAIN / MF_MODE_ATOMIC; MF_MODE_LOG reads the snapshot row);
  */
 #define MF_EPOCH_DUP_ITEMS   1
+/* flags bits 8..15: XCD mask (bit x: only the launch's wavefronts on XCD x take users, the others
+ * exit at once; 0 = every XCD).  Lets two concurrent launches keep to disjoint XCDs, i.e.
+ * disjoint L2 caches (the SVD epoch's heaviest users beside the rest). */
+#define MF_EPOCH_XCD_SHIFT   8
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
                  const mf_hyper_t *hp, int32_t mode, void *qlog, void *elog, int32_t n_waves,
@@ -146,12 +150,13 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
  * c_k = ck_pos[x] <= k (x = the rating's index in perm; c_k = k - ((k - row_ptr[u]) mod
  * mf_ckpt_interval())) by the epoch kernel's recursion p <- ap * p + err_m * lr_pu * q_{item(m)}
  * (ap = 1 - lr_pu * reg_pu on factor columns) over the snapshot item rows qb -- call it before
- * mf_log_apply.  Requires ldq * sizeof(dtype) <= 1 KiB.
+ * mf_log_apply.  Requires ldq * sizeof(dtype) <= 1 KiB.  flags: bits 8..15 an XCD mask as in
+ * mf_svd_epoch (MF_EPOCH_XCD_SHIFT), 0 = every XCD.
  */
 int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_factors,
                   const mf_csr_t *csr, const void *qb, const mf_hyper_t *hp, const int32_t *perm,
                   const int32_t *ck_pos, const int32_t *piece_beg, int64_t n_pieces, void *sums,
-                  int32_t dtype, void *stream);
+                  int32_t flags, int32_t dtype, void *stream);
 
 /* Checkpoint interval of the checkpoint log (ratings per stored user row). */
 int mf_ckpt_interval(void);

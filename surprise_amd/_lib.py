@@ -19,6 +19,7 @@ MF_MODE_PLAIN, MF_MODE_ATOMIC, MF_MODE_LOG = 0, 1, 2
 MODES = {"plain": MF_MODE_PLAIN, "atomic": MF_MODE_ATOMIC, "log": MF_MODE_LOG}
 MF_MERGE_SUM, MF_MERGE_COUNT, MF_MERGE_MEAN = 0, 1, 2
 MF_EPOCH_DUP_ITEMS = 1
+MF_EPOCH_XCD_SHIFT = 8  # flags bits 8..15: XCD mask (include/surprise_amd.h)
 MAX_FACTORS = {MF_F32: 512, MF_F64: 256}
 
 
@@ -51,7 +52,7 @@ SIGNATURES = {
     "mf_sumsq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
     "mf_log_reduce": [_vp, _i32, _i32, _vp, _vp, _i64, _vp, _i32, _vp],
     "mf_log_replay": [_vp, _vp, _i32, _i32, ctypes.POINTER(MfCsr), _vp,
-                      ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _i32, _vp],
+                      ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _i32, _i32, _vp],
     "mf_ckpt_interval": [],
     "mf_log_apply": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
                      ctypes.POINTER(MfHyper), _vp, _i32, _vp, _i32, _vp, _i32, _vp],

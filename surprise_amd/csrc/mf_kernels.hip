@@ -37,7 +37,8 @@ extern thread_local char g_err[256];
 template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
-                    int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, void *stream);
+                    int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
+                    void *stream);
 }  // namespace mf_ext
 
 namespace {
@@ -73,6 +74,14 @@ int grid_for_waves(int64_t waves) {
     int64_t blocks = (waves * kWave + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
     return (int)blocks;
+}
+
+// blocks giving `waves` wave slots on the XCDs of xmask (wave_slot): a multiple of 8
+int grid_for_waves_x(int64_t waves, int xmask) {
+    if (!(xmask & 0xFF)) return grid_for_waves(waves);
+    const int64_t per = (grid_for_waves(waves) + __builtin_popcount(xmask & 0xFF) - 1) /
+                        __builtin_popcount(xmask & 0xFF);
+    return (int)(8 * per);
 }
 
 // G = 8-byte lane groups per row = ceil(ld * sizeof(T) / 512) (the epoch kernel's layout)
@@ -192,6 +201,27 @@ __device__ __forceinline__ int xcc_id() {
     // HW_REG_XCC_ID (hwreg 20), bits [3:0]: the XCD this wave runs on (mf_selftest_xcc: blocks
     // are dealt to the 8 XCDs round-robin).
     return (int)(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 0xF);
+}
+
+// The calling wave's slot among the launch's waves on the XCDs of xmask (bit x: XCD x; 0: every
+// XCD), and the number of such slots.  Blocks are dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md, checked by mf_selftest_xcc), so every group of 8 consecutive blocks holds
+// one block per XCD: slot = ((b / 8) * c + rank of the wave's XCD in xmask) * 4 + wave in block,
+// c = popcount(xmask).  Launches with a mask have a multiple of 8 blocks (grid_for_waves_x).
+// Returns false for a wave on an XCD outside the mask (it exits).
+__device__ __forceinline__ bool wave_slot(int xmask, int64_t &slot, int64_t &n_slots) {
+    const int64_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    if (!xmask) {
+        slot = (int64_t)blockIdx.x * (kBlock / kWave) + w;
+        n_slots = ((int64_t)gridDim.x * kBlock) / kWave;
+        return true;
+    }
+    const int x = __builtin_amdgcn_readfirstlane(xcc_id());
+    if (!((xmask >> x) & 1)) return false;
+    const int c = __builtin_popcount(xmask), rank = __builtin_popcount(xmask & ((1 << x) - 1));
+    slot = ((int64_t)(blockIdx.x >> 3) * c + rank) * (kBlock / kWave) + w;
+    n_slots = (int64_t)(gridDim.x >> 3) * c * (kBlock / kWave);
+    return true;
 }
 
 // ---------------------------------------------------------------- buffer (SRSRC) memory ops
@@ -442,7 +472,7 @@ __device__ __forceinline__ void epoch_body(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, T *ycbuf,
-    int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req)
+    int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -451,9 +481,8 @@ __device__ __forceinline__ void epoch_body(
     // wave id through readfirstlane: the compiler then knows it (and every user index, CSR
     // bound and loop counter derived from it) is wave-uniform -> SGPRs, scalar loads, scalar
     // branches instead of exec-masked ones.
-    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
-                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int64_t grid_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    int64_t wave, grid_waves;
+    if (!wave_slot(xmask, wave, grid_waves)) return;
     const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
     if (wave >= n_waves) return;  // whole wave exits (a 1-wave launch still uses a 4-wave block)
 
@@ -839,7 +868,7 @@ __device__ __forceinline__ void epoch_body_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *qlog, T *elog, int K,
-    int biased, Hyper<T> hp, int n_items, int64_t n_waves_req)
+    int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -848,9 +877,8 @@ __device__ __forceinline__ void epoch_body_la(
     constexpr int kB = G == 1 ? MF_LA_BANK : MF_LA_BANK_G2;
     static_assert(!CK || (kB % kCkpt == 0 && kB <= kWave), "checkpoints: whole banks");
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
-                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int64_t grid_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    int64_t wave, grid_waves;
+    if (!wave_slot(xmask, wave, grid_waves)) return;
     const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
     if (wave >= n_waves) return;
 
@@ -931,6 +959,9 @@ __device__ __forceinline__ void epoch_body_la(
             }
         };
         auto flush = [&](const int j0p) {  // log rows j0p .. j0p + kB - 1
+#if defined(MF_EXP_LA_NO_STORE)  // timing experiment only: no log written (wrong results)
+            return;
+#endif
             if constexpr (CK) {
 #pragma unroll
                 for (int x = 0; x < kLg; ++x)
@@ -1119,7 +1150,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *ycbuf, int K,
-    Hyper<T> hp, int n_items, int64_t n_waves_req)
+    Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -1127,9 +1158,8 @@ __device__ __forceinline__ void epoch_body_pp_la(
     constexpr int kB = G == 1 ? MF_LA_BANK : MF_LA_BANK_G2;
     constexpr int U = Lane1<T, G>::U;
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
-                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int64_t grid_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    int64_t wave, grid_waves;
+    if (!wave_slot(xmask, wave, grid_waves)) return;
     const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
     if (wave >= n_waves) return;
 
@@ -1399,10 +1429,10 @@ __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,                      \
         const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,       \
         T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, T *elog,\
-        int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req
+        int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask
 #define MF_EPOCH_ARGS \
     row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, elog, K, biased, hp,    \
-        n_items, n_waves_req
+        n_items, n_waves_req, xmask
 
 template <typename T, int G, int MODE, bool PP, bool DUPS>
 __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
@@ -1410,17 +1440,17 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
     if constexpr (MODE == kAtomic && PP && !DUPS && G <= kLaMaxG && MF_PP_LA) {
         if (elog) {  // deferred y (elog = ycbuf)
             epoch_body_pp_la<T, G>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
-                                   yj, elog, K, hp, n_items, n_waves_req);
+                                   yj, elog, K, hp, n_items, n_waves_req, xmask);
             return;
         }
     }
     if constexpr (MODE == kLog && !PP && G <= kLaMaxG && MF_LA) {
         if (elog)
             epoch_body_la<T, G, true>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
-                                      qlog, elog, K, biased, hp, n_items, n_waves_req);
+                                      qlog, elog, K, biased, hp, n_items, n_waves_req, xmask);
         else
             epoch_body_la<T, G, false>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb,
-                                       ldq, qlog, elog, K, biased, hp, n_items, n_waves_req);
+                                       ldq, qlog, elog, K, biased, hp, n_items, n_waves_req, xmask);
     } else {
         epoch_body<T, G, MODE, PP, DUPS, kPF>(MF_EPOCH_ARGS);
     }
@@ -1433,7 +1463,8 @@ namespace mf_ext {
 template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
-                    int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, void *stream)
+                    int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
+                    void *stream)
 {
     // elog: SVD: the checkpoint log (the lookahead body: kLog, up to two lane groups);
     //       SVD++: the deferred y buffer (kAtomic)
@@ -1448,16 +1479,17 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
         // (kLog reads a snapshot: a repeated item sees the chunk-start row, no forwarding)
         auto kern = (dups && M != kLog) ? mf_epoch_kernel<T, V, M, PP, true>
                                         : mf_epoch_kernel<T, V, M, PP, false>;
-        hipLaunchKernelGGL(kern, dim3(grid_for_waves(waves)), dim3(kBlock), 0, (hipStream_t)stream,
+        hipLaunchKernelGGL(kern, dim3(grid_for_waves_x(waves, xmask)), dim3(kBlock), 0,
+                           (hipStream_t)stream,
                            csr->row_ptr, csr->items, (const T *)csr->ratings, sched, n_sched,
                            (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K,
-                           biased, cast_hyper<T>(hp), csr->n_items, waves);
+                           biased, cast_hyper<T>(hp), csr->n_items, waves, xmask);
         return check_launch(PP ? "mf_epoch_kernel<svdpp>" : "mf_epoch_kernel<svd>");
     });
 }
 template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
-    void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, void *);
+    void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, void *);
 }  // namespace mf_ext
 #else  // the main translation unit
 
@@ -1681,7 +1713,7 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     const T *__restrict__ ckpt, const T *__restrict__ elog, int ldq, int K,
     const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T reg_pu,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
-    const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums)
+    const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int xmask)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -1689,9 +1721,8 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     constexpr int kR = kCkpt - 1;    // replay steps at most
     constexpr int kU = MF_REPLAY_U;  // ratings per group; two groups in flight
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
-                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    int64_t wave, n_waves;
+    if (!wave_slot(xmask, wave, n_waves)) return;
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), q_oob = (uint32_t)n_items * qrow;
     const rsrc_t q_rs = make_rsrc(qb, q_oob);
     uint32_t cq[G];
@@ -2818,6 +2849,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
                  int32_t dtype, void *stream)
 {
     const bool dups = flags & MF_EPOCH_DUP_ITEMS;
+    const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
     if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, qlog, dtype)) return rc;
     if (PP && !yj) return set_err(MF_E_ARG, "null yj");
     if (n_sched <= 0) return 0;
@@ -2830,7 +2862,8 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         using T = decltype(tag_t);
         constexpr int M = decltype(mode_c)::value;
         return mf_ext::launch_epoch_tm<T, M, PP>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj,
-                                                  qlog, elog, K, biased, hp, waves, dups, stream);
+                                                  qlog, elog, K, biased, hp, waves, dups, xmask,
+                                                  stream);
     };
     auto by_mode = [&](auto tag_t) -> int {
         switch (mode) {
@@ -2930,16 +2963,17 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
 int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_factors,
                   const mf_csr_t *csr, const void *qb, const mf_hyper_t *hp, const int32_t *perm,
                   const int32_t *ck_pos, const int32_t *piece_beg, int64_t n_pieces, void *sums,
-                  int32_t dtype, void *stream)
+                  int32_t flags, int32_t dtype, void *stream)
 {
     if (n_pieces < 0 || ldq < n_factors + 1 || n_factors < 0) return set_err(MF_E_ARG, "bad shape");
+    const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
     if (n_pieces == 0) return 0;
     if (!qlog || !elog || !csr || !qb || !hp || !perm || !ck_pos || !piece_beg || !sums)
         return set_err(MF_E_ARG, "null argument");
     const int64_t rb = (int64_t)ldq * (dtype == MF_F64 ? 8 : 4);
     if (rb > 512 * kLaMaxG) return set_err(MF_E_UNSUPPORTED, "checkpoint log: ldq * size <= 1 KiB only");
-    const int64_t cap = (int64_t)n_cus() * MF_REPLAY_WPC;
-    const int g = grid_for_waves(n_pieces < cap ? n_pieces : cap);
+    const int64_t cap = (int64_t)n_cus() * MF_REPLAY_WPC * (xmask ? __builtin_popcount(xmask) : 8) / 8;
+    const int g = grid_for_waves_x(n_pieces < cap ? n_pieces : cap, xmask);
     hipStream_t st = (hipStream_t)stream;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
@@ -2951,7 +2985,7 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
                 hipLaunchKernelGGL((log_replay_kernel<T, V>), dim3(g), dim3(kBlock), 0, st,
                                    (const T *)qlog, (const T *)elog, ldq, n_factors, csr->items,
                                    (const T *)qb, csr->n_items, (T)hp->lr_pu, (T)hp->reg_pu, perm,
-                                   ck_pos, piece_beg, n_pieces, (T *)sums);
+                                   ck_pos, piece_beg, n_pieces, (T *)sums, xmask);
                 return check_launch("log_replay_kernel");
             }
         });

@@ -97,13 +97,18 @@ def piece_bounds(offs, counts, piece_rows=PIECE_ROWS):
 
 
 def split_heavy(users, row_ptr, heavy):
-    """[rest, heaviest] of a chunk's users (schedule order kept): the heaviest are those with
-    >= heavy * the largest degree.  One group only when either would be empty."""
+    """[rest, heaviest] of a chunk's users (schedule order kept): the heaviest are the
+    int(heavy) users of largest degree (heavy >= 1) or those with >= heavy * the largest degree
+    (heavy < 1).  One group only when either would be empty."""
     users = np.asarray(users, np.int32)
     deg = np.diff(np.asarray(row_ptr, np.int64))[users]
     if not len(users) or heavy <= 0:
         return [users]
-    h = deg >= heavy * deg.max()
+    if heavy >= 1:
+        h = np.zeros(len(users), bool)
+        h[np.argsort(-deg, kind="stable")[:int(heavy)]] = True
+    else:
+        h = deg >= heavy * deg.max()
     if h.all() or not h.any():
         return [users]
     return [users[~h], users[h]]
@@ -282,10 +287,14 @@ class MFEngine(ItemSync, Predictor):
         self.ckpt = (self.mode == _lib.MF_MODE_LOG and bool(ckpt) and algo == "svd"
                      and esz_q <= 1024)
         # ... and then splits each chunk's users in two launches on two streams: the heaviest
-        # users (>= heavy * the chunk's largest degree: their sequential chains bound the epoch)
-        # beside the rest, whose log replay then overlaps the heavy chains
+        # users (their sequential chains bound a small epoch) on one XCD beside the rest on the
+        # other seven, whose log replay then overlaps the heavy chains
         if heavy is None:
-            heavy = float(os.environ.get("SURPRISE_AMD_HEAVY", "0"))
+            env = os.environ.get("SURPRISE_AMD_HEAVY")
+            heavy = float(env) if env is not None else self._auto_heavy(row_ptr)
+        # the heavy launch keeps to the XCDs of this mask and the rest to the others (disjoint
+        # L2s: the rest's log replay then does not evict the heavy chains' item rows)
+        self.heavy_xcd = int(os.environ.get("SURPRISE_AMD_HEAVY_XCD", "1"), 0) & 0xFF
         C = _lib.load().mf_ckpt_interval() if self.ckpt else 0
         _pu = []
         pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
@@ -376,6 +385,22 @@ class MFEngine(ItemSync, Predictor):
         if not self.biased:
             self._hyper.global_mean = 0.0
 
+    HEAVY_USERS = 128     # users in the heavy launch (measured: 64 0.231, 128 0.224, 256 0.232 ms)
+    HEAVY_MAX_NNZ = 8_000_000
+
+    def _auto_heavy(self, row_ptr):
+        """The heavy/light XCD split pays where the epoch is bound by its longest user chains:
+        small epochs (<= HEAVY_MAX_NNZ ratings per chunk) on a full 8-XCD MI355X (256 CUs); larger
+        epochs are bandwidth-bound and would leave the heavy XCD idle."""
+        if not self.ckpt or self.deterministic:
+            return 0.0
+        props = self.torch.cuda.get_device_properties(self.dev)
+        nnz = int(row_ptr[-1] - row_ptr[0])
+        if (props.multi_processor_count != 256 or nnz > self.n_chunks * self.HEAVY_MAX_NNZ
+                or self.n_users < 16 * self.HEAVY_USERS):
+            return 0.0
+        return float(self.HEAVY_USERS)
+
     # ------------------------------------------------------------------ state in / out
     def set_factors(self, pu, qi, bu=None, bi=None, yj=None):
         """Upload host fp64 arrays (n, K) into the padded device tables."""
@@ -427,10 +452,11 @@ class MFEngine(ItemSync, Predictor):
     def is_log(self):
         return self.mode == _lib.MF_MODE_LOG
 
-    def _epoch(self, sched, n_sched, n_waves, flags, st):
+    def _epoch(self, sched, n_sched, n_waves, flags, st, xmask=0):
         qlog = ctypes.c_void_p(self._qlog_base) if self.is_log else None
         elog = ctypes.c_void_p(self._elog_base) if self.ckpt else None
         flags |= _lib.MF_EPOCH_DUP_ITEMS if self.dup_items else 0
+        flags |= xmask << _lib.MF_EPOCH_XCD_SHIFT
         if self.algo == "svd":
             _lib.call("mf_svd_epoch", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
@@ -477,14 +503,15 @@ class MFEngine(ItemSync, Predictor):
             self.side.wait_event(fork)
             sh = ctypes.c_void_p(self.side.cuda_stream)
             n_h = hv["sched"].numel()
-            self._epoch(hv["sched"], n_h, n_h, 0, sh)
+            self._epoch(hv["sched"], n_h, n_h, 0, sh, self.heavy_xcd)
             if "end_h" in ev:
                 ev["end_h"].record(self.side)
             self._reduce_log(hv, self.sums.data_ptr() +
                              lg["n_pieces"] * self.ldq * self.sums.element_size(), sh)
             join = torch.cuda.Event()
             join.record(self.side)
-        self._epoch(s, s.numel(), self.n_waves, 0, st)
+        lx = (~self.heavy_xcd & 0xFF) if hv is not None and self.heavy_xcd else 0
+        self._epoch(s, s.numel(), self.n_waves, 0, st, lx)
         if "end" in ev:
             ev["end"].record(self.stream)
         if self.ydefer:
@@ -494,20 +521,21 @@ class MFEngine(ItemSync, Predictor):
                       self._ptr(y["pb"]), y["n_pieces"], self._ptr(y["ipp"]), self.n_items,
                       self._ptr(self.ypc_c), self._ptr(self.ypc_A), self.dtype, st)
         if lg is not None:
-            self._reduce_log(lg, self.sums.data_ptr(), st)
+            self._reduce_log(lg, self.sums.data_ptr(), st, lx)
         if hv is not None:
             self.stream.wait_event(join)
         if "end_r" in ev:
             ev["end_r"].record(self.stream)
 
-    def _reduce_log(self, lg, sums_ptr, st):
-        """Piece sums of one user group's log: mf_log_replay (checkpoint form) or mf_log_reduce."""
+    def _reduce_log(self, lg, sums_ptr, st, xmask=0):
+        """Piece sums of one user group's log: mf_log_replay (checkpoint form) or mf_log_reduce.
+        xmask: run on those XCDs only (bit x: XCD x; 0: all)."""
         if self.ckpt:
             _lib.call("mf_log_replay", ctypes.c_void_p(self._qlog_base),
                       ctypes.c_void_p(self._elog_base), self.ldq, self.K, ctypes.byref(self._csr),
                       self._ptr(self.qb), ctypes.byref(self._hyper), self._ptr(lg["perm"]),
                       self._ptr(lg["ck"]), self._ptr(lg["pb"]), lg["n_pieces"],
-                      ctypes.c_void_p(sums_ptr), self.dtype, st)
+                      ctypes.c_void_p(sums_ptr), xmask << _lib.MF_EPOCH_XCD_SHIFT, self.dtype, st)
         else:
             _lib.call("mf_log_reduce", ctypes.c_void_p(self._qlog_base), self.ldq, self.K + 1,
                       self._ptr(lg["perm"]), self._ptr(lg["pb"]), lg["n_pieces"],
