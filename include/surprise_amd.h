@@ -97,6 +97,10 @@ typedef struct mf_csr {
  * exit at once; 0 = every XCD).  Lets two concurrent launches keep to disjoint XCDs, i.e.
  * disjoint L2 caches (the SVD epoch's heaviest users beside the rest). */
 #define MF_EPOCH_XCD_SHIFT   8
+/* mf_svdpp_epoch, MF_MODE_ATOMIC with ycbuf, rows of <= 1 KiB: one user chain per workgroup
+ * (n_waves = chains) whose q deltas go through an LDS ring to three waves that issue the float
+ * atomics; sched entries < 0 are skipped (a schedule laid out per chain, strided by n_waves). */
+#define MF_EPOCH_SVDPP_HELPERS 2
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
                  const mf_hyper_t *hp, int32_t mode, void *qlog, void *elog, int32_t n_waves,

@@ -118,6 +118,26 @@ def svdpp_sgd(row_ptr, items, ratings, n_items, K, n_epochs, global_mean, hp, pu
     return pu, qi, yj, bu, bi
 
 
+def svdpp_sgd_hotstale(row_ptr, items, ratings, n_items, K, n_epochs, global_mean, hp, pu, qi,
+                       yj, hot, bu=None, bi=None):
+    """SVD++ in the GPU helper-wave schedule's form: y deferred per epoch, q live except the
+    items with hot[i] != 0 (epoch-start snapshot, steps folded with the count-aware weight)."""
+    row_ptr, items, ratings = _csr_args(row_ptr, items, ratings)
+    n_users = len(row_ptr) - 1
+    pu = np.ascontiguousarray(pu, dtype=np.float64)
+    qi = np.ascontiguousarray(qi, dtype=np.float64)
+    yj = np.ascontiguousarray(yj, dtype=np.float64)
+    bu = np.zeros(n_users) if bu is None else np.ascontiguousarray(bu, dtype=np.float64)
+    bi = np.zeros(n_items) if bi is None else np.ascontiguousarray(bi, dtype=np.float64)
+    hot = np.ascontiguousarray(hot, dtype=np.int32)
+    lib().oracle_svdpp_sgd_hotstale(ctypes.c_int64(n_users), ctypes.c_int64(n_items), _p(row_ptr),
+                                    _p(items), _p(ratings), ctypes.c_int32(K),
+                                    ctypes.c_int32(n_epochs), ctypes.c_double(global_mean),
+                                    ctypes.byref(hp), _p(hot), _p(pu), _p(qi), _p(yj), _p(bu),
+                                    _p(bi))
+    return pu, qi, yj, bu, bi
+
+
 def svd_sgd_groups(row_ptr, items, ratings, n_items, K, n_epochs, biased, global_mean, hp,
                    pu, qi, group_of_user, n_groups, chunk_of_user=None, n_chunks=1,
                    bu=None, bi=None):

@@ -20,6 +20,7 @@ MODES = {"plain": MF_MODE_PLAIN, "atomic": MF_MODE_ATOMIC, "log": MF_MODE_LOG}
 MF_MERGE_SUM, MF_MERGE_COUNT, MF_MERGE_MEAN = 0, 1, 2
 MF_EPOCH_DUP_ITEMS = 1
 MF_EPOCH_XCD_SHIFT = 8  # flags bits 8..15: XCD mask (include/surprise_amd.h)
+MF_EPOCH_SVDPP_HELPERS = 2
 MAX_FACTORS = {MF_F32: 512, MF_F64: 256}
 
 

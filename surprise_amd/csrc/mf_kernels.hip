@@ -38,7 +38,7 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    void *stream);
+                    bool hx, void *stream);
 }  // namespace mf_ext
 
 namespace {
@@ -1129,6 +1129,96 @@ __device__ __forceinline__ void epoch_body_la(
 #define MF_PP_LA 1  // SVD++ (atomic q rows, deferred y): the lookahead body below
 #endif
 
+// ---- SVD++ q deltas through an LDS ring (MF_SVDPP_HELPERS): one chain wave per workgroup
+// trains users; its per-rating q deltas go into a ring of row images in LDS and the workgroup's
+// three other waves issue the float atomics.  A wave that issues float atomics itself is held
+// by them (each stays counted in vmcnt for thousands of cycles and a wave can keep only a few
+// dozen in flight): measured, the SVD++ epoch with the atomics in the chain wave took 2.4x the
+// same loop without them.  Slot t % R holds rating t's delta row, written as the chain's 8-byte
+// lane elements (a row image: byte c * sizeof(T) = column c) and read back one column per lane
+// (64 consecutive dwords per atomic instruction).  head / tail[h]: ratings pushed / passed.
+#ifndef MF_PP_HX_BANK
+#define MF_PP_HX_BANK 8  // ratings per bank of gathered item rows in the helper-wave chain
+#endif
+#ifndef MF_PP_HX_R
+#define MF_PP_HX_R (4 * MF_PP_HX_BANK)  // ring slots
+#endif
+constexpr int kHxHelpers = 3;
+constexpr int kSpinMax = 1 << 22;  // bounded spins (s_sleep 2 each, ~0.2 s): never hang the GPU
+
+template <typename T, int G>
+struct PPRing {
+    static constexpr int R = MF_PP_HX_R;
+    typename Lane8<T>::vec data[R][G][kWave];
+    uint32_t off[R];
+    int head, done;
+    int tail[kHxHelpers];
+};
+
+__device__ __forceinline__ int lds_load(int *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// helper wave h of a chain: issue the atomics of the slots t = h (mod kHxHelpers)
+template <typename T, int G>
+__device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_items)
+{
+    constexpr int R = PPRing<T, G>::R;
+    constexpr int U = Lane1<T, G>::U;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t qrow = (uint32_t)ldq * sizeof(T), q_oob = (uint32_t)n_items * qrow;
+    const rsrc_t q_rs = make_rsrc(qb, q_oob);
+    uint32_t cq1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int c = lane + kWave * u;
+        cq1[u] = c < ldq ? (uint32_t)c * sizeof(T) : q_oob;
+    }
+    const T *img = (const T *)&ring->data[0][0][0];
+    constexpr int kSlotT = G * kWave * (int)(sizeof(typename Lane8<T>::vec) / sizeof(T));
+    int t = 0, spins = 0;
+    while (true) {
+        int hd = lds_load(&ring->head);
+        if (t >= hd) {
+            if (lds_load(&ring->done)) {
+                asm volatile("" ::: "memory");
+                hd = lds_load(&ring->head);
+                if (t >= hd) break;
+            } else {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > kSpinMax) break;
+                continue;
+            }
+        }
+        spins = 0;
+        asm volatile("" ::: "memory");
+        for (int tt = t + ((h - t % kHxHelpers) + kHxHelpers) % kHxHelpers; tt < hd;
+             tt += kHxHelpers) {
+            const int slot = tt % R;
+#if defined(MF_EXP_ATOM_SPREAD)  // timing experiment only (wrong results): rows spread uniformly
+            const uint32_t off = (uint32_t)(((uint32_t)(blockIdx.x * 131 + tt * 7919)) % n_items) * qrow;
+#else
+            const uint32_t off = __builtin_amdgcn_readfirstlane(ring->off[slot]);
+#endif
+            T v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = img[slot * kSlotT + lane + kWave * u];
+#if !defined(MF_EXP_NO_QATOM)
+#pragma unroll
+            for (int u = 0; u < U; ++u) atom_add1(q_rs, qb, q_oob, cq1[u], off, v[u]);
+#else
+            asm volatile("" ::"v"(v[0]), "s"(off));
+#endif
+        }
+        t = hd;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slots' reads have returned
+        lds_store(&ring->tail[h], t);
+    }
+}
+
 // ---- SVD++ rating loop in lookahead form (kAtomic, deferred y, G <= 2, no repeated items)
 //
 // SVDpp.sgd per rating (mf.pyx:478-498) in the exact per-user affine form: with m_k = u_impl
@@ -1145,26 +1235,33 @@ __device__ __forceinline__ void epoch_body_la(
 // bank's row gathers (a row's vmcnt wait then never covers an atomic younger than a whole bank:
 // an atomic stays counted for thousands of cycles under load).  The y update is deferred:
 // c_u = (m_n - dc^n m_0) / sqrt|I_u| goes to ycbuf (mf_svdpp_y_fold applies it after the chunk).
-template <typename T, int G>
+template <typename T, int G, bool HX>
 __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *ycbuf, int K,
-    Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask)
+    Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, PPRing<T, G> *ring)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
     constexpr int W = L::W;
-    constexpr int kB = G == 1 ? MF_LA_BANK : MF_LA_BANK_G2;
+    // (the chain of a helper-wave launch is alone on its SIMD: registers for deeper banks)
+    constexpr int kB = HX ? MF_PP_HX_BANK : (G == 1 ? MF_LA_BANK : MF_LA_BANK_G2);
     constexpr int U = Lane1<T, G>::U;
     const int lane = threadIdx.x & (kWave - 1);
     int64_t wave, grid_waves;
-    if (!wave_slot(xmask, wave, grid_waves)) return;
+    if (HX) {  // one chain per workgroup (wave 0; the others are pp_ring_helper)
+        wave = blockIdx.x;
+        grid_waves = gridDim.x;
+    } else if (!wave_slot(xmask, wave, grid_waves)) {
+        return;
+    }
     const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
     if (wave >= n_waves) return;
 
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), yrow = (uint32_t)ldu * sizeof(T);
     const uint32_t q_oob = (uint32_t)n_items * qrow, y_oob = (uint32_t)n_items * yrow;
+    int pushed = 0;  // HX: ratings pushed to the ring
     uint32_t cq[G], cu[G], cq1[U], cy1[U];
     vec one[G], lrp[G], ap[G], lry[G], lrpy[G], lrq[G], nrq[G];
     const T dc = T(1) - hp.lr_yj * hp.reg_yj;
@@ -1228,7 +1325,11 @@ __device__ __forceinline__ void epoch_body_pp_la(
             T acc1[U];
 #pragma unroll
             for (int uu = 0; uu < U; ++uu) acc1[uu] = T(0);
+#if defined(MF_EXP_NO_YGATHER)  // timing experiment only (wrong results): u_impl = 0
+            for (int x0 = 0; x0 < 0; x0 += kWave) {
+#else
             for (int x0 = 0; x0 < n; x0 += kWave) {
+#endif
                 const int gid = it[x0 + lane < n ? x0 + lane : n - 1];
                 const int cnt = n - x0 < kWave ? n - x0 : kWave;
                 for (int x = 0; x < cnt; x += kYB) {
@@ -1273,27 +1374,40 @@ __device__ __forceinline__ void epoch_body_pp_la(
             }
         };
         auto flush = [&]() {  // the float atomics of the previous bank's ratings
+            if constexpr (HX) {  // ... handed to the helper waves through the ring
+                constexpr int R = PPRing<T, G>::R;
+                for (int spins = 0; spins < kSpinMax; ++spins) {  // room for kB rows
+                    int m = lds_load(&ring->tail[0]);
 #pragma unroll
-            for (int d = 0; d < kB; ++d) {
-                T d1[U];
-                to_lane1<G>(dl[d], d1);
-#if defined(MF_EXP_ATOM_SPREAD)  // timing experiment only (wrong results): no two waves on a row
-                const uint32_t ao = (uint32_t)((wave * 131 + d) % n_items) * qrow;
-#else
-                const uint32_t ao = dlo[d];
-#endif
-#if defined(MF_EXP_GLOBAL_ATOM)  // timing experiment: global_atomic_add_f32 instead of buffer
-#pragma unroll
-                for (int uu = 0; uu < U; ++uu) {
-                    const uint32_t o = ao + cq1[uu];
-                    if (o < q_oob)
-                        __hip_atomic_fetch_add((T *)((char *)qb + o), d1[uu], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
+                    for (int h = 1; h < kHxHelpers; ++h) {
+                        const int th = lds_load(&ring->tail[h]);
+                        m = th < m ? th : m;
+                    }
+                    if (pushed + kB - m <= R) break;
+                    __builtin_amdgcn_s_sleep(1);
                 }
-#elif !defined(MF_EXP_NO_QATOM)
+                asm volatile("" ::: "memory");
 #pragma unroll
-                for (int uu = 0; uu < U; ++uu) atom_add1(q_rs, qb, q_oob, cq1[uu], ao, d1[uu]);
+                for (int d = 0; d < kB; ++d) {
+                    const int slot = (pushed + d) % R;
+#pragma unroll
+                    for (int v = 0; v < G; ++v) ring->data[slot][v][lane] = dl[d][v];
+                    ring->off[slot] = dlo[d];
+                }
+                pushed += kB;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows before the count
+                lds_store(&ring->head, pushed);
+            } else {
+#pragma unroll
+                for (int d = 0; d < kB; ++d) {
+                    T d1[U];
+                    to_lane1<G>(dl[d], d1);
+#if !defined(MF_EXP_NO_QATOM)
+#pragma unroll
+                    for (int uu = 0; uu < U; ++uu)
+                        atom_add1(q_rs, qb, q_oob, cq1[uu], dlo[d], d1[uu]);
 #endif
+                }
             }
         };
         {
@@ -1418,7 +1532,14 @@ __device__ __forceinline__ void epoch_body_pp_la(
         __builtin_amdgcn_s_setprio(0);
     };
 
-    for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w]);
+    for (int64_t w = wave; w < n_sched; w += n_waves) {
+        const int u = sched[w];
+        if (u >= 0) do_user(u);  // (HX schedules are padded with -1)
+    }
+    if constexpr (HX) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lds_store(&ring->done, 1);
+    }
 }
 
 #ifndef MF_LA
@@ -1439,8 +1560,9 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
 {
     if constexpr (MODE == kAtomic && PP && !DUPS && G <= kLaMaxG && MF_PP_LA) {
         if (elog) {  // deferred y (elog = ycbuf)
-            epoch_body_pp_la<T, G>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
-                                   yj, elog, K, hp, n_items, n_waves_req, xmask);
+            epoch_body_pp_la<T, G, false>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu,
+                                          qb, ldq, yj, elog, K, hp, n_items, n_waves_req, xmask,
+                                          nullptr);
             return;
         }
     }
@@ -1456,6 +1578,30 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
     }
 }
 
+// SVD++ with helper waves (MF_SVDPP_HELPERS): workgroup = chain wave 0 + kHxHelpers atomic waves
+template <typename T, int G>
+__global__ __launch_bounds__(kBlock) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS)
+{
+    __shared__ PPRing<T, G> ring;
+    const int w = threadIdx.x / kWave;
+    if (threadIdx.x == 0) {
+        ring.head = 0;
+        ring.done = 0;
+        for (int h = 0; h < kHxHelpers; ++h) ring.tail[h] = 0;
+    }
+    __syncthreads();
+    if (w == 0) {
+        epoch_body_pp_la<T, G, true>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
+                                     yj, elog, K, hp, n_items, n_waves_req, 0, &ring);
+        if (blockIdx.x >= n_waves_req) {  // (no chain in this workgroup)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lds_store(&ring.done, 1);
+        }
+    } else {
+        pp_ring_helper<T, G>(&ring, w - 1, qb, ldq, n_items);
+    }
+}
+
 }  // namespace
 
 #ifdef MF_TU_EPOCH
@@ -1464,7 +1610,7 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    void *stream)
+                    bool hx, void *stream)
 {
     // elog: SVD: the checkpoint log (the lookahead body: kLog, up to two lane groups);
     //       SVD++: the deferred y buffer (kAtomic)
@@ -1474,8 +1620,22 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     // popular item's c_u diverges: measured held-out RMSE 1.82 on ML-1M)
     if (elog && PP && M != kAtomic)
         return set_err(MF_E_UNSUPPORTED, "deferred y: MF_MODE_ATOMIC only");
+    if (hx && !(PP && M == kAtomic && elog && !dups))
+        return set_err(MF_E_UNSUPPORTED, "helper waves: SVD++, MF_MODE_ATOMIC, deferred y, no repeated items");
     return dispatch_g<T>(ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
+        if constexpr (PP && M == kAtomic && V <= kLaMaxG) {
+            if (hx) {  // one workgroup per chain: wave 0 trains, waves 1-3 issue the q atomics
+                hipLaunchKernelGGL((mf_svdpp_hx_kernel<T, V>), dim3(waves), dim3(kBlock), 0,
+                                   (hipStream_t)stream, csr->row_ptr, csr->items,
+                                   (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
+                                   (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
+                                   cast_hyper<T>(hp), csr->n_items, waves, 0);
+                return check_launch("mf_svdpp_hx_kernel");
+            }
+        } else {
+            if (hx) return set_err(MF_E_UNSUPPORTED, "helper waves: rows of <= 1 KiB");
+        }
         // (kLog reads a snapshot: a repeated item sees the chunk-start row, no forwarding)
         auto kern = (dups && M != kLog) ? mf_epoch_kernel<T, V, M, PP, true>
                                         : mf_epoch_kernel<T, V, M, PP, false>;
@@ -1489,7 +1649,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
 }
 template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
-    void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, void *);
+    void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, bool, void *);
 }  // namespace mf_ext
 #else  // the main translation unit
 
@@ -2849,6 +3009,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
                  int32_t dtype, void *stream)
 {
     const bool dups = flags & MF_EPOCH_DUP_ITEMS;
+    const bool hx = flags & MF_EPOCH_SVDPP_HELPERS;
     const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
     if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, qlog, dtype)) return rc;
     if (PP && !yj) return set_err(MF_E_ARG, "null yj");
@@ -2863,7 +3024,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         constexpr int M = decltype(mode_c)::value;
         return mf_ext::launch_epoch_tm<T, M, PP>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj,
                                                   qlog, elog, K, biased, hp, waves, dups, xmask,
-                                                  stream);
+                                                  hx, stream);
     };
     auto by_mode = [&](auto tag_t) -> int {
         switch (mode) {

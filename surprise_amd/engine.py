@@ -114,6 +114,28 @@ def split_heavy(users, row_ptr, heavy):
     return [users[~h], users[h]]
 
 
+def chain_schedule(users, row_ptr, n_chains, user_cost=16):
+    """The users laid out for n_chains user chains taking entries c, c + n_chains, ... (the
+    helper-wave SVD++ launch): longest-processing-time-first, each user (heaviest first) to the
+    chain with the least work so far (degree + user_cost per user), padded with -1."""
+    import heapq
+    users = np.asarray(users, np.int32)
+    deg = np.diff(np.asarray(row_ptr, np.int64))[users]
+    order = np.argsort(-deg, kind="stable")
+    n_chains = max(1, min(int(n_chains), len(users)))
+    lists = [[] for _ in range(n_chains)]
+    heap = [(0, c) for c in range(n_chains)]
+    for x in order:
+        load, c = heapq.heappop(heap)
+        lists[c].append(users[x])
+        heapq.heappush(heap, (load + int(deg[x]) + user_cost, c))
+    m = max(len(x) for x in lists) if lists else 0
+    out = np.full((m, n_chains), -1, np.int32)
+    for c, x in enumerate(lists):
+        out[:len(x), c] = x
+    return out.ravel()
+
+
 def ckpt_positions(row_ptr, perm, interval, pos_user=None):
     """Checkpoint position of every log position (mf_log_replay's ck_pos): for rating k of user
     u, k - ((k - row_ptr[u]) mod interval).  pos_user: position_users(row_ptr), if at hand."""
@@ -329,6 +351,20 @@ class MFEngine(ItemSync, Predictor):
         self.ydefer = (algo == "svdpp" and self.mode == _lib.MF_MODE_ATOMIC
                        and not self.deterministic
                        and os.environ.get("SURPRISE_AMD_YDEFER", "1") != "0")
+        # ... with helper waves (rows <= 1 KiB, no repeated items): one user chain per CU whose
+        # q atomics the workgroup's other three waves issue (mf_svdpp_epoch flag
+        # MF_EPOCH_SVDPP_HELPERS); the chains take users in a longest-first balanced layout
+        self.dup_items = int(_has_duplicate_items(row_ptr, items))
+        self.hx = (self.ydefer and self.ldq * esz <= 1024 and not self.dup_items
+                   and os.environ.get("SURPRISE_AMD_SVDPP_HX", "1") != "0")
+        self.hx_sched = []
+        if self.hx:
+            props = torch.cuda.get_device_properties(self.dev)
+            self.hx_chains = int(os.environ.get("SURPRISE_AMD_HX_PER_CU", "2")) * \
+                props.multi_processor_count
+            for us in self.sched:
+                self.hx_sched.append(to_dev(chain_schedule(us.cpu().numpy(), row_ptr,
+                                                           self.hx_chains)))
         self.ycsc = []
         if self.ydefer:
             for us in self.sched:
@@ -347,7 +383,6 @@ class MFEngine(ItemSync, Predictor):
         self._wt = 0
         self._work_cleared = True
         self.work = self._works[0]
-        self.dup_items = int(_has_duplicate_items(row_ptr, items))
 
         # ---- factor tables
         U, I, ld, ldq = self.n_users, self.n_items, self.ld, self.ldq
@@ -511,7 +546,11 @@ class MFEngine(ItemSync, Predictor):
             join = torch.cuda.Event()
             join.record(self.side)
         lx = (~self.heavy_xcd & 0xFF) if hv is not None and self.heavy_xcd else 0
-        self._epoch(s, s.numel(), self.n_waves, 0, st, lx)
+        if self.hx:
+            hs = self.hx_sched[c]
+            self._epoch(hs, hs.numel(), self.hx_chains, _lib.MF_EPOCH_SVDPP_HELPERS, st)
+        else:
+            self._epoch(s, s.numel(), self.n_waves, 0, st, lx)
         if "end" in ev:
             ev["end"].record(self.stream)
         if self.ydefer:

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 constexpr int kRowF = 128;  // floats per row (512 B)
 
@@ -18,7 +19,7 @@ __device__ __forceinline__ int xcc_id() {
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) void hammer(float *tab, int n_rows, int iters, uint32_t seed)
+__global__ __launch_bounds__(256) void hammer(float *tab, int n_rows, int iters, uint32_t seed, int skew)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -29,7 +30,12 @@ __global__ __launch_bounds__(256) void hammer(float *tab, int n_rows, int iters,
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
     for (int it = 0; it < iters; ++it) {
         s = s * 1664525u + 1013904223u;
-        const uint32_t row = __builtin_amdgcn_readfirstlane((s >> 8) % (uint32_t)n_rows);
+        uint32_t row = (s >> 8) % (uint32_t)n_rows;
+        if (skew) {  // popularity ~ power law: row = n * x^3, x uniform in [0, 1)
+            const float x = (float)(s >> 8) * (1.0f / 16777216.0f);
+            row = (uint32_t)((float)n_rows * x * x * x);
+        }
+        row = __builtin_amdgcn_readfirstlane(row);
         for (int h = 0; h < 2; ++h) {
             const int c = lane + 64 * h;
             if (MODE == 0)
@@ -45,8 +51,10 @@ __global__ __launch_bounds__(256) void hammer(float *tab, int n_rows, int iters,
     }
 }
 
-int main()
+int main(int argc, char **argv)
 {
+    const int skew = argc > 1 ? atoi(argv[1]) : 0;
+    printf("row distribution: %s\n", skew ? "skewed (n x^3)" : "uniform");
     const int n_rows = 3706, blocks = 256 * 4, iters = 2000;  // 4 blocks (16 waves) per CU
     float *tab;
     const size_t tab_f = (size_t)n_rows * kRowF;
@@ -60,10 +68,10 @@ int main()
             hipEventCreate(&a); hipEventCreate(&b);
             hipEventRecord(a, 0);
             switch (mode) {
-                case 0: hipLaunchKernelGGL(hammer<0>, dim3(blocks), dim3(256), 0, 0, tab, n_rows, iters, 7u); break;
-                case 1: hipLaunchKernelGGL(hammer<1>, dim3(blocks), dim3(256), 0, 0, tab, n_rows, iters, 7u); break;
-                case 2: hipLaunchKernelGGL(hammer<2>, dim3(blocks), dim3(256), 0, 0, tab, n_rows, iters, 7u); break;
-                default: hipLaunchKernelGGL(hammer<3>, dim3(blocks), dim3(256), 0, 0, tab, n_rows, iters, 7u); break;
+                case 0: hipLaunchKernelGGL(hammer<0>, dim3(blocks), dim3(256), 0, 0, tab, n_rows, iters, 7u, skew); break;
+                case 1: hipLaunchKernelGGL(hammer<1>, dim3(blocks), dim3(256), 0, 0, tab, n_rows, iters, 7u, skew); break;
+                case 2: hipLaunchKernelGGL(hammer<2>, dim3(blocks), dim3(256), 0, 0, tab, n_rows, iters, 7u, skew); break;
+                default: hipLaunchKernelGGL(hammer<3>, dim3(blocks), dim3(256), 0, 0, tab, n_rows, iters, 7u, skew); break;
             }
             hipEventRecord(b, 0);
             if (hipEventSynchronize(b) != hipSuccess) { printf("kernel failed\n"); return 1; }
