@@ -83,9 +83,10 @@ typedef struct mf_csr {
  *               bytes (|I_u| * ldq * sizeof(dtype)).  Other modes: NULL.
  *   elog      : NULL, or (MF_MODE_LOG, ldq * sizeof(dtype) <= 1 KiB) the checkpoint form of the
  *               log: device [nnz + mf_ckpt_interval()] errors, elog[k] = err_k, and qlog row k
- *               holds [p_u | 1 | 0..] before rating k only where k - row_ptr[u] is a multiple of
- *               mf_ckpt_interval() (other rows are not written); mf_log_replay rebuilds the
- *               gradients.  ~1/8 of the log bytes: the epoch kernel's memory traffic.
+ *               holds [p_u | 1 | 0..] AFTER rating k (= before rating k + 1; for a user's odd
+ *               last rating the final row) only where k - row_ptr[u] is even (other rows are
+ *               not written); mf_log_replay rebuilds the gradients.  Requires
+ *               1 - lr_pu * reg_pu != 0 (the replay undoes one step).  About half the log bytes.
  *   n_waves   : wavefronts to launch (<= 0: library default = fill the GPU);
  *               1 with MF_MODE_PLAIN gives the exact sequential reference order when
  *               sched = 0..n_users-1.
@@ -101,6 +102,11 @@ typedef struct mf_csr {
  * (n_waves = chains) whose q deltas go through an LDS ring to three waves that issue the float
  * atomics; sched entries < 0 are skipped (a schedule laid out per chain, strided by n_waves). */
 #define MF_EPOCH_SVDPP_HELPERS 2
+/* the same bit for mf_svd_epoch / mf_svd_epoch_sq with the checkpoint log (elog): two user chains
+ * per workgroup (n_waves = chains), whose checkpoint rows and errors go through LDS rings to two
+ * waves that issue the global stores (a chain's vector-memory counter then holds only its row
+ * gathers); sched entries < 0 are skipped. */
+#define MF_EPOCH_HELPERS 2
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
                  const mf_hyper_t *hp, int32_t mode, void *qlog, void *elog, int32_t n_waves,
@@ -150,10 +156,11 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
 /*
  * Delta-log merge, step 1 for the checkpoint form (mf_svd_epoch with elog): the same sums as
  * mf_log_reduce would give on the gradient log, sums[p][c] = sum over the piece's ratings k of
- * err_k * p_k[c] (c <= n_factors; 0 above), where p_k is rebuilt from the checkpoint row
- * c_k = ck_pos[x] <= k (x = the rating's index in perm; c_k = k - ((k - row_ptr[u]) mod
- * mf_ckpt_interval())) by the epoch kernel's recursion p <- ap * p + err_m * lr_pu * q_{item(m)}
- * (ap = 1 - lr_pu * reg_pu on factor columns) over the snapshot item rows qb -- call it before
+ * err_k * p_k[c] (c <= n_factors; 0 above), where p_k comes from the pair's checkpoint row
+ * c_k = ck_pos[x] (x = the rating's index in perm; c_k = k - ((k - row_ptr[u]) mod 2)), which
+ * holds p_{c_k + 1}: for k = c_k + 1 the row itself, for k = c_k the epoch kernel's step undone,
+ * p_k = (row - err_k * lr_pu * q_{item(k)}) / ap (ap = 1 - lr_pu * reg_pu on factor columns;
+ * q from the snapshot table qb; every rating of a piece has the same item) -- call it before
  * mf_log_apply.  Requires ldq * sizeof(dtype) <= 1 KiB.  flags: bits 8..15 an XCD mask as in
  * mf_svd_epoch (MF_EPOCH_XCD_SHIFT), 0 = every XCD.
  */
@@ -161,6 +168,26 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
                   const mf_csr_t *csr, const void *qb, const mf_hyper_t *hp, const int32_t *perm,
                   const int32_t *ck_pos, const int32_t *piece_beg, int64_t n_pieces, void *sums,
                   int32_t flags, int32_t dtype, void *stream);
+
+/*
+ * mf_svd_epoch in MF_MODE_LOG with the checkpoint log (elog != NULL, the lookahead body), also
+ * keeping user_sq current: user_sq[u] = sum_{c < n_factors} p_u[c]^2 (fp64) of every trained
+ * user's row after the epoch -- the <p^2> statistic of the log fold's count-aware weights
+ * without another pass over pu (mf_user_sq_reduce).  Same item-side results as mf_svd_epoch.
+ */
+int mf_svd_epoch_sq(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
+                    void *bu, int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
+                    const mf_hyper_t *hp, void *qlog, void *elog, double *user_sq,
+                    int32_t n_waves, int32_t flags, int32_t dtype, void *stream);
+
+/* user_sq[r] = sum_{c < n_cols} x[r * ld + c]^2 (fp64) for r < n_rows: initial user_sq. */
+int mf_user_sq(const void *pu, int64_t n_rows, int32_t n_cols, int32_t ld, double *user_sq,
+               int32_t dtype, void *stream);
+
+/* out[0] = sum of user_sq[0..n_rows) in a fixed order, out[1] = n_rows * n_cols: the {sum,
+ * count} pair mf_sumsq accumulates (here written, not added; bit-reproducible). */
+int mf_user_sq_reduce(const double *user_sq, int64_t n_rows, int32_t n_cols, double *out,
+                      void *stream);
 
 /* Checkpoint interval of the checkpoint log (ratings per stored user row). */
 int mf_ckpt_interval(void);
@@ -178,14 +205,18 @@ int mf_ckpt_interval(void);
  *   MF_MERGE_COUNT: w = (1 - (1-eta)^N) / (N eta), N = totals[i] (ratings of item i in the chunk,
  *                   all ranks), eta = lr_bi (1 + reg_bi) in bias_col and lr_qi (<p^2> + reg_qi)
  *                   in factor columns, <p^2> = p2stat[0] / p2stat[1] (mf_sumsq's two doubles).
- * stat_next (nullable, 2 device doubles, not p2stat): set to {0, 0} -- the next chunk's mf_sumsq
- * accumulator, cleared here instead of by a separate fill.
+ * stat_next (nullable, 2 device doubles, not p2stat): user_sq NULL: set to {0, 0} -- the next
+ * chunk's mf_sumsq accumulator, cleared here instead of by a separate fill; user_sq != NULL
+ * (mf_svd_epoch_sq's array, n_users rows): set to mf_user_sq_reduce's {sum, n_users * n_factors}
+ * -- the next chunk's <p^2>, summed inside this launch (every epoch kernel of the chunk must have
+ * finished before it).
  */
 int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
                  const void *sums, const int32_t *item_piece_ptr, const void *sums2,
                  const int32_t *item_piece_ptr2, const int32_t *totals, const mf_hyper_t *hp,
                  const double *p2stat, int32_t rule, void *delta_out, int32_t apply,
-                 double *stat_next, int32_t dtype, void *stream);
+                 double *stat_next, const double *user_sq, int64_t n_users, int32_t dtype,
+                 void *stream);
 
 /* Merge rules of mf_item_merge. */
 #define MF_MERGE_SUM   0 /* delta = sum_r d_r                                                      */

@@ -21,6 +21,7 @@ MF_MERGE_SUM, MF_MERGE_COUNT, MF_MERGE_MEAN = 0, 1, 2
 MF_EPOCH_DUP_ITEMS = 1
 MF_EPOCH_XCD_SHIFT = 8  # flags bits 8..15: XCD mask (include/surprise_amd.h)
 MF_EPOCH_SVDPP_HELPERS = 2
+MF_EPOCH_HELPERS = 2  # (the same bit: SVD checkpoint-log store waves)
 MAX_FACTORS = {MF_F32: 512, MF_F64: 256}
 
 
@@ -50,13 +51,17 @@ SIGNATURES = {
                        ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_svdpp_y_fold": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32,
                         _vp],
+    "mf_svd_epoch_sq": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32,
+                        _i32, ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_sumsq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
+    "mf_user_sq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
+    "mf_user_sq_reduce": [_vp, _i64, _i32, _vp, _vp],
     "mf_log_reduce": [_vp, _i32, _i32, _vp, _vp, _i64, _vp, _i32, _vp],
     "mf_log_replay": [_vp, _vp, _i32, _i32, ctypes.POINTER(MfCsr), _vp,
                       ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _i32, _i32, _vp],
     "mf_ckpt_interval": [],
     "mf_log_apply": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
-                     ctypes.POINTER(MfHyper), _vp, _i32, _vp, _i32, _vp, _i32, _vp],
+                     ctypes.POINTER(MfHyper), _vp, _i32, _vp, _i32, _vp, _vp, _i64, _i32, _vp],
     "mf_item_merge": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
                       ctypes.POINTER(MfHyper), _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp],
     "mf_item_apply": [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp],

@@ -38,7 +38,7 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    bool hx, void *stream);
+                    bool hx, double *psq, void *stream);
 }  // namespace mf_ext
 
 namespace {
@@ -793,10 +793,9 @@ __device__ __forceinline__ void epoch_body(
     for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w]);
 }
 
-#ifndef MF_CKPT
-#define MF_CKPT 2  // checkpoint interval of the SVD log (elog != NULL): a user row per 2 ratings
-#endif
-constexpr int kCkpt = MF_CKPT;
+// checkpoint interval of the SVD log (elog != NULL): one user row per pair of ratings (the
+// replay's inverse step needs exactly 2)
+constexpr int kCkpt = 2;
 #ifndef MF_LA_MAX_G
 #define MF_LA_MAX_G 2  // lookahead body / checkpoint log for rows of up to 2 lane groups (1 KiB)
 #endif
@@ -849,6 +848,108 @@ __device__ __forceinline__ void wave_sum2_u(T x, T y, T &sx, T &sy) {
     sy = readlane(z, 63);
 }
 
+// ---- checkpoint-log stores through LDS (MF_EPOCH_SVD_HELPERS): a wave's vmcnt counts its loads
+// AND its stores in one in-order counter (gfx9), so a chain wave that stores its checkpoint rows
+// waits, at a later row gather, for stores that the memory system keeps pending for thousands of
+// cycles under load (measured: the heaviest ML-1M chain 136 us with its stores, 112 us without).
+// With helpers a workgroup holds two chain waves (0, 1) and two helper waves (2, 3): chain c puts
+// each bank's checkpoint rows and errors into its LDS ring (ds writes count in lgkmcnt, not
+// vmcnt) and helper 2 + c issues the global stores.
+#ifndef MF_CK_RING
+#define MF_CK_RING 4  // banks per ring
+#endif
+constexpr int kCkSpinMax = 1 << 22;  // bounded spins (s_sleep each): never hang the GPU
+
+template <typename T, int G, int kLg>
+struct CkRing {
+    static constexpr int E = MF_CK_RING;
+    typename Lane8<T>::vec rows[E][kLg][G][kWave];
+    T err[E][kWave];
+    int64_t base[E];  // the user's first CSR position
+    int n[E], j0[E];  // the user's rating count, the bank's first rating
+    int head, done, tail;
+};
+
+__device__ __forceinline__ int lds_ld(int *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// helper wave of one chain: the global stores of every bank the chain pushes, until it is done
+template <typename T, int G, int kLg>
+__device__ void ck_ring_helper(CkRing<T, G, kLg> *ring, T *qlog, T *elog, int ldq, int kB)
+{
+    using L = Lane8<T>;
+    constexpr int W = L::W;
+    constexpr int E = CkRing<T, G, kLg>::E;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t qrow = (uint32_t)ldq * sizeof(T);
+    uint32_t cl[G];
+#pragma unroll
+    for (int v = 0; v < G; ++v) {
+        const int c0 = (lane + kWave * v) * W;
+        cl[v] = c0 < ldq ? (uint32_t)c0 * sizeof(T) : kLogOob;
+    }
+    int t = 0, spins = 0;
+    while (true) {
+        int hd = lds_ld(&ring->head);
+        if (t >= hd) {
+            if (lds_ld(&ring->done)) {
+                asm volatile("" ::: "memory");
+                hd = lds_ld(&ring->head);
+                if (t >= hd) break;
+            } else {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kCkSpinMax) break;
+                continue;
+            }
+        }
+        spins = 0;
+        asm volatile("" ::: "memory");
+        for (; t < hd; ++t) {
+            const int e = t % E;
+            const int64_t s = __builtin_amdgcn_readfirstlane((int)(ring->base[e] & 0xffffffff)) |
+                              ((int64_t)__builtin_amdgcn_readfirstlane((int)(ring->base[e] >> 32)) << 32);
+            const int n = __builtin_amdgcn_readfirstlane(ring->n[e]);
+            const int j0 = __builtin_amdgcn_readfirstlane(ring->j0[e]);
+            const rsrc_t l_rs = make_rsrc(qlog + s * ldq, (uint32_t)n * qrow);
+            const rsrc_t e_rs = make_rsrc(elog + s, (uint32_t)n * sizeof(T));
+            typename L::vec r[kLg][G];
+#pragma unroll
+            for (int x = 0; x < kLg; ++x)
+#pragma unroll
+                for (int v = 0; v < G; ++v) r[x][v] = ring->rows[e][x][v][lane];
+            const T ev = ring->err[e][lane];
+#pragma unroll
+            for (int x = 0; x < kLg; ++x)
+#pragma unroll
+                for (int v = 0; v < G; ++v)
+                    L::template sts<0>(l_rs, cl[v], (uint32_t)(j0 + x * kCkpt) * qrow, r[x][v]);
+            Buf<T>::template st<0>(e_rs, lane < kB ? (uint32_t)(j0 + lane) * sizeof(T) : kLogOob, ev);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the entries' reads have returned
+        lds_st(&ring->tail, t);
+    }
+}
+
+// chain slot of wave 0 / 1 of a helper-wave launch (two chains per block) on the XCDs of xmask
+__device__ __forceinline__ bool chain_slot(int xmask, int64_t &slot, int64_t &n_slots) {
+    const int64_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    if (!xmask) {
+        slot = (int64_t)blockIdx.x * 2 + w;
+        n_slots = (int64_t)gridDim.x * 2;
+        return true;
+    }
+    const int x = __builtin_amdgcn_readfirstlane(xcc_id());
+    if (!((xmask >> x) & 1)) return false;
+    const int c = __builtin_popcount(xmask), rank = __builtin_popcount(xmask & ((1 << x) - 1));
+    slot = ((int64_t)(blockIdx.x >> 3) * c + rank) * 2 + w;
+    n_slots = (int64_t)(gridDim.x >> 3) * c * 2;
+    return true;
+}
+
 // ---- SVD rating loop in lookahead form (kLog, SVD, G = 1: K <= 127 fp32 / K <= 63 fp64)
 //
 // Per user, with q_k = the snapshot row [q | b] of rating k and p_k's column K the constant 1:
@@ -863,24 +964,34 @@ __device__ __forceinline__ void wave_sum2_u(T x, T y, T &sx, T &sy) {
 // (columns 0..K; mf_log_apply turns the sums into the item steps).  Same arithmetic as the
 // reference recursion up to rounding (fp64: equal to the delta-log oracle to 1e-9,
 // tests/test_gpu_parity.py).
-template <typename T, int G, bool CK>
+template <typename T, int G>
+constexpr int la_bank() { return G == 1 ? MF_LA_BANK : MF_LA_BANK_G2; }
+
+template <typename T, int G, bool CK, bool HX = false>
 __device__ __forceinline__ void epoch_body_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *qlog, T *elog, int K,
-    int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask)
+    int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, double *psq,
+    CkRing<T, G, la_bank<T, G>() / kCkpt> *ring = nullptr)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
     constexpr int W = L::W;
     // ratings per bank of gathered rows (a power of 2 <= 64)
-    constexpr int kB = G == 1 ? MF_LA_BANK : MF_LA_BANK_G2;
+    constexpr int kB = la_bank<T, G>();
     static_assert(!CK || (kB % kCkpt == 0 && kB <= kWave), "checkpoints: whole banks");
+    static_assert(!HX || CK, "helper stores: checkpoint log only");
     const int lane = threadIdx.x & (kWave - 1);
     int64_t wave, grid_waves;
-    if (!wave_slot(xmask, wave, grid_waves)) return;
+    if (HX) {  // (the caller checked the XCD mask)
+        chain_slot(xmask, wave, grid_waves);
+    } else if (!wave_slot(xmask, wave, grid_waves)) {
+        return;
+    }
     const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
     if (wave >= n_waves) return;
+    int pushed = 0;  // HX: banks pushed to the ring
 
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), prow = (uint32_t)ldu * sizeof(T);
     const uint32_t q_oob = (uint32_t)n_items * qrow;
@@ -942,8 +1053,9 @@ __device__ __forceinline__ void epoch_body_la(
         };
         vec bank[2][kB][G];
         T br[2][kB];
-        // log rows of the current bank: CK: the checkpoints p_k (k = 0 mod kCkpt) and err_k in
-        // lane k mod kB of ev; otherwise every rating's gradient row g_k = err_k p_k
+        // log rows of the current bank: CK: per pair (c, c + 1) of the user's ratings (c even) the
+        // row p_{c+1} at log row c, and err_k in lane k mod kB of ev; otherwise every rating's
+        // gradient row g_k = err_k p_k
         constexpr int kLg = CK ? kB / kCkpt : kB;
         vec lg[kLg][G];
         T ev = T(0);
@@ -962,7 +1074,29 @@ __device__ __forceinline__ void epoch_body_la(
 #if defined(MF_EXP_LA_NO_STORE)  // timing experiment only: no log written (wrong results)
             return;
 #endif
-            if constexpr (CK) {
+            if constexpr (HX) {  // to the LDS ring; the helper wave stores
+                constexpr int E = CkRing<T, G, kLg>::E;
+                for (int spins = 0; spins < kCkSpinMax; ++spins) {
+                    if (pushed - lds_ld(&ring->tail) < E) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                asm volatile("" ::: "memory");
+                const int e = pushed % E;
+#pragma unroll
+                for (int x = 0; x < kLg; ++x)
+#pragma unroll
+                    for (int v = 0; v < G; ++v) ring->rows[e][x][v][lane] = lg[x][v];
+                ring->err[e][lane] = ev;
+                if (lane == 0) {
+                    ring->base[e] = s;
+                    ring->n[e] = n;
+                    ring->j0[e] = j0p;
+                }
+                ++pushed;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the entry before the count
+                lds_st(&ring->head, pushed);
+                return;
+            } else if constexpr (CK) {
 #pragma unroll
                 for (int x = 0; x < kLg; ++x)
 #pragma unroll
@@ -1042,7 +1176,9 @@ __device__ __forceinline__ void epoch_body_la(
                 px += qn[v] * A[v];
                 py += qn[v] * D[v];
                 if (!CK) lg[d][v] = err * pk[v];  // the log row g_k = err_k p_k (old p, mf.pyx:261)
-                else if (d % kCkpt == 0) lg[d / kCkpt][v] = pk[v];  // checkpoint p_k
+                // checkpoint of the pair (c, c + 1), c = k - 1 even: p_{c+1}, the row after
+                // rating c (k = n: the user's final row, for odd n -- the masked tail step)
+                else if (d % kCkpt == 1) lg[d / kCkpt][v] = pk[v];
             }
             if (CK) ev = lane == d ? err : ev;
             T Xn, Yn;
@@ -1115,14 +1251,30 @@ __device__ __forceinline__ void epoch_body_la(
             tail_bank(B0{});
         }
         // after rating n-1: p_n = A_{n-1} + err_{n-1} D_{n-1}, c_n = lr_bu err_{n-1} + c0_{n-1}
+        double sq = 0;  // psq: sum of p_n^2 over the factor columns (the log fold's <p^2>)
 #pragma unroll
-        for (int v = 0; v < G; ++v) L::template st<0>(p_rs, cu[v], A_p[v] + err_p * D_p[v]);
+        for (int v = 0; v < G; ++v) {
+            const vec pn = A_p[v] + err_p * D_p[v];
+            L::template st<0>(p_rs, cu[v], pn);
+#pragma unroll
+            for (int e = 0; e < W; ++e) {
+                const double x = (double)L::get(pn, e);
+                sq += (lane + kWave * v) * W + e < K ? x * x : 0.0;
+            }
+        }
+        if (psq) {
+            sq = wave_sum(sq);
+            if (lane == 0) psq[u] = sq;
+        }
         const T bu_u = lr_bu * err_p + c0_p - hp.gm;
         Buf<T>::template st<0>(b_rs, lane == 0 ? 0u : (uint32_t)sizeof(T), bu_u);
         __builtin_amdgcn_s_setprio(0);
     };
 
-    for (int64_t w = wave; w < n_sched; w += n_waves) do_user(sched[w]);
+    for (int64_t w = wave; w < n_sched; w += n_waves) {
+        const int u = sched[w];
+        if (u >= 0) do_user(u);  // (chain schedules are padded with -1)
+    }
 }
 
 #ifndef MF_PP_LA
@@ -1550,7 +1702,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,                      \
         const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,       \
         T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, T *elog,\
-        int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask
+        int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, double *psq
 #define MF_EPOCH_ARGS \
     row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, elog, K, biased, hp,    \
         n_items, n_waves_req, xmask
@@ -1569,12 +1721,39 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
     if constexpr (MODE == kLog && !PP && G <= kLaMaxG && MF_LA) {
         if (elog)
             epoch_body_la<T, G, true>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
-                                      qlog, elog, K, biased, hp, n_items, n_waves_req, xmask);
+                                      qlog, elog, K, biased, hp, n_items, n_waves_req, xmask, psq);
         else
             epoch_body_la<T, G, false>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb,
-                                       ldq, qlog, elog, K, biased, hp, n_items, n_waves_req, xmask);
+                                       ldq, qlog, elog, K, biased, hp, n_items, n_waves_req, xmask,
+                                       psq);
     } else {
         epoch_body<T, G, MODE, PP, DUPS, kPF>(MF_EPOCH_ARGS);
+    }
+}
+
+// SVD checkpoint log with helper waves (MF_EPOCH_HELPERS): workgroup = chain waves 0, 1 + their
+// store waves 2, 3 (ck_ring_helper)
+template <typename T, int G>
+__global__ __launch_bounds__(kBlock) void mf_svd_hx_kernel(MF_EPOCH_PARAMS)
+{
+    constexpr int kLg = la_bank<T, G>() / kCkpt;
+    __shared__ CkRing<T, G, kLg> rings[2];
+    if (xmask) {  // (the whole block leaves an XCD outside the mask)
+        const int x = __builtin_amdgcn_readfirstlane(xcc_id());
+        if (!((xmask >> x) & 1)) return;
+    }
+    const int w = threadIdx.x / kWave;
+    if (threadIdx.x == 0)
+        for (int c = 0; c < 2; ++c) rings[c].head = rings[c].done = rings[c].tail = 0;
+    __syncthreads();
+    if (w < 2) {
+        epoch_body_la<T, G, true, true>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb,
+                                        ldq, qlog, elog, K, biased, hp, n_items, n_waves_req, xmask,
+                                        psq, &rings[w]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lds_st(&rings[w].done, 1);
+    } else {
+        ck_ring_helper<T, G, kLg>(&rings[w - 2], qlog, elog, ldq, la_bank<T, G>());
     }
 }
 
@@ -1610,8 +1789,10 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    bool hx, void *stream)
+                    bool hx, double *psq, void *stream)
 {
+    if (psq && (PP || M != kLog || !elog))
+        return set_err(MF_E_UNSUPPORTED, "user_sq: the SVD checkpoint-log epoch only");
     // elog: SVD: the checkpoint log (the lookahead body: kLog, up to two lane groups);
     //       SVD++: the deferred y buffer (kAtomic)
     if (elog && !PP && (M != kLog || !MF_LA || (int64_t)ldq * sizeof(T) > 512 * kLaMaxG))
@@ -1620,8 +1801,9 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     // popular item's c_u diverges: measured held-out RMSE 1.82 on ML-1M)
     if (elog && PP && M != kAtomic)
         return set_err(MF_E_UNSUPPORTED, "deferred y: MF_MODE_ATOMIC only");
-    if (hx && !(PP && M == kAtomic && elog && !dups))
-        return set_err(MF_E_UNSUPPORTED, "helper waves: SVD++, MF_MODE_ATOMIC, deferred y, no repeated items");
+    if (hx && !(PP && M == kAtomic && elog && !dups) && !(!PP && M == kLog && elog))
+        return set_err(MF_E_UNSUPPORTED, "helper waves: SVD++ (MF_MODE_ATOMIC, deferred y, no repeated "
+                                         "items) or the SVD checkpoint log");
     return dispatch_g<T>(ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         if constexpr (PP && M == kAtomic && V <= kLaMaxG) {
@@ -1630,8 +1812,22 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
                                    (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
-                                   cast_hyper<T>(hp), csr->n_items, waves, 0);
+                                   cast_hyper<T>(hp), csr->n_items, waves, 0, nullptr);
                 return check_launch("mf_svdpp_hx_kernel");
+            }
+        } else if constexpr (!PP && M == kLog && V <= kLaMaxG && MF_LA) {
+            if (hx) {  // two chains per workgroup, each with a store wave
+                int64_t blocks = (waves + 1) / 2;
+                if (xmask) {
+                    const int c = __builtin_popcount(xmask & 0xFF);
+                    blocks = 8 * ((blocks + c - 1) / c);
+                }
+                hipLaunchKernelGGL((mf_svd_hx_kernel<T, V>), dim3(blocks), dim3(kBlock), 0,
+                                   (hipStream_t)stream, csr->row_ptr, csr->items,
+                                   (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
+                                   (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
+                                   cast_hyper<T>(hp), csr->n_items, waves, xmask, psq);
+                return check_launch("mf_svd_hx_kernel");
             }
         } else {
             if (hx) return set_err(MF_E_UNSUPPORTED, "helper waves: rows of <= 1 KiB");
@@ -1643,13 +1839,14 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                            (hipStream_t)stream,
                            csr->row_ptr, csr->items, (const T *)csr->ratings, sched, n_sched,
                            (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K,
-                           biased, cast_hyper<T>(hp), csr->n_items, waves, xmask);
+                           biased, cast_hyper<T>(hp), csr->n_items, waves, xmask, psq);
         return check_launch(PP ? "mf_epoch_kernel<svdpp>" : "mf_epoch_kernel<svd>");
     });
 }
 template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
-    void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, bool, void *);
+    void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, bool, double *,
+    void *);
 }  // namespace mf_ext
 #else  // the main translation unit
 
@@ -1703,6 +1900,63 @@ __global__ __launch_bounds__(kBlock) void sumsq_kernel(const T *__restrict__ x, 
         atomicAdd(out, t);
         if (blockIdx.x == 0) atomicAdd(out + 1, (double)n_rows * K);  // {sum, count}
     }
+}
+
+// out = {sum of sq[0..n) in a fixed order, n * K}, by one whole workgroup: per-thread strided sums
+// (8 loads in flight), then a fixed tree in LDS
+__device__ __forceinline__ void block_sum_sq(const double *__restrict__ sq, int64_t n, int K,
+                                             double *out)
+{
+    __shared__ double part[kBlock];
+    double acc = 0;
+    constexpr int kU = 8;
+    for (int64_t i0 = threadIdx.x; i0 < n; i0 += (int64_t)kU * kBlock) {
+        double v[kU];
+#pragma unroll
+        for (int a = 0; a < kU; ++a) {
+            const int64_t i = i0 + (int64_t)a * kBlock;
+            v[a] = i < n ? sq[i] : 0.0;
+        }
+#pragma unroll
+        for (int a = 0; a < kU; ++a) acc += v[a];
+    }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = kBlock / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) part[threadIdx.x] += part[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = part[0];
+        out[1] = (double)n * K;
+    }
+}
+
+// Per-user sum of squares of the factor columns (fp64), one wave per row: the initial values of
+// the user_sq array that the checkpoint-log epoch (mf_svd_epoch_sq) keeps current.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void user_sq_kernel(const T *__restrict__ x, int64_t n_rows,
+                                                         int K, int ld, double *__restrict__ out)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    for (int64_t r = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave; r < n_rows; r += n_waves) {
+        double acc = 0;
+        for (int c = lane; c < K; c += kWave) {
+            const double v = (double)x[r * ld + c];
+            acc += v * v;
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) out[r] = acc;
+    }
+}
+
+// {sum of user_sq[0..n), n * K} in a fixed order (one block: strided per-thread sums, then a
+// fixed tree): the <p^2> statistic of the log fold, bit-reproducible
+__global__ __launch_bounds__(kBlock) void user_sq_reduce_kernel(const double *__restrict__ sq,
+                                                                int64_t n, int K, double *out)
+{
+    block_sum_sq(sq, n, K, out);
 }
 
 template <typename T>
@@ -1847,10 +2101,7 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
 #define MF_EPOCH_WPC 64  // epoch kernel: default cap on waves per CU
 #endif
 #ifndef MF_REPLAY_U
-#define MF_REPLAY_U 8  // ratings per replay group
-#endif
-#ifndef MF_REPLAY_NT
-#define MF_REPLAY_NT 0  // 1: checkpoint rows read non-temporally (measured slower)
+#define MF_REPLAY_U 16  // ratings per replay group (two groups in flight)
 #endif
 #ifndef MF_REPLAY_WPC
 #define MF_REPLAY_WPC 16  // replay waves per CU
@@ -1858,28 +2109,32 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
 
 // ---------------------------------------------------------------- checkpoint-log replay
 //
-// The SVD log in checkpoint form (mf_svd_epoch with elog != NULL): per user, the row p_c before
-// the rating at every segment position c = 0 mod kCkpt (qlog row c, CSR position) and err_k of
-// every rating (elog[k]).  The gradient of rating k, g_k = err_k p_k, is rebuilt here by
-// replaying the user recursion p_{m+1} = ap o p_m + err_m (lrp o q_{i_m}) from its checkpoint
-// (k - c < kCkpt steps) over the SNAPSHOT item rows -- the operations of the epoch kernel's
-// lookahead body, in its order -- and summed per piece exactly like log_reduce_kernel.  The
-// epoch then writes ~(ldq * size / kCkpt + size) bytes per rating instead of a whole row.
-// One wave per piece (<= 64 ratings of one item): lane x holds rating x's position, checkpoint,
-// step count, and the item-row offsets / errs of its replayed positions (vector gathers once per
-// piece); per rating only v_readlane broadcasts, the row gathers and packed FMAs remain.
+// The SVD log in checkpoint form (mf_svd_epoch with elog != NULL): per pair (c, c + 1) of a
+// user's ratings (c - row_ptr[u] even) log row c holds p_{c+1}, the user row AFTER rating c
+// (for a user's odd last rating c: the final row), and elog[k] = err_k for every rating.  The
+// gradient of rating k is g_k = err_k p_k (p_k = the row before rating k):
+//   k = c + 1:  p_k = row c, as stored;
+//   k = c:      p_k = (p_{c+1} - err_c lrp o q_{i_c}) / ap  -- the epoch kernel's step
+//               p_{c+1} = ap o p_c + err_c lrp o q_{i_c} undone (ap = 1 - lr_pu reg_pu on factor
+//               columns, 1 elsewhere; lrp = lr_pu on factor columns, 0 elsewhere).
+// A piece holds ratings of ONE item, so q_{i_c} is the piece's own (snapshot) item row: one
+// load per piece, and the replay gathers nothing but the checkpoint rows (no item rows, no item
+// ids).  Summed per piece in perm order exactly like log_reduce_kernel; equal to the gradient
+// log's sums up to a rounding of the undone step (fp64: the delta-log oracle to 1e-9).
+// One wave per piece (<= 64 ratings): lane x holds rating x's checkpoint offset, parity and
+// err (vector gathers once per piece); per rating v_readlane broadcasts, the row gather and 3
+// packed FMAs.  Two groups of MF_REPLAY_U rows are in flight per wave.
 template <typename T, int G>
 __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     const T *__restrict__ ckpt, const T *__restrict__ elog, int ldq, int K,
-    const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T reg_pu,
+    const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T inv_ap,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
     const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int xmask)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
     constexpr int W = L::W;
-    constexpr int kR = kCkpt - 1;    // replay steps at most
-    constexpr int kU = MF_REPLAY_U;  // ratings per group; two groups in flight
+    constexpr int kU = MF_REPLAY_U;
     const int lane = threadIdx.x & (kWave - 1);
     int64_t wave, n_waves;
     if (!wave_slot(xmask, wave, n_waves)) return;
@@ -1887,7 +2142,7 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     const rsrc_t q_rs = make_rsrc(qb, q_oob);
     uint32_t cq[G];
     int cc[G];
-    vec lrp[G], ap[G];
+    vec lrp[G], iap[G];
 #pragma unroll
     for (int v = 0; v < G; ++v) {
         const int c0 = (lane + kWave * v) * W;
@@ -1897,79 +2152,53 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
         for (int e = 0; e < W; ++e) {
             const bool fac = c0 + e < K;
             L::set(lrp[v], e, fac ? lr_pu : T(0));
-            L::set(ap[v], e, fac ? T(1) - lr_pu * reg_pu : T(1));
+            L::set(iap[v], e, fac ? inv_ap : T(1));
         }
     }
     for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
         const int beg = piece_beg[pc], cnt = piece_beg[pc + 1] - beg;  // 1 <= cnt <= 64
         const int xl = beg + (lane < cnt ? lane : cnt - 1);
-        const int k_l = perm[xl], c_l = ck_pos[xl];  // lane x: rating x and its checkpoint
-        const int r_l = k_l - c_l;                    // steps from the checkpoint (< kCkpt)
+        const int k_l = perm[xl], c_l = ck_pos[xl];  // lane x: rating x and its pair's row
+        const int odd_l = k_l - c_l;                  // 1: k = c + 1 (the row as stored)
         const T ek_l = lane < cnt ? elog[k_l] : T(0);  // lanes >= cnt: weight 0
-        uint32_t qo_l[kR];  // q_oob for steps the rating does not take (load 0, no traffic)
-        T e_l[kR];
+        // the piece's item row (snapshot) -> D = lrp o q_i
+        const uint32_t qoff = (uint32_t)items[readlane(k_l, 0)] * qrow;
+        vec D[G];
 #pragma unroll
-        for (int m = 0; m < kR; ++m) {
-            const int pm = m < r_l ? c_l + m : k_l;
-            qo_l[m] = m < r_l ? (uint32_t)items[pm] * qrow : q_oob;
-            e_l[m] = elog[pm];
-        }
+        for (int v = 0; v < G; ++v) D[v] = lrp[v] * L::template lds<0>(q_rs, cq[v], qoff);
         vec acc[G];
 #pragma unroll
         for (int v = 0; v < G; ++v) acc[v] = L::splat(T(0));
-        // every load unconditional (masked rows read 0): the waits stay counted, so one group's
-        // rows arrive while the other group computes
-        auto load_grp = [&](const int x0, vec (&p)[kU][G], vec (&q)[kU][kR][G]) {
+        auto load_grp = [&](const int x0, vec (&p)[kU][G]) {
 #pragma unroll
             for (int y = 0; y < kU; ++y) {  // (x past cnt: lane cnt-1's rating, weight 0)
                 const int x = x0 + y < kWave ? x0 + y : kWave - 1;
                 const T *row = ckpt + (int64_t)readlane(c_l, x) * ldq;
-#if defined(MF_REPLAY_CK_AUX)  // timing experiment: checkpoint rows with a cache policy
-                const rsrc_t ck_rs = make_rsrc(row, qrow);
 #pragma unroll
-                for (int v = 0; v < G; ++v) p[y][v] = L::template ld<MF_REPLAY_CK_AUX>(ck_rs, cq[v]);
-#else
-#pragma unroll
-                for (int v = 0; v < G; ++v)  // (non-temporal: keep L2 for the item rows)
-                    p[y][v] = MF_REPLAY_NT ? __builtin_nontemporal_load((const vec *)(row + cc[v]))
-                                           : *(const vec *)(row + cc[v]);
-#endif
-#pragma unroll
-                for (int m = 0; m < kR; ++m) {
-                    const uint32_t off = readlane((int)qo_l[m], x);
-#pragma unroll
-                    for (int v = 0; v < G; ++v) q[y][m][v] = L::template lds<0>(q_rs, cq[v], off);
-                }
+                for (int v = 0; v < G; ++v) p[y][v] = *(const vec *)(row + cc[v]);
             }
         };
-        auto comp_grp = [&](const int x0, vec (&p)[kU][G], vec (&q)[kU][kR][G]) {
+        auto comp_grp = [&](const int x0, vec (&p)[kU][G]) {
 #pragma unroll
             for (int y = 0; y < kU; ++y) {
                 const int x = x0 + y < kWave ? x0 + y : kWave - 1;
-                const int r = readlane(r_l, x);
-#pragma unroll
-                for (int m = 0; m < kR; ++m) {
-                    const T e = readlane(e_l[m], x);
-#pragma unroll
-                    for (int v = 0; v < G; ++v) {  // the epoch kernel's p_{m+1} = A_m + err_m D_m
-                        const vec A = ap[v] * p[y][v], D = lrp[v] * q[y][m][v];
-                        const vec pn = A + e * D;
-                        p[y][v] = m < r ? pn : p[y][v];
-                    }
-                }
+                const int odd = readlane(odd_l, x);
                 const T ek = readlane(ek_l, x);
 #pragma unroll
-                for (int v = 0; v < G; ++v) acc[v] += ek * p[y][v];  // g_k = err_k p_k, in order
+                for (int v = 0; v < G; ++v) {
+                    const vec pc_ = iap[v] * (p[y][v] - ek * D[v]);  // p_c from p_{c+1}
+                    acc[v] += ek * (odd ? p[y][v] : pc_);           // g_k = err_k p_k, in order
+                }
             }
         };
-        vec pA[kU][G], qA[kU][kR][G], pB[kU][G], qB[kU][kR][G];
-        load_grp(0, pA, qA);
+        vec pA[kU][G], pB[kU][G];
+        load_grp(0, pA);
         for (int x0 = 0; x0 < cnt; x0 += 2 * kU) {
-            load_grp(x0 + kU, pB, qB);
-            comp_grp(x0, pA, qA);
+            load_grp(x0 + kU, pB);
+            comp_grp(x0, pA);
             if (x0 + kU >= cnt) break;
-            load_grp(x0 + 2 * kU, pA, qA);
-            comp_grp(x0 + kU, pB, qB);
+            load_grp(x0 + 2 * kU, pA);
+            comp_grp(x0 + kU, pB);
         }
 #pragma unroll
         for (int v = 0; v < G; ++v) {
@@ -1988,9 +2217,16 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     const int32_t *__restrict__ item_piece_ptr2, const int32_t *__restrict__ totals,
     int count_rule, double eta_bias, double lr_fac, double reg_fac, double lr_f, double reg_f,
     double lr_b, double reg_b, const double *__restrict__ p2stat, T *__restrict__ delta_out,
-    int apply, double *__restrict__ stat_next)
+    int apply, double *__restrict__ stat_next, const double *__restrict__ user_sq, int64_t n_sq,
+    int sq_cols)
 {
-    if (stat_next && blockIdx.x == 0 && threadIdx.x < 2) stat_next[threadIdx.x] = 0.0;
+    if (stat_next && blockIdx.x == 0) {
+        if (user_sq) {  // the next chunk's {sum |p_u|^2, count} (every epoch kernel has finished)
+            block_sum_sq(user_sq, n_sq, sq_cols, stat_next);
+        } else if (threadIdx.x < 2) {
+            stat_next[threadIdx.x] = 0.0;  // (cleared for the next chunk's mf_sumsq)
+        }
+    }
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -3006,7 +3242,7 @@ template <bool PP>
 int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                  int32_t biased, const mf_hyper_t *hp, int32_t mode, int32_t n_waves, int32_t flags,
-                 int32_t dtype, void *stream)
+                 int32_t dtype, void *stream, double *psq = nullptr)
 {
     const bool dups = flags & MF_EPOCH_DUP_ITEMS;
     const bool hx = flags & MF_EPOCH_SVDPP_HELPERS;
@@ -3024,7 +3260,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         constexpr int M = decltype(mode_c)::value;
         return mf_ext::launch_epoch_tm<T, M, PP>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj,
                                                   qlog, elog, K, biased, hp, waves, dups, xmask,
-                                                  hx, stream);
+                                                  hx, psq, stream);
     };
     auto by_mode = [&](auto tag_t) -> int {
         switch (mode) {
@@ -3047,7 +3283,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 900; }
+int mf_version(void) { return 910; }
 
 #ifndef MF_SOURCE_HASH
 #define MF_SOURCE_HASH "unknown"
@@ -3067,6 +3303,17 @@ int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
     if (elog && mode != MF_MODE_LOG) return set_err(MF_E_ARG, "elog needs MF_MODE_LOG");
     return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, nullptr, qlog, elog,
                                n_factors, biased, hp, mode, n_waves, flags, dtype, stream);
+}
+
+int mf_svd_epoch_sq(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
+                    void *bu, int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
+                    const mf_hyper_t *hp, void *qlog, void *elog, double *user_sq,
+                    int32_t n_waves, int32_t flags, int32_t dtype, void *stream)
+{
+    if (!elog || !user_sq) return set_err(MF_E_ARG, "mf_svd_epoch_sq needs elog and user_sq");
+    return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, nullptr, qlog, elog,
+                               n_factors, biased, hp, MF_MODE_LOG, n_waves, flags, dtype, stream,
+                               user_sq);
 }
 
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
@@ -3097,6 +3344,35 @@ int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *
     else
         return set_err(MF_E_ARG, "bad dtype");
     return check_launch("sumsq_kernel");
+}
+
+int mf_user_sq(const void *pu, int64_t n_rows, int32_t n_cols, int32_t ld, double *user_sq,
+               int32_t dtype, void *stream)
+{
+    if (!user_sq || n_rows < 0 || n_cols < 0 || ld < n_cols) return set_err(MF_E_ARG, "bad argument");
+    if (n_rows == 0) return 0;
+    if (!pu) return set_err(MF_E_ARG, "null pu");
+    const int g = grid_for_waves(n_rows < 4096 ? n_rows : 4096);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MF_F32)
+        hipLaunchKernelGGL(user_sq_kernel<float>, dim3(g), dim3(kBlock), 0, st, (const float *)pu,
+                           n_rows, n_cols, ld, user_sq);
+    else if (dtype == MF_F64)
+        hipLaunchKernelGGL(user_sq_kernel<double>, dim3(g), dim3(kBlock), 0, st, (const double *)pu,
+                           n_rows, n_cols, ld, user_sq);
+    else
+        return set_err(MF_E_ARG, "bad dtype");
+    return check_launch("user_sq_kernel");
+}
+
+int mf_user_sq_reduce(const double *user_sq, int64_t n_rows, int32_t n_cols, double *out,
+                      void *stream)
+{
+    if (!out || n_rows < 0 || n_cols < 0 || (n_rows > 0 && !user_sq))
+        return set_err(MF_E_ARG, "bad argument");
+    hipLaunchKernelGGL(user_sq_reduce_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream,
+                       user_sq, n_rows, n_cols, out);
+    return check_launch("user_sq_reduce_kernel");
 }
 
 int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *perm,
@@ -3145,7 +3421,8 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
             } else {
                 hipLaunchKernelGGL((log_replay_kernel<T, V>), dim3(g), dim3(kBlock), 0, st,
                                    (const T *)qlog, (const T *)elog, ldq, n_factors, csr->items,
-                                   (const T *)qb, csr->n_items, (T)hp->lr_pu, (T)hp->reg_pu, perm,
+                                   (const T *)qb, csr->n_items, (T)hp->lr_pu,
+                                   (T)(1.0 / (1.0 - hp->lr_pu * hp->reg_pu)), perm,
                                    ck_pos, piece_beg, n_pieces, (T *)sums, xmask);
                 return check_launch("log_replay_kernel");
             }
@@ -3195,9 +3472,11 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
                  const void *sums, const int32_t *item_piece_ptr, const void *sums2,
                  const int32_t *item_piece_ptr2, const int32_t *totals, const mf_hyper_t *hp,
                  const double *p2stat, int32_t rule, void *delta_out, int32_t apply,
-                 double *stat_next, int32_t dtype, void *stream)
+                 double *stat_next, const double *user_sq, int64_t n_users, int32_t dtype,
+                 void *stream)
 {
     if (stat_next && stat_next == p2stat) return set_err(MF_E_ARG, "stat_next aliases p2stat");
+    if (user_sq && (!stat_next || n_users < 0)) return set_err(MF_E_ARG, "user_sq needs stat_next");
     if (sums2 && !item_piece_ptr2) return set_err(MF_E_ARG, "sums2 needs item_piece_ptr2");
     if (n_items < 0 || ld < 1 || n_factors < 0 || n_factors > ld || bias_col >= ld)
         return set_err(MF_E_ARG, "bad shape");
@@ -3221,7 +3500,8 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
                                st, (T *)qb, n_items, ld, n_factors, bias_col, (const T *)sums,
                                item_piece_ptr, (const T *)sums2, item_piece_ptr2, totals,
                                count_rule, eta_b, lr_c, reg_c, lr_f,
-                               reg_f, lr_b, reg_b, p2stat, (T *)delta_out, apply, stat_next);
+                               reg_f, lr_b, reg_b, p2stat, (T *)delta_out, apply, stat_next,
+                               user_sq, (int64_t)n_users, n_factors);
             return check_launch("log_apply_kernel");
         });
     };

@@ -306,8 +306,12 @@ class MFEngine(ItemSync, Predictor):
         # ratings + err per rating; mf_log_replay rebuilds the gradients)
         if ckpt is None:
             ckpt = os.environ.get("SURPRISE_AMD_CKPT", "1") != "0"
+        # (the replay undoes one user step, dividing by ap = 1 - lr_pu reg_pu: kept well away
+        # from 0, else the gradient log)
+        h = dict(hyper or {})
+        ap = 1.0 - h.get("lr_pu", 0.0) * h.get("reg_pu", 0.0)
         self.ckpt = (self.mode == _lib.MF_MODE_LOG and bool(ckpt) and algo == "svd"
-                     and esz_q <= 1024)
+                     and esz_q <= 1024 and abs(ap) >= 0.5)
         # ... and then splits each chunk's users in two launches on two streams: the heaviest
         # users (their sequential chains bound a small epoch) on one XCD beside the rest on the
         # other seven, whose log replay then overlaps the heavy chains
@@ -317,6 +321,9 @@ class MFEngine(ItemSync, Predictor):
         # the heavy launch keeps to the XCDs of this mask and the rest to the others (disjoint
         # L2s: the rest's log replay then does not evict the heavy chains' item rows)
         self.heavy_xcd = int(os.environ.get("SURPRISE_AMD_HEAVY_XCD", "1"), 0) & 0xFF
+        self.lpt = int(os.environ.get("SURPRISE_AMD_LPT", str(self.LPT_PER_SIMD)))
+        # checkpoint stores through LDS rings + store waves (mf_svd_epoch_sq, MF_EPOCH_HELPERS)
+        self.ck_helpers = os.environ.get("SURPRISE_AMD_CK_HX", "0") != "0"
         C = _lib.load().mf_ckpt_interval() if self.ckpt else 0
         _pu = []
         pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
@@ -340,6 +347,15 @@ class MFEngine(ItemSync, Predictor):
                 if self.ckpt:
                     lg["ck"] = to_dev(ckpt_positions(row_ptr, perm, C, pos_user()))
                 lgs.append(lg)
+            if self.ckpt and self.lpt > 0 and len(parts[0]) <= self.LPT_MAX_USERS:
+                # the (light) group's epoch as LPT chains: lpt waves per SIMD of its XCDs, each
+                # taking a balanced list of users heaviest-first (the heavy group: one wave each)
+                props = torch.cuda.get_device_properties(self.dev)
+                n_x = 8 - bin(self.heavy_xcd).count("1") if len(lgs) > 1 and self.heavy_xcd else 8
+                chains = max(1, self.lpt * 4 * props.multi_processor_count * n_x // 8)
+                lgs[0]["chain"] = to_dev(chain_schedule(parts[0], row_ptr, chains,
+                                                        self.LPT_USER_COST))
+                lgs[0]["n_chains"] = chains
             main = lgs[0]
             main["heavy"] = lgs[1] if len(lgs) > 1 else None
             self.sched.append(main["sched"])
@@ -383,6 +399,12 @@ class MFEngine(ItemSync, Predictor):
         self._wt = 0
         self._work_cleared = True
         self.work = self._works[0]
+        # checkpoint log: the epoch kernel keeps user_sq[u] = |p_u|^2 (factor columns) current, and
+        # the next chunk's <pu^2> is its fixed-order sum, taken right after this chunk's epoch
+        # kernels (mf_user_sq_reduce, off the step's critical path; no mf_sumsq pass)
+        self.user_sq = (torch.zeros(max(self.n_users, 1), dtype=torch.float64, device=dev)
+                        if self.ckpt else None)
+        self._sq_valid = self._sq_pending = False
 
         # ---- factor tables
         U, I, ld, ldq = self.n_users, self.n_items, self.ld, self.ldq
@@ -420,6 +442,9 @@ class MFEngine(ItemSync, Predictor):
         if not self.biased:
             self._hyper.global_mean = 0.0
 
+    LPT_PER_SIMD = 2      # checkpoint-log epoch: LPT user chains per SIMD (0: one wave per user)
+    LPT_USER_COST = int(os.environ.get("SURPRISE_AMD_LPT_COST", "16"))  # per-user cost, ratings
+    LPT_MAX_USERS = 200_000  # (a host-side heap pass; larger epochs are bandwidth-bound anyway)
     HEAVY_USERS = 128     # users in the heavy launch (measured: 64 0.231, 128 0.224, 256 0.232 ms)
     HEAVY_MAX_NNZ = 8_000_000
 
@@ -459,6 +484,7 @@ class MFEngine(ItemSync, Predictor):
             self.qb_s.copy_(self.qb)
         if self.yj_s is not None:
             self.yj_s.copy_(self.yj)
+        self._sq_valid = False
 
     def get_factors(self, ctx=None):
         """Host fp64 copies (pu, qi, bu, bi, yj) with the padding columns dropped.  With ctx
@@ -518,6 +544,9 @@ class MFEngine(ItemSync, Predictor):
         st = self._st()
         ev = events or {}
         self._chunk = c
+        if self.ckpt:
+            self._run_chunk_ckpt(c, ev)
+            return
         if self.is_log:
             self.work = self._works[self._wt % 2]
             self._wt += 1
@@ -562,6 +591,79 @@ class MFEngine(ItemSync, Predictor):
         if lg is not None:
             self._reduce_log(lg, self.sums.data_ptr(), st, lx)
         if hv is not None:
+            self.stream.wait_event(join)
+        if "end_r" in ev:
+            ev["end_r"].record(self.stream)
+
+    def _epoch_sq(self, sched, n_sched, n_waves, st, xmask=0):
+        """The checkpoint-log epoch kernel keeping user_sq current (mf_svd_epoch_sq); with
+        ck_helpers its checkpoint stores go through LDS rings to store waves."""
+        if self.ck_helpers and n_waves <= 0:
+            n_waves = n_sched
+        _lib.call("mf_svd_epoch_sq", ctypes.byref(self._csr), self._ptr(sched), n_sched,
+                  self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb), self.ldq,
+                  self.K, int(self.biased), ctypes.byref(self._hyper),
+                  ctypes.c_void_p(self._qlog_base), ctypes.c_void_p(self._elog_base),
+                  self._ptr(self.user_sq), n_waves,
+                  (_lib.MF_EPOCH_DUP_ITEMS if self.dup_items else 0) |
+                  (_lib.MF_EPOCH_HELPERS if self.ck_helpers else 0) |
+                  (xmask << _lib.MF_EPOCH_XCD_SHIFT), self.dtype, st)
+
+    def _sq_reduce(self, out, st):
+        _lib.call("mf_user_sq_reduce", self._ptr(self.user_sq), self.n_users, self.K,
+                  self._ptr(out), st)
+
+    def _run_chunk_ckpt(self, c, ev):
+        """run_chunk for the checkpoint log.  <pu^2> of this chunk's start is in work slot t % 2:
+        summed from user_sq by the previous chunk's mf_log_apply (or here, at the first chunk
+        after set_factors or after a chunk that was not folded); the epoch kernels keep user_sq
+        current and this chunk's mf_log_apply sums slot (t + 1) % 2.  A split chunk runs on two
+        streams: the heavy users' epoch + replay on the main stream (the longest path, no waits
+        inside it), the light users' epoch + replay on the side stream after a fork from the
+        main stream; the main stream joins the side stream at the end."""
+        torch = self.torch
+        st = self._st()
+        cur = self._works[self._wt % 2]
+        self._wt += 1
+        self.work = cur
+        self._work_cleared = True  # (written, never accumulated: nothing to clear)
+        if not self._sq_valid:
+            _lib.call("mf_user_sq", self._ptr(self.pu), self.n_users, self.K, self.ld,
+                      self._ptr(self.user_sq), self.dtype, st)
+            self._sq_reduce(cur, st)
+            self._sq_valid = True
+        elif self._sq_pending:  # (the previous chunk was not folded by mf_log_apply)
+            self._sq_reduce(cur, st)
+        self._sq_pending = True
+        if "start" in ev:
+            ev["start"].record(self.stream)
+        lg = self.logs[c]
+        hv = lg["heavy"]
+        sums_h = self.sums.data_ptr() + lg["n_pieces"] * self.ldq * self.sums.element_size()
+        ls, ln, lw = lg["sched"], lg["sched"].numel(), self.n_waves
+        if "chain" in lg:
+            ls, ln, lw = lg["chain"], lg["chain"].numel(), lg["n_chains"]
+        if hv is None:
+            self._epoch_sq(ls, ln, lw, st)
+            if "end" in ev:
+                ev["end"].record(self.stream)
+            self._reduce_log(lg, self.sums.data_ptr(), st)
+        else:
+            side = self.side
+            sh = ctypes.c_void_p(side.cuda_stream)
+            lx = (~self.heavy_xcd & 0xFF) if self.heavy_xcd else 0
+            fork = torch.cuda.Event()
+            fork.record(self.stream)
+            side.wait_event(fork)
+            n_h = hv["sched"].numel()  # (the longest path first: the host may lag the GPU)
+            self._epoch_sq(hv["sched"], n_h, n_h, st, self.heavy_xcd)
+            if "end" in ev:
+                ev["end"].record(self.stream)
+            self._epoch_sq(ls, ln, lw, sh, lx)
+            self._reduce_log(lg, self.sums.data_ptr(), sh, lx)
+            join = torch.cuda.Event()
+            join.record(side)
+            self._reduce_log(hv, sums_h, st)
             self.stream.wait_event(join)
         if "end_r" in ev:
             ev["end_r"].record(self.stream)
@@ -634,7 +736,17 @@ class MFEngine(ItemSync, Predictor):
                   self._ptr(self._totals()[c]), ctypes.byref(self._hyper),
                   self._ptr(self.work), _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM,
                   None if delta_out is None else self._ptr(delta_out), int(apply),
-                  self._next_work() if apply else None, self.dtype, self._st())
+                  *self._stat_args(apply), self.dtype, self._st())
+
+    def _stat_args(self, apply):
+        """mf_log_apply's (stat_next, user_sq, n_users): the next chunk's <pu^2> slot -- summed
+        from user_sq inside the launch (checkpoint log) or cleared for mf_sumsq."""
+        if not apply:
+            return None, None, 0
+        if self.ckpt:
+            self._sq_pending = False
+            return self._ptr(self._works[self._wt % 2]), self._ptr(self.user_sq), self.n_users
+        return self._next_work(), None, 0
 
     def _next_work(self):
         """The next chunk's <pu^2> accumulator, cleared by this chunk's mf_log_apply."""
@@ -720,7 +832,7 @@ class MFEngine(ItemSync, Predictor):
                       self._ptr(self._totals()[c]),
                       ctypes.byref(self._hyper), self._ptr(self.work),
                       _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM, None, 1,
-                      self._next_work(), self.dtype, st)
+                      *self._stat_args(True), self.dtype, st)
             x = 1
         for tab, snap, ld, _, rule in self._snap_tables():
             if rule == "affine":
