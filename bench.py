@@ -39,7 +39,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); 6.3 TB/s achievable copy
-EVENT_EVERY = 4  # steps between HIP-event-instrumented steps
+PHASE_STEPS = 5  # epochs with HIP events around each phase, after the timed region
 BOX_CPU_SHARE = 16  # host cores of one GPU's share on the GPU box (os.cpu_count() shows the host)
 SHAPE_DEFAULTS = {  # shape -> (algo, n_factors, scaling)
     "ml-1m": ("svd", 100, "weak"),
@@ -180,9 +180,10 @@ def hyper_for(algo, gm):
 
 # ---------------------------------------------------------------------------- timing
 def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
-    """Warmup, then `steps` epochs between barriers + synchronize.  Every EVENT_EVERY-th timed
-    step carries HIP events on the engine's stream around each phase (a recorded timing event
-    idles the GPU for a few us, which the other steps do not pay).  Returns (seconds, phases)."""
+    """Warmup, then `steps` epochs between barriers + synchronize (no timing events inside the
+    timed region), then -- instrument -- PHASE_STEPS more epochs carrying HIP events on the
+    engine's stream around each phase (a recorded timing event idles the GPU for a few us).
+    Returns (seconds of the timed region, phases of the instrumented epochs)."""
     for _ in range(warmup):
         for c in range(eng.n_chunks):
             eng.run_chunk(c)
@@ -194,12 +195,15 @@ def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
     recs = []
     t0 = time.perf_counter()
     for step in range(steps):
-        timed = instrument and step % EVENT_EVERY == 0
         for c in range(eng.n_chunks):
-            if not timed:
-                eng.run_chunk(c)
-                eng.sync_items(ctx)
-                continue
+            eng.run_chunk(c)
+            eng.sync_items(ctx)
+    torch.cuda.synchronize()
+    if ctx is not None:
+        ctx.barrier()
+    elapsed = time.perf_counter() - t0
+    for step in range(PHASE_STEPS if instrument else 0):
+        for c in range(eng.n_chunks):
             ev = {k: torch.cuda.Event(enable_timing=True)
                   for k in ("begin", "start", "end", "end_h", "end_r", "done")}
             ev["begin"].record(eng.stream)
@@ -208,9 +212,6 @@ def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
             ev["done"].record(eng.stream)
             recs.append(ev)
     torch.cuda.synchronize()
-    if ctx is not None:
-        ctx.barrier()
-    elapsed = time.perf_counter() - t0
     phases = {}
     if recs:
         span = lambda a, b: float(np.mean([e[a].elapsed_time(e[b]) for e in recs]))
@@ -389,10 +390,11 @@ def main():
         "traffic_breakdown": tinfo.get("per_kernel") if tinfo else None,
         "traffic_source": tinfo.get("source") if tinfo else None,
         "note": "achieved = algorithmic bytes of a step (SURVEY 8(d): a gather + scatter of the "
-                "user and item rows per rating) / the measured step time; ML-1M's tables (pu "
-                "2.4 MB, qb 1.6 MB) are L2/MALL-resident, so HBM moves far fewer bytes than the "
-                "algorithmic figure (`traffic`, PMC) and the epoch kernel is bound by the "
-                "heaviest user's sequential chain, not by HBM",
+                "user and item rows per rating) / the measured step time (<= 1 by construction). "
+                "ML-1M's tables (pu 2.7 MB, qb 1.7 MB) are L2/MALL-resident: the HBM-side bytes "
+                "(`traffic`: every kernel's 2 x FETCH_SIZE + WRITE_SIZE per step, PMC, MALL hits "
+                "included) are mostly the checkpoint log written and re-read, and the step is "
+                "bound by the heaviest user's sequential chain (1805 ratings), not by HBM",
     }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline and algo == "svd":
@@ -420,6 +422,10 @@ def main():
             "roofline": {"achieved": b2 * n_train / (e2 / n2) / 1e9, "peak": HBM_PEAK_GBS,
                          "frac": b2 * n_train / (e2 / n2) / 1e9 / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_update": b2}}
+        t2, ti2 = traffic_for("svdpp", 100, "ml-1m")
+        result["svdpp_c3"]["roofline"].update(
+            traffic=t2, traffic_breakdown=ti2.get("per_kernel") if ti2 else None,
+            traffic_source=ti2.get("source") if ti2 else None)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -102,11 +102,11 @@ typedef struct mf_csr {
  * (n_waves = chains) whose q deltas go through an LDS ring to three waves that issue the float
  * atomics; sched entries < 0 are skipped (a schedule laid out per chain, strided by n_waves). */
 #define MF_EPOCH_SVDPP_HELPERS 2
-/* the same bit for mf_svd_epoch / mf_svd_epoch_sq with the checkpoint log (elog): two user chains
- * per workgroup (n_waves = chains), whose checkpoint rows and errors go through LDS rings to two
- * waves that issue the global stores (a chain's vector-memory counter then holds only its row
- * gathers); sched entries < 0 are skipped. */
-#define MF_EPOCH_HELPERS 2
+/* mf_svd_epoch / mf_svd_epoch_sq with the checkpoint log (elog): err_k is written into its pair's
+ * checkpoint row, padding column E + (k - c) (E = n_factors + 1 rounded up to even for fp32,
+ * n_factors + 1 for fp64; needs E + 2 <= ldq) instead of elog[k]; mf_log_replay with the same
+ * flag reads it there (no per-rating gather of elog). */
+#define MF_EPOCH_ERR_IN_ROW 4
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
                  const mf_hyper_t *hp, int32_t mode, void *qlog, void *elog, int32_t n_waves,

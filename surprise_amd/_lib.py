@@ -21,7 +21,7 @@ MF_MERGE_SUM, MF_MERGE_COUNT, MF_MERGE_MEAN = 0, 1, 2
 MF_EPOCH_DUP_ITEMS = 1
 MF_EPOCH_XCD_SHIFT = 8  # flags bits 8..15: XCD mask (include/surprise_amd.h)
 MF_EPOCH_SVDPP_HELPERS = 2
-MF_EPOCH_HELPERS = 2  # (the same bit: SVD checkpoint-log store waves)
+MF_EPOCH_ERR_IN_ROW = 4  # checkpoint log: errors in the checkpoint rows' padding
 MAX_FACTORS = {MF_F32: 512, MF_F64: 256}
 
 

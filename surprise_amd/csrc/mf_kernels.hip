@@ -38,7 +38,7 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    bool hx, double *psq, void *stream);
+                    bool hx, double *psq, int err_col, void *stream);
 }  // namespace mf_ext
 
 namespace {
@@ -848,108 +848,6 @@ __device__ __forceinline__ void wave_sum2_u(T x, T y, T &sx, T &sy) {
     sy = readlane(z, 63);
 }
 
-// ---- checkpoint-log stores through LDS (MF_EPOCH_SVD_HELPERS): a wave's vmcnt counts its loads
-// AND its stores in one in-order counter (gfx9), so a chain wave that stores its checkpoint rows
-// waits, at a later row gather, for stores that the memory system keeps pending for thousands of
-// cycles under load (measured: the heaviest ML-1M chain 136 us with its stores, 112 us without).
-// With helpers a workgroup holds two chain waves (0, 1) and two helper waves (2, 3): chain c puts
-// each bank's checkpoint rows and errors into its LDS ring (ds writes count in lgkmcnt, not
-// vmcnt) and helper 2 + c issues the global stores.
-#ifndef MF_CK_RING
-#define MF_CK_RING 4  // banks per ring
-#endif
-constexpr int kCkSpinMax = 1 << 22;  // bounded spins (s_sleep each): never hang the GPU
-
-template <typename T, int G, int kLg>
-struct CkRing {
-    static constexpr int E = MF_CK_RING;
-    typename Lane8<T>::vec rows[E][kLg][G][kWave];
-    T err[E][kWave];
-    int64_t base[E];  // the user's first CSR position
-    int n[E], j0[E];  // the user's rating count, the bank's first rating
-    int head, done, tail;
-};
-
-__device__ __forceinline__ int lds_ld(int *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_st(int *p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// helper wave of one chain: the global stores of every bank the chain pushes, until it is done
-template <typename T, int G, int kLg>
-__device__ void ck_ring_helper(CkRing<T, G, kLg> *ring, T *qlog, T *elog, int ldq, int kB)
-{
-    using L = Lane8<T>;
-    constexpr int W = L::W;
-    constexpr int E = CkRing<T, G, kLg>::E;
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint32_t qrow = (uint32_t)ldq * sizeof(T);
-    uint32_t cl[G];
-#pragma unroll
-    for (int v = 0; v < G; ++v) {
-        const int c0 = (lane + kWave * v) * W;
-        cl[v] = c0 < ldq ? (uint32_t)c0 * sizeof(T) : kLogOob;
-    }
-    int t = 0, spins = 0;
-    while (true) {
-        int hd = lds_ld(&ring->head);
-        if (t >= hd) {
-            if (lds_ld(&ring->done)) {
-                asm volatile("" ::: "memory");
-                hd = lds_ld(&ring->head);
-                if (t >= hd) break;
-            } else {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > kCkSpinMax) break;
-                continue;
-            }
-        }
-        spins = 0;
-        asm volatile("" ::: "memory");
-        for (; t < hd; ++t) {
-            const int e = t % E;
-            const int64_t s = __builtin_amdgcn_readfirstlane((int)(ring->base[e] & 0xffffffff)) |
-                              ((int64_t)__builtin_amdgcn_readfirstlane((int)(ring->base[e] >> 32)) << 32);
-            const int n = __builtin_amdgcn_readfirstlane(ring->n[e]);
-            const int j0 = __builtin_amdgcn_readfirstlane(ring->j0[e]);
-            const rsrc_t l_rs = make_rsrc(qlog + s * ldq, (uint32_t)n * qrow);
-            const rsrc_t e_rs = make_rsrc(elog + s, (uint32_t)n * sizeof(T));
-            typename L::vec r[kLg][G];
-#pragma unroll
-            for (int x = 0; x < kLg; ++x)
-#pragma unroll
-                for (int v = 0; v < G; ++v) r[x][v] = ring->rows[e][x][v][lane];
-            const T ev = ring->err[e][lane];
-#pragma unroll
-            for (int x = 0; x < kLg; ++x)
-#pragma unroll
-                for (int v = 0; v < G; ++v)
-                    L::template sts<0>(l_rs, cl[v], (uint32_t)(j0 + x * kCkpt) * qrow, r[x][v]);
-            Buf<T>::template st<0>(e_rs, lane < kB ? (uint32_t)(j0 + lane) * sizeof(T) : kLogOob, ev);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the entries' reads have returned
-        lds_st(&ring->tail, t);
-    }
-}
-
-// chain slot of wave 0 / 1 of a helper-wave launch (two chains per block) on the XCDs of xmask
-__device__ __forceinline__ bool chain_slot(int xmask, int64_t &slot, int64_t &n_slots) {
-    const int64_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    if (!xmask) {
-        slot = (int64_t)blockIdx.x * 2 + w;
-        n_slots = (int64_t)gridDim.x * 2;
-        return true;
-    }
-    const int x = __builtin_amdgcn_readfirstlane(xcc_id());
-    if (!((xmask >> x) & 1)) return false;
-    const int c = __builtin_popcount(xmask), rank = __builtin_popcount(xmask & ((1 << x) - 1));
-    slot = ((int64_t)(blockIdx.x >> 3) * c + rank) * 2 + w;
-    n_slots = (int64_t)(gridDim.x >> 3) * c * 2;
-    return true;
-}
-
 // ---- SVD rating loop in lookahead form (kLog, SVD, G = 1: K <= 127 fp32 / K <= 63 fp64)
 //
 // Per user, with q_k = the snapshot row [q | b] of rating k and p_k's column K the constant 1:
@@ -964,34 +862,25 @@ __device__ __forceinline__ bool chain_slot(int xmask, int64_t &slot, int64_t &n_
 // (columns 0..K; mf_log_apply turns the sums into the item steps).  Same arithmetic as the
 // reference recursion up to rounding (fp64: equal to the delta-log oracle to 1e-9,
 // tests/test_gpu_parity.py).
-template <typename T, int G>
-constexpr int la_bank() { return G == 1 ? MF_LA_BANK : MF_LA_BANK_G2; }
-
-template <typename T, int G, bool CK, bool HX = false>
+template <typename T, int G, bool CK, bool ER = false>
 __device__ __forceinline__ void epoch_body_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *qlog, T *elog, int K,
     int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, double *psq,
-    CkRing<T, G, la_bank<T, G>() / kCkpt> *ring = nullptr)
+    int err_col)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
     constexpr int W = L::W;
     // ratings per bank of gathered rows (a power of 2 <= 64)
-    constexpr int kB = la_bank<T, G>();
+    constexpr int kB = G == 1 ? MF_LA_BANK : MF_LA_BANK_G2;
     static_assert(!CK || (kB % kCkpt == 0 && kB <= kWave), "checkpoints: whole banks");
-    static_assert(!HX || CK, "helper stores: checkpoint log only");
     const int lane = threadIdx.x & (kWave - 1);
     int64_t wave, grid_waves;
-    if (HX) {  // (the caller checked the XCD mask)
-        chain_slot(xmask, wave, grid_waves);
-    } else if (!wave_slot(xmask, wave, grid_waves)) {
-        return;
-    }
+    if (!wave_slot(xmask, wave, grid_waves)) return;
     const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
     if (wave >= n_waves) return;
-    int pushed = 0;  // HX: banks pushed to the ring
 
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), prow = (uint32_t)ldu * sizeof(T);
     const uint32_t q_oob = (uint32_t)n_items * qrow;
@@ -1003,7 +892,7 @@ __device__ __forceinline__ void epoch_body_la(
         const uint32_t b = (uint32_t)c0 * sizeof(T);
         cq[v] = c0 < ldq ? b : q_oob;
         cu[v] = c0 < ldu ? b : prow;  // >= the pu record (K elements): dropped
-        cl[v] = c0 < ldq ? b : kLogOob;
+        cl[v] = c0 < (ER ? err_col : ldq) ? b : kLogOob;  // (ER: the err columns' own store)
 #pragma unroll
         for (int e = 0; e < W; ++e) {
             const int c = c0 + e;
@@ -1013,6 +902,11 @@ __device__ __forceinline__ void epoch_body_la(
             L::set(ap[v], e, fac ? T(1) - hp.lr_pu * hp.reg_pu : T(1));
         }
     }
+    // err_col > 0: lane d < kB of a bank's err vector goes to row d & ~1 (its pair's checkpoint),
+    // column err_col + (d & 1)
+    const uint32_t ce = (ER && lane < kB)
+                            ? (uint32_t)(((lane & ~1) * ldq + err_col + (lane & 1)) * sizeof(T))
+                            : kLogOob;
     const T lr_bu = biased ? hp.lr_bu : T(0);
     const T abu = T(1) - lr_bu * hp.reg_bu;
     const T kb = hp.gm * (T(1) - abu);
@@ -1027,7 +921,7 @@ __device__ __forceinline__ void epoch_body_la(
         else if (n * 4 > prio_len) __builtin_amdgcn_s_setprio(2);
         else if (n * 8 > prio_len) __builtin_amdgcn_s_setprio(1);
         const rsrc_t l_rs = make_rsrc(qlog + s * ldq, (uint32_t)n * qrow);
-        const rsrc_t e_rs = make_rsrc(CK ? elog + s : qlog, (uint32_t)n * sizeof(T));
+        const rsrc_t e_rs = make_rsrc(CK && !ER ? elog + s : qlog, (uint32_t)n * sizeof(T));
         const int32_t *__restrict__ it = items + s;
         const T *__restrict__ rt = ratings + s;
         const rsrc_t p_rs = make_rsrc(pu + (int64_t)u * ldu, (uint32_t)K * sizeof(T));
@@ -1037,6 +931,7 @@ __device__ __forceinline__ void epoch_body_la(
 #pragma unroll
         for (int v = 0; v < G; ++v) p0[v] = L::template ld<0>(p_rs, cu[v]) + one[v];
         const T bu0 = Buf<T>::template ld<0>(b_rs, 0);
+
 
         // Two banks of kB gathered rows alternate.  At the start of a bank: the ids of the bank
         // after next are requested, then the next bank's rows, THEN the previous bank's kB log
@@ -1074,36 +969,19 @@ __device__ __forceinline__ void epoch_body_la(
 #if defined(MF_EXP_LA_NO_STORE)  // timing experiment only: no log written (wrong results)
             return;
 #endif
-            if constexpr (HX) {  // to the LDS ring; the helper wave stores
-                constexpr int E = CkRing<T, G, kLg>::E;
-                for (int spins = 0; spins < kCkSpinMax; ++spins) {
-                    if (pushed - lds_ld(&ring->tail) < E) break;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                asm volatile("" ::: "memory");
-                const int e = pushed % E;
-#pragma unroll
-                for (int x = 0; x < kLg; ++x)
-#pragma unroll
-                    for (int v = 0; v < G; ++v) ring->rows[e][x][v][lane] = lg[x][v];
-                ring->err[e][lane] = ev;
-                if (lane == 0) {
-                    ring->base[e] = s;
-                    ring->n[e] = n;
-                    ring->j0[e] = j0p;
-                }
-                ++pushed;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the entry before the count
-                lds_st(&ring->head, pushed);
-                return;
-            } else if constexpr (CK) {
+            if constexpr (CK) {
 #pragma unroll
                 for (int x = 0; x < kLg; ++x)
 #pragma unroll
                     for (int v = 0; v < G; ++v)
                         L::template sts<MF_LOG_AUX>(l_rs, cl[v], (uint32_t)(j0p + x * kCkpt) * qrow,
                                                     lg[x][v]);
-                Buf<T>::template st<0>(e_rs, lane < kB ? (uint32_t)(j0p + lane) * sizeof(T) : kLogOob, ev);
+                // err_k: into its pair's row (columns err_col, err_col + 1; the row stores above
+                // leave those columns alone) or to elog[k]; one store per bank either way
+                if constexpr (ER)
+                    Buf<T>::template st<0>(l_rs, ce + (uint32_t)j0p * qrow, ev);
+                else
+                    Buf<T>::template st<0>(e_rs, lane < kB ? (uint32_t)(j0p + lane) * sizeof(T) : kLogOob, ev);
                 return;
             }
 #if defined(MF_EXP_PAIR_STORE)  // timing experiment only: 2 rows per dwordx4 (wrong layout)
@@ -1702,7 +1580,8 @@ __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,                      \
         const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,       \
         T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, T *elog,\
-        int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, double *psq
+        int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, double *psq,   \
+        int err_col
 #define MF_EPOCH_ARGS \
     row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, elog, K, biased, hp,    \
         n_items, n_waves_req, xmask
@@ -1718,43 +1597,22 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
             return;
         }
     }
-    if constexpr (MODE == kLog && !PP && G <= kLaMaxG && MF_LA) {
-        if (elog)
-            epoch_body_la<T, G, true>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
-                                      qlog, elog, K, biased, hp, n_items, n_waves_req, xmask, psq);
-        else
-            epoch_body_la<T, G, false>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb,
-                                       ldq, qlog, elog, K, biased, hp, n_items, n_waves_req, xmask,
-                                       psq);
+    if constexpr (MODE == kLog && !PP && G <= kLaMaxG && MF_LA) {  // (the gradient log)
+        epoch_body_la<T, G, false>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
+                                   qlog, elog, K, biased, hp, n_items, n_waves_req, xmask, psq, 0);
     } else {
         epoch_body<T, G, MODE, PP, DUPS, kPF>(MF_EPOCH_ARGS);
     }
 }
 
-// SVD checkpoint log with helper waves (MF_EPOCH_HELPERS): workgroup = chain waves 0, 1 + their
-// store waves 2, 3 (ck_ring_helper)
-template <typename T, int G>
-__global__ __launch_bounds__(kBlock) void mf_svd_hx_kernel(MF_EPOCH_PARAMS)
+// SVD checkpoint log (elog != NULL): its own kernel, so that its register allocation is its own
+// (ER: the errors go into the checkpoint rows, MF_EPOCH_ERR_IN_ROW)
+template <typename T, int G, bool ER>
+__global__ __launch_bounds__(kBlock) void mf_ckpt_epoch_kernel(MF_EPOCH_PARAMS)
 {
-    constexpr int kLg = la_bank<T, G>() / kCkpt;
-    __shared__ CkRing<T, G, kLg> rings[2];
-    if (xmask) {  // (the whole block leaves an XCD outside the mask)
-        const int x = __builtin_amdgcn_readfirstlane(xcc_id());
-        if (!((xmask >> x) & 1)) return;
-    }
-    const int w = threadIdx.x / kWave;
-    if (threadIdx.x == 0)
-        for (int c = 0; c < 2; ++c) rings[c].head = rings[c].done = rings[c].tail = 0;
-    __syncthreads();
-    if (w < 2) {
-        epoch_body_la<T, G, true, true>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb,
-                                        ldq, qlog, elog, K, biased, hp, n_items, n_waves_req, xmask,
-                                        psq, &rings[w]);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        lds_st(&rings[w].done, 1);
-    } else {
-        ck_ring_helper<T, G, kLg>(&rings[w - 2], qlog, elog, ldq, la_bank<T, G>());
-    }
+    epoch_body_la<T, G, true, ER>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
+                                  qlog, elog, K, biased, hp, n_items, n_waves_req, xmask, psq,
+                                  err_col);
 }
 
 // SVD++ with helper waves (MF_SVDPP_HELPERS): workgroup = chain wave 0 + kHxHelpers atomic waves
@@ -1789,10 +1647,10 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    bool hx, double *psq, void *stream)
+                    bool hx, double *psq, int err_col, void *stream)
 {
-    if (psq && (PP || M != kLog || !elog))
-        return set_err(MF_E_UNSUPPORTED, "user_sq: the SVD checkpoint-log epoch only");
+    if ((psq || err_col) && (PP || M != kLog || !elog))
+        return set_err(MF_E_UNSUPPORTED, "user_sq / errors in rows: the SVD checkpoint log only");
     // elog: SVD: the checkpoint log (the lookahead body: kLog, up to two lane groups);
     //       SVD++: the deferred y buffer (kAtomic)
     if (elog && !PP && (M != kLog || !MF_LA || (int64_t)ldq * sizeof(T) > 512 * kLaMaxG))
@@ -1801,9 +1659,8 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     // popular item's c_u diverges: measured held-out RMSE 1.82 on ML-1M)
     if (elog && PP && M != kAtomic)
         return set_err(MF_E_UNSUPPORTED, "deferred y: MF_MODE_ATOMIC only");
-    if (hx && !(PP && M == kAtomic && elog && !dups) && !(!PP && M == kLog && elog))
-        return set_err(MF_E_UNSUPPORTED, "helper waves: SVD++ (MF_MODE_ATOMIC, deferred y, no repeated "
-                                         "items) or the SVD checkpoint log");
+    if (hx && !(PP && M == kAtomic && elog && !dups))
+        return set_err(MF_E_UNSUPPORTED, "helper waves: SVD++, MF_MODE_ATOMIC, deferred y, no repeated items");
     return dispatch_g<T>(ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         if constexpr (PP && M == kAtomic && V <= kLaMaxG) {
@@ -1812,25 +1669,23 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
                                    (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
-                                   cast_hyper<T>(hp), csr->n_items, waves, 0, nullptr);
+                                   cast_hyper<T>(hp), csr->n_items, waves, 0, nullptr, 0);
                 return check_launch("mf_svdpp_hx_kernel");
-            }
-        } else if constexpr (!PP && M == kLog && V <= kLaMaxG && MF_LA) {
-            if (hx) {  // two chains per workgroup, each with a store wave
-                int64_t blocks = (waves + 1) / 2;
-                if (xmask) {
-                    const int c = __builtin_popcount(xmask & 0xFF);
-                    blocks = 8 * ((blocks + c - 1) / c);
-                }
-                hipLaunchKernelGGL((mf_svd_hx_kernel<T, V>), dim3(blocks), dim3(kBlock), 0,
-                                   (hipStream_t)stream, csr->row_ptr, csr->items,
-                                   (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
-                                   (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
-                                   cast_hyper<T>(hp), csr->n_items, waves, xmask, psq);
-                return check_launch("mf_svd_hx_kernel");
             }
         } else {
             if (hx) return set_err(MF_E_UNSUPPORTED, "helper waves: rows of <= 1 KiB");
+        }
+        if constexpr (M == kLog && !PP && V <= kLaMaxG && MF_LA) {
+            if (elog) {  // the checkpoint log
+                auto ck = err_col > 0 ? mf_ckpt_epoch_kernel<T, V, true>
+                                      : mf_ckpt_epoch_kernel<T, V, false>;
+                hipLaunchKernelGGL(ck, dim3(grid_for_waves_x(waves, xmask)), dim3(kBlock), 0,
+                                   (hipStream_t)stream, csr->row_ptr, csr->items,
+                                   (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
+                                   (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
+                                   cast_hyper<T>(hp), csr->n_items, waves, xmask, psq, err_col);
+                return check_launch("mf_ckpt_epoch_kernel");
+            }
         }
         // (kLog reads a snapshot: a repeated item sees the chunk-start row, no forwarding)
         auto kern = (dups && M != kLog) ? mf_epoch_kernel<T, V, M, PP, true>
@@ -1839,14 +1694,14 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                            (hipStream_t)stream,
                            csr->row_ptr, csr->items, (const T *)csr->ratings, sched, n_sched,
                            (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K,
-                           biased, cast_hyper<T>(hp), csr->n_items, waves, xmask, psq);
+                           biased, cast_hyper<T>(hp), csr->n_items, waves, xmask, psq, err_col);
         return check_launch(PP ? "mf_epoch_kernel<svdpp>" : "mf_epoch_kernel<svd>");
     });
 }
 template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
     void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, bool, double *,
-    void *);
+    int, void *);
 }  // namespace mf_ext
 #else  // the main translation unit
 
@@ -2129,7 +1984,8 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     const T *__restrict__ ckpt, const T *__restrict__ elog, int ldq, int K,
     const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T inv_ap,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
-    const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int xmask)
+    const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int xmask,
+    int err_col)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -2160,7 +2016,8 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
         const int xl = beg + (lane < cnt ? lane : cnt - 1);
         const int k_l = perm[xl], c_l = ck_pos[xl];  // lane x: rating x and its pair's row
         const int odd_l = k_l - c_l;                  // 1: k = c + 1 (the row as stored)
-        const T ek_l = lane < cnt ? elog[k_l] : T(0);  // lanes >= cnt: weight 0
+        // err_k: gathered from elog, or (err_col > 0) read from the row below
+        const T ek_l = lane < cnt && err_col <= 0 ? elog[k_l] : T(0);  // lanes >= cnt: weight 0
         // the piece's item row (snapshot) -> D = lrp o q_i
         const uint32_t qoff = (uint32_t)items[readlane(k_l, 0)] * qrow;
         vec D[G];
@@ -2183,7 +2040,17 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
             for (int y = 0; y < kU; ++y) {
                 const int x = x0 + y < kWave ? x0 + y : kWave - 1;
                 const int odd = readlane(odd_l, x);
-                const T ek = readlane(ek_l, x);
+                T ek;
+                if (err_col > 0) {  // column err_col + odd of the checkpoint row
+                    const int c = err_col + odd, l = (c / W) % kWave, vg = (c / W) / kWave;
+                    T e = T(0);
+#pragma unroll
+                    for (int v = 0; v < G; ++v)
+                        if (v == vg) e = readlane(L::get(p[y][v], c % W), l);
+                    ek = x0 + y < cnt ? e : T(0);
+                } else {
+                    ek = readlane(ek_l, x);
+                }
 #pragma unroll
                 for (int v = 0; v < G; ++v) {
                     const vec pc_ = iap[v] * (p[y][v] - ek * D[v]);  // p_c from p_{c+1}
@@ -2210,6 +2077,9 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     }
 }
 
+#ifndef MF_APPLY_U
+#define MF_APPLY_U 16  // mf_log_apply: piece rows in flight per wave (a popular item has ~60)
+#endif
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     T *__restrict__ qb, int n_items, int ld, int n_fac, int bias_col, const T *__restrict__ sums,
@@ -2247,7 +2117,7 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
             const int32_t *__restrict__ ipp = part ? item_piece_ptr2 : item_piece_ptr;
             const int p0 = ipp ? ipp[i] : (int)i;
             const int p1 = ipp ? ipp[i + 1] : (int)i + 1;
-            constexpr int kU = 8;  // independent loads in flight
+            constexpr int kU = MF_APPLY_U;  // independent loads in flight
             for (int pc = p0; pc < p1; pc += kU) {
                 T g[kU][V];
 #pragma unroll
@@ -3238,6 +3108,14 @@ int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const v
     return 0;
 }
 
+// First of the two padding columns that hold a checkpoint row's errors (MF_EPOCH_ERR_IN_ROW):
+// past the bias column, 8-byte aligned for fp32 (one lane's pair); 0 if the row has no room.
+int err_column(int K, int ldq, int dtype)
+{
+    const int c = dtype == MF_F32 ? ((K + 2) & ~1) : K + 1;
+    return c + 2 <= ldq ? c : 0;
+}
+
 template <bool PP>
 int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
@@ -3248,6 +3126,13 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
     const bool hx = flags & MF_EPOCH_SVDPP_HELPERS;
     const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
     if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, qlog, dtype)) return rc;
+    int err_col = 0;
+    if (flags & MF_EPOCH_ERR_IN_ROW) {
+        if (PP || mode != MF_MODE_LOG || !elog)
+            return set_err(MF_E_ARG, "MF_EPOCH_ERR_IN_ROW: the SVD checkpoint log only");
+        err_col = err_column(K, ldq, dtype);
+        if (err_col <= 0) return set_err(MF_E_UNSUPPORTED, "MF_EPOCH_ERR_IN_ROW: no spare columns");
+    }
     if (PP && !yj) return set_err(MF_E_ARG, "null yj");
     if (n_sched <= 0) return 0;
     // default: one wave per user up to MF_EPOCH_WPC waves per CU (then strided): a wave that
@@ -3260,7 +3145,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         constexpr int M = decltype(mode_c)::value;
         return mf_ext::launch_epoch_tm<T, M, PP>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj,
                                                   qlog, elog, K, biased, hp, waves, dups, xmask,
-                                                  hx, psq, stream);
+                                                  hx, psq, err_col, stream);
     };
     auto by_mode = [&](auto tag_t) -> int {
         switch (mode) {
@@ -3407,6 +3292,9 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
     if (n_pieces == 0) return 0;
     if (!qlog || !elog || !csr || !qb || !hp || !perm || !ck_pos || !piece_beg || !sums)
         return set_err(MF_E_ARG, "null argument");
+    const int err_col = (flags & MF_EPOCH_ERR_IN_ROW) ? err_column(n_factors, ldq, dtype) : 0;
+    if ((flags & MF_EPOCH_ERR_IN_ROW) && err_col <= 0)
+        return set_err(MF_E_UNSUPPORTED, "MF_EPOCH_ERR_IN_ROW: no spare columns");
     const int64_t rb = (int64_t)ldq * (dtype == MF_F64 ? 8 : 4);
     if (rb > 512 * kLaMaxG) return set_err(MF_E_UNSUPPORTED, "checkpoint log: ldq * size <= 1 KiB only");
     const int64_t cap = (int64_t)n_cus() * MF_REPLAY_WPC * (xmask ? __builtin_popcount(xmask) : 8) / 8;
@@ -3423,7 +3311,7 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
                                    (const T *)qlog, (const T *)elog, ldq, n_factors, csr->items,
                                    (const T *)qb, csr->n_items, (T)hp->lr_pu,
                                    (T)(1.0 / (1.0 - hp->lr_pu * hp->reg_pu)), perm,
-                                   ck_pos, piece_beg, n_pieces, (T *)sums, xmask);
+                                   ck_pos, piece_beg, n_pieces, (T *)sums, xmask, err_col);
                 return check_launch("log_replay_kernel");
             }
         });

@@ -322,8 +322,12 @@ class MFEngine(ItemSync, Predictor):
         # L2s: the rest's log replay then does not evict the heavy chains' item rows)
         self.heavy_xcd = int(os.environ.get("SURPRISE_AMD_HEAVY_XCD", "1"), 0) & 0xFF
         self.lpt = int(os.environ.get("SURPRISE_AMD_LPT", str(self.LPT_PER_SIMD)))
-        # checkpoint stores through LDS rings + store waves (mf_svd_epoch_sq, MF_EPOCH_HELPERS)
-        self.ck_helpers = os.environ.get("SURPRISE_AMD_CK_HX", "0") != "0"
+        self.heavy_replay_all = os.environ.get("SURPRISE_AMD_HEAVY_REPLAY_ALL", "1") != "0"
+        # checkpoint log with MF_EPOCH_ERR_IN_ROW where the row has room: each pair's two errors
+        # ride in its checkpoint row's padding (the replay gathers no elog entries)
+        e0 = ((self.K + 2) & ~1) if self.dtype == _lib.MF_F32 else self.K + 1
+        self.err_in_row = (self.ckpt and e0 + 2 <= self.ldq
+                           and os.environ.get("SURPRISE_AMD_ERR_IN_ROW", "1") != "0")
         C = _lib.load().mf_ckpt_interval() if self.ckpt else 0
         _pu = []
         pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
@@ -442,7 +446,8 @@ class MFEngine(ItemSync, Predictor):
         if not self.biased:
             self._hyper.global_mean = 0.0
 
-    LPT_PER_SIMD = 2      # checkpoint-log epoch: LPT user chains per SIMD (0: one wave per user)
+    LPT_PER_SIMD = 0      # checkpoint-log epoch: LPT user chains per SIMD (0: one wave per user;
+                          # measured at ML-1M: 1 / 2 / 4 chains per SIMD no faster than 0)
     LPT_USER_COST = int(os.environ.get("SURPRISE_AMD_LPT_COST", "16"))  # per-user cost, ratings
     LPT_MAX_USERS = 200_000  # (a host-side heap pass; larger epochs are bandwidth-bound anyway)
     HEAVY_USERS = 128     # users in the heavy launch (measured: 64 0.231, 128 0.224, 256 0.232 ms)
@@ -596,17 +601,14 @@ class MFEngine(ItemSync, Predictor):
             ev["end_r"].record(self.stream)
 
     def _epoch_sq(self, sched, n_sched, n_waves, st, xmask=0):
-        """The checkpoint-log epoch kernel keeping user_sq current (mf_svd_epoch_sq); with
-        ck_helpers its checkpoint stores go through LDS rings to store waves."""
-        if self.ck_helpers and n_waves <= 0:
-            n_waves = n_sched
+        """The checkpoint-log epoch kernel keeping user_sq current (mf_svd_epoch_sq)."""
         _lib.call("mf_svd_epoch_sq", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                   self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb), self.ldq,
                   self.K, int(self.biased), ctypes.byref(self._hyper),
                   ctypes.c_void_p(self._qlog_base), ctypes.c_void_p(self._elog_base),
                   self._ptr(self.user_sq), n_waves,
                   (_lib.MF_EPOCH_DUP_ITEMS if self.dup_items else 0) |
-                  (_lib.MF_EPOCH_HELPERS if self.ck_helpers else 0) |
+                  (_lib.MF_EPOCH_ERR_IN_ROW if self.err_in_row else 0) |
                   (xmask << _lib.MF_EPOCH_XCD_SHIFT), self.dtype, st)
 
     def _sq_reduce(self, out, st):
@@ -652,21 +654,30 @@ class MFEngine(ItemSync, Predictor):
             side = self.side
             sh = ctypes.c_void_p(side.cuda_stream)
             lx = (~self.heavy_xcd & 0xFF) if self.heavy_xcd else 0
-            fork = torch.cuda.Event()
-            fork.record(self.stream)
-            side.wait_event(fork)
+            self._ev_record("fork", self.stream)
+            self._ev_wait(side, "fork")
             n_h = hv["sched"].numel()  # (the longest path first: the host may lag the GPU)
             self._epoch_sq(hv["sched"], n_h, n_h, st, self.heavy_xcd)
             if "end" in ev:
                 ev["end"].record(self.stream)
             self._epoch_sq(ls, ln, lw, sh, lx)
             self._reduce_log(lg, self.sums.data_ptr(), sh, lx)
-            join = torch.cuda.Event()
-            join.record(side)
-            self._reduce_log(hv, sums_h, st)
-            self.stream.wait_event(join)
+            self._ev_record("join", side)
+            # (the heavy replay starts when the longest chain ends: by then the light users'
+            # work is (nearly) done, so it may spread over every XCD)
+            self._reduce_log(hv, sums_h, st, 0 if self.heavy_replay_all else self.heavy_xcd)
+            self._ev_wait(self.stream, "join")
         if "end_r" in ev:
             ev["end_r"].record(self.stream)
+
+    def _ev_record(self, name, stream):
+        """Record the engine's cross-stream event `name` on stream."""
+        evs = self.__dict__.setdefault("_events", {})
+        evs[name] = self.torch.cuda.Event()
+        evs[name].record(stream)
+
+    def _ev_wait(self, stream, name):
+        stream.wait_event(self._events[name])
 
     def _reduce_log(self, lg, sums_ptr, st, xmask=0):
         """Piece sums of one user group's log: mf_log_replay (checkpoint form) or mf_log_reduce.
@@ -676,7 +687,9 @@ class MFEngine(ItemSync, Predictor):
                       ctypes.c_void_p(self._elog_base), self.ldq, self.K, ctypes.byref(self._csr),
                       self._ptr(self.qb), ctypes.byref(self._hyper), self._ptr(lg["perm"]),
                       self._ptr(lg["ck"]), self._ptr(lg["pb"]), lg["n_pieces"],
-                      ctypes.c_void_p(sums_ptr), xmask << _lib.MF_EPOCH_XCD_SHIFT, self.dtype, st)
+                      ctypes.c_void_p(sums_ptr),
+                      (xmask << _lib.MF_EPOCH_XCD_SHIFT) |
+                      (_lib.MF_EPOCH_ERR_IN_ROW if self.err_in_row else 0), self.dtype, st)
         else:
             _lib.call("mf_log_reduce", ctypes.c_void_p(self._qlog_base), self.ldq, self.K + 1,
                       self._ptr(lg["perm"]), self._ptr(lg["pb"]), lg["n_pieces"],

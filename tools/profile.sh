@@ -1,7 +1,8 @@
 # usage (on the GPU box): bash tools/profile.sh TAG [extra bench args, e.g. --algo svdpp]
 # 1) kernel trace + stats of the bench; 2) FETCH_SIZE and WRITE_SIZE in separate --pmc passes
-#    (MI355X_MICROARCH.md HBM/rocprofv3: one TCC counter group per pass); 3) summary json with the
-#    HBM bytes of one step summed over every kernel (profiles/traffic_<algo>_k<K>_<shape>.json).
+#    (MI355X_MICROARCH.md HBM/rocprofv3: one TCC counter group per pass), 3) TCC hit / miss;
+# then python3 tools/summarize_prof.py TAG (here, after the merge) writes profiles/TAG_* and
+# profiles/traffic_<algo>_k<K>_<shape>.json (HBM bytes of one step summed over every kernel).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -11,6 +12,7 @@ EXTRA="$*"
 mkdir -p gpurun_out
 B="bench.py --no-cpu-baseline --no-rmse --no-svdpp"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 $B --steps 20 --warmup 3 $EXTRA > gpurun_out/prof_${TAG}_bench.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d gpurun_out/pmc_fetch_$TAG -o run -- python3 $B --steps 5 --warmup 1 $EXTRA > gpurun_out/pmc_fetch_${TAG}.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d gpurun_out/pmc_write_$TAG -o run -- python3 $B --steps 5 --warmup 1 $EXTRA > gpurun_out/pmc_write_${TAG}.log 2>&1 || exit $?
-python3 tools/summarize_prof.py $TAG
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d gpurun_out/pmc_fetch_$TAG -o run -- python3 $B --steps 5 --warmup 1 $EXTRA > gpurun_out/pmc_fetch_${TAG}.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d gpurun_out/pmc_write_$TAG -o run -- python3 $B --steps 5 --warmup 1 $EXTRA > gpurun_out/pmc_write_${TAG}.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -T --output-format csv -d gpurun_out/pmc_l2_$TAG -o run -- python3 $B --steps 5 --warmup 1 $EXTRA > gpurun_out/pmc_l2_${TAG}.log 2>&1 || exit $?
+echo "profile $TAG done"

@@ -9,6 +9,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
+PMC_STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 11  # warmup + timed + phase steps of a --pmc run
+SETUP = ("elementwise", "rocclr", "user_sq_kernel", "fill")  # one-off setup kernels, not in a step
 out = os.path.join(ROOT, "gpurun_out")
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
@@ -61,31 +63,36 @@ write = pmc("write", "WRITE_SIZE")
 summary["FETCH_SIZE_kib"] = fetch
 summary["WRITE_SIZE_kib"] = write
 # HBM-side bytes, corrected as MI355X_MICROARCH.md (HBM) prescribes: FETCH_SIZE tallies 128-B read
-# requests at 64 B on gfx950 -> x2; WRITE_SIZE is exact.  One step = the dispatches of every
-# kernel per epoch-kernel dispatch (the PMC runs time warmup + steps epochs and nothing else).
+# requests at 64 B on gfx950 -> x2; WRITE_SIZE is exact.  One step = every dispatch of the PMC run
+# (PMC_STEPS epochs, nothing else) / PMC_STEPS, setup kernels listed apart.
 bench_line = summary.get("bench_line_under_profiler")
-if fetch and write and bench_line and EPOCH in fetch and EPOCH in write:
-    per = {}
-    n_epoch = fetch[EPOCH]["dispatches"]
+if fetch and write and bench_line:
+    per, setup = {}, {}
     for k in sorted(set(fetch) & set(write)):
-        d = fetch[k]["dispatches"] / n_epoch  # dispatches per step
+        d = fetch[k]["dispatches"] / PMC_STEPS  # dispatches per step
         fb = 2 * fetch[k]["mean_per_dispatch"] * 1024 * d
         wb = write[k]["mean_per_dispatch"] * 1024 * d
-        per[k] = {"dispatches_per_step": d, "read_bytes": fb, "write_bytes": wb,
-                  "bytes_per_step": fb + wb}
+        row = {"dispatches_per_step": d, "read_bytes": fb, "write_bytes": wb,
+               "bytes_per_step": fb + wb}
+        (setup if any(x in k for x in SETUP) else per)[k] = row
     total = sum(v["bytes_per_step"] for v in per.values())
     cfg = bench_line["config"]
     n_up = bench_line["roofline"]["updates_per_step"]
     traffic = {"bytes_per_step": total, "bytes_per_update": total / n_up,
                "algorithmic_bytes_per_update": bench_line["roofline"]["algorithmic_bytes_per_update"],
-               "per_kernel": per,
+               "per_kernel": per, "setup_kernels_excluded": setup,
                "source": "profiles/%s_summary.json (2 x FETCH_SIZE + WRITE_SIZE, separate --pmc "
-                         "passes, every kernel of the step)" % tag,
+                         "passes of %d epochs, every kernel of the step)" % (tag, PMC_STEPS),
                "workload": cfg["workload"]}
     summary["traffic"] = traffic
     name = "traffic_%s_k%d_%s.json" % (cfg["algo"], cfg["n_factors"], cfg.get("shape", "ml-1m"))
     with open(os.path.join(prof, name), "w") as f:
         json.dump(traffic, f, indent=1)
+hit, miss = pmc("l2", "TCC_HIT_sum"), pmc("l2", "TCC_MISS_sum")
+if hit and miss:
+    summary["l2_hit_rate"] = {k: hit[k]["mean_per_dispatch"] / max(1.0, hit[k]["mean_per_dispatch"] +
+                                                                    miss[k]["mean_per_dispatch"])
+                              for k in sorted(set(hit) & set(miss))}
 with open(os.path.join(prof, "%s_summary.json" % tag), "w") as f:
     json.dump(summary, f, indent=1)
 print(json.dumps(summary, indent=1)[:4000])
