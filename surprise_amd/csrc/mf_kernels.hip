@@ -2905,13 +2905,23 @@ __global__ __launch_bounds__(kBlock) void y_apply_kernel(
             const int c = lane + kWave * v;
             y[v] = c < K ? yj[j * ldu + c] : T(0);
         }
-        for (int p = p0; p < p1; ++p) {
-            const T A = pc_A[p];
+        constexpr int kP = 8;  // pieces' rows in flight (a popular item has ~60 pieces)
+        for (int p = p0; p < p1; p += kP) {
+            T A[kP], g[kP][V];
 #pragma unroll
-            for (int v = 0; v < V; ++v) {
-                const int c = lane + kWave * v;
-                y[v] = A * y[v] + (c < K ? pc_c[(int64_t)p * ldu + c] : T(0));
+            for (int a = 0; a < kP; ++a) {
+                const bool ok = p + a < p1;
+                A[a] = ok ? pc_A[p + a] : T(1);  // (past the item: the identity map)
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    const int c = lane + kWave * v;
+                    g[a][v] = ok && c < K ? pc_c[(int64_t)(p + a) * ldu + c] : T(0);
+                }
             }
+#pragma unroll
+            for (int a = 0; a < kP; ++a)  // composed in piece order
+#pragma unroll
+                for (int v = 0; v < V; ++v) y[v] = A[a] * y[v] + g[a][v];
         }
 #pragma unroll
         for (int v = 0; v < V; ++v) {
