@@ -382,7 +382,8 @@ def main():
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
         "kernel": "one epoch step (%s): %s" % (
-            mode, "sumsq + mf_epoch_kernel + log_replay_kernel + log_apply_kernel" if mode == "log"
+            mode, "mf_ckpt_epoch_kernel (heavy + light users) + log_replay_kernel (both groups) "
+                  "+ log_apply_kernel" if mode == "log"
             else "mf_epoch_kernel + y fold (+ merge)"),
         "algorithmic_bytes_per_update": B, "updates_per_step": n_train,
         "algorithmic_bytes_per_step": bytes_step,
