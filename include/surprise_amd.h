@@ -161,13 +161,14 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
  * holds p_{c_k + 1}: for k = c_k + 1 the row itself, for k = c_k the epoch kernel's step undone,
  * p_k = (row - err_k * lr_pu * q_{item(k)}) / ap (ap = 1 - lr_pu * reg_pu on factor columns;
  * q from the snapshot table qb; every rating of a piece has the same item) -- call it before
- * mf_log_apply.  Requires ldq * sizeof(dtype) <= 1 KiB.  flags: bits 8..15 an XCD mask as in
- * mf_svd_epoch (MF_EPOCH_XCD_SHIFT), 0 = every XCD.
+ * mf_log_apply.  piece_item (nullable): the item of each piece (else read through perm and the
+ * CSR items).  Requires ldq * sizeof(dtype) <= 1 KiB.  flags: bits 8..15 an XCD mask as in
+ * mf_svd_epoch (MF_EPOCH_XCD_SHIFT), 0 = every XCD; MF_EPOCH_ERR_IN_ROW: errors in the rows.
  */
 int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_factors,
                   const mf_csr_t *csr, const void *qb, const mf_hyper_t *hp, const int32_t *perm,
                   const int32_t *ck_pos, const int32_t *piece_beg, int64_t n_pieces, void *sums,
-                  int32_t flags, int32_t dtype, void *stream);
+                  const int32_t *piece_item, int32_t flags, int32_t dtype, void *stream);
 
 /*
  * mf_svd_epoch in MF_MODE_LOG with the checkpoint log (elog != NULL, the lookahead body), also

@@ -58,7 +58,7 @@ SIGNATURES = {
     "mf_user_sq_reduce": [_vp, _i64, _i32, _vp, _vp],
     "mf_log_reduce": [_vp, _i32, _i32, _vp, _vp, _i64, _vp, _i32, _vp],
     "mf_log_replay": [_vp, _vp, _i32, _i32, ctypes.POINTER(MfCsr), _vp,
-                      ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _i32, _i32, _vp],
+                      ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _vp],
     "mf_ckpt_interval": [],
     "mf_log_apply": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
                      ctypes.POINTER(MfHyper), _vp, _i32, _vp, _i32, _vp, _vp, _i64, _i32, _vp],

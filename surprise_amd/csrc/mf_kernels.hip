@@ -1985,7 +1985,7 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T inv_ap,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
     const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int xmask,
-    int err_col)
+    int err_col, const int32_t *__restrict__ piece_item)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -2019,7 +2019,8 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
         // err_k: gathered from elog, or (err_col > 0) read from the row below
         const T ek_l = lane < cnt && err_col <= 0 ? elog[k_l] : T(0);  // lanes >= cnt: weight 0
         // the piece's item row (snapshot) -> D = lrp o q_i
-        const uint32_t qoff = (uint32_t)items[readlane(k_l, 0)] * qrow;
+        // (piece_item: the item id without the perm -> items hop on the piece's critical path)
+        const uint32_t qoff = (uint32_t)(piece_item ? piece_item[pc] : items[readlane(k_l, 0)]) * qrow;
         vec D[G];
 #pragma unroll
         for (int v = 0; v < G; ++v) D[v] = lrp[v] * L::template lds<0>(q_rs, cq[v], qoff);
@@ -3295,7 +3296,7 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
 int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_factors,
                   const mf_csr_t *csr, const void *qb, const mf_hyper_t *hp, const int32_t *perm,
                   const int32_t *ck_pos, const int32_t *piece_beg, int64_t n_pieces, void *sums,
-                  int32_t flags, int32_t dtype, void *stream)
+                  const int32_t *piece_item, int32_t flags, int32_t dtype, void *stream)
 {
     if (n_pieces < 0 || ldq < n_factors + 1 || n_factors < 0) return set_err(MF_E_ARG, "bad shape");
     const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
@@ -3321,7 +3322,8 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
                                    (const T *)qlog, (const T *)elog, ldq, n_factors, csr->items,
                                    (const T *)qb, csr->n_items, (T)hp->lr_pu,
                                    (T)(1.0 / (1.0 - hp->lr_pu * hp->reg_pu)), perm,
-                                   ck_pos, piece_beg, n_pieces, (T *)sums, xmask, err_col);
+                                   ck_pos, piece_beg, n_pieces, (T *)sums, xmask, err_col,
+                                   piece_item);
                 return check_launch("log_replay_kernel");
             }
         });

@@ -350,6 +350,9 @@ class MFEngine(ItemSync, Predictor):
                           n_pieces=len(pb) - 1, cnt=cnt)
                 if self.ckpt:
                     lg["ck"] = to_dev(ckpt_positions(row_ptr, perm, C, pos_user()))
+                    # the item of every piece (mf_log_replay's piece_item)
+                    lg["pitem"] = to_dev(np.repeat(np.arange(self.n_items, dtype=np.int32),
+                                                   np.diff(ipp)))
                 lgs.append(lg)
             if self.ckpt and self.lpt > 0 and len(parts[0]) <= self.LPT_MAX_USERS:
                 # the (light) group's epoch as LPT chains: lpt waves per SIMD of its XCDs, each
@@ -687,7 +690,7 @@ class MFEngine(ItemSync, Predictor):
                       ctypes.c_void_p(self._elog_base), self.ldq, self.K, ctypes.byref(self._csr),
                       self._ptr(self.qb), ctypes.byref(self._hyper), self._ptr(lg["perm"]),
                       self._ptr(lg["ck"]), self._ptr(lg["pb"]), lg["n_pieces"],
-                      ctypes.c_void_p(sums_ptr),
+                      ctypes.c_void_p(sums_ptr), self._ptr(lg["pitem"]),
                       (xmask << _lib.MF_EPOCH_XCD_SHIFT) |
                       (_lib.MF_EPOCH_ERR_IN_ROW if self.err_in_row else 0), self.dtype, st)
         else:

@@ -39,8 +39,8 @@ def test_version_and_error_without_device(lib):
     rc = lib.mf_svd_epoch(ctypes.byref(csr), None, 1, None, None, 16, None, 16, 10, 1, None,
                           0, None, None, 0, 0, 0, None)
     assert rc == 1001 and b"null csr" in lib.mf_last_error()
-    rc = lib.mf_log_replay(None, None, 16, 10, None, None, None, None, None, None, 3, None, 0, 0,
-                           None)
+    rc = lib.mf_log_replay(None, None, 16, 10, None, None, None, None, None, None, 3, None, None,
+                           0, 0, None)
     assert rc == 1001 and b"null argument" in lib.mf_last_error()
     assert lib.mf_ckpt_interval() in (2, 4, 8, 16)
     rc = lib.mf_log_apply(None, 10, 16, 10, 10, None, None, None, None, None, None, None, 1, None,

@@ -400,6 +400,60 @@ def test_heavy_user_split_matches_single_launch(torch, u1):
         np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=1e-10, err_msg=k)
 
 
+@pytest.mark.parametrize("K,dtype,heavy", [(100, "float32", 0.25), (20, "float64", 0.0),
+                                            (61, "float64", 0.25)])
+def test_errors_in_checkpoint_rows_equal_elog(torch, u1, K, dtype, heavy):
+    """MF_EPOCH_ERR_IN_ROW (each pair's errors stored in its checkpoint row's padding, read back
+    by the replay from the loaded row) against the errors in elog: the same values reach the same
+    operations, so the fits are bit-identical (split and unsplit chunks)."""
+    from surprise_amd.engine import MFEngine
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
+                 reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    rng = np.random.RandomState(2)
+    pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
+    out = []
+    for in_row in (True, False):
+        eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype=dtype,
+                       mode="log", heavy=heavy)
+        assert eng.ckpt and eng.err_in_row
+        eng.err_in_row = in_row
+        eng.set_factors(pu0, qi0)
+        eng.run_epochs(3)
+        out.append(eng.get_factors())
+    for k in ("pu", "qi", "bu", "bi"):
+        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
+
+
+def test_user_sq_statistic_equals_sumsq(torch, u1):
+    """<pu^2> for the next chunk, summed from the epoch kernel's per-user |p_u|^2 inside
+    mf_log_apply, equals mf_sumsq over the updated pu (fp64, up to summation order)."""
+    import ctypes
+    from surprise_amd import _lib
+    from surprise_amd.engine import MFEngine
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    K = 40
+    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
+                 reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    rng = np.random.RandomState(3)
+    eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype="float64",
+                   mode="log", n_chunks=2, heavy=0.25)
+    eng.set_factors(rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K)))
+    for c in (0, 1, 0):
+        eng.run_chunk(c)
+        eng.sync_items(None)
+        nxt = eng._works[eng._wt % 2].cpu().numpy()
+        ref = torch.zeros(2, dtype=torch.float64, device="cuda")
+        _lib.call("mf_sumsq", ctypes.c_void_p(eng.pu.data_ptr()), eng.n_users, K, eng.ld,
+                  ctypes.c_void_p(ref.data_ptr()), _lib.MF_F64,
+                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        ref = ref.cpu().numpy()
+        assert nxt[1] == ref[1] == ts.n_users * K
+        assert abs(nxt[0] - ref[0]) <= 1e-12 * ref[0], (nxt, ref)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("K", [20, 100, 130])
 def test_svdpp_y_fold_equals_sequential_composition(torch, K):
