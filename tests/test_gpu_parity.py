@@ -347,13 +347,15 @@ def test_zero_epochs_and_single_rating_users(torch):
 
 
 @pytest.mark.parametrize("K,dtype,chunks", [(20, "float64", 1), (20, "float64", 3),
-                                            (100, "float64", 2), (100, "float32", 1)])
+                                            (100, "float64", 2), (100, "float32", 1),
+                                            (127, "float32", 2)])
 def test_checkpoint_log_matches_gradient_log(torch, u1, K, dtype, chunks):
-    """The checkpoint log (a user row every mf_ckpt_interval() ratings + err per rating,
-    mf_log_replay rebuilding the gradients, <pu^2> summed inside the replay) against the
-    gradient log (a whole gradient row per rating, mf_log_reduce, mf_sumsq): the same epochs from
-    the same state.  Same arithmetic up to the summation of the statistic and one FMA
-    contraction per rating: fp64 within 1e-10, fp32 within 1e-5."""
+    """The checkpoint log (one user row per pair of ratings, errors in the rows' padding -- or in
+    elog where the row has no room, K=127 fp32 --, mf_log_replay rebuilding the gradients by
+    undoing one step, <pu^2> from user_sq) against the gradient log (a whole gradient row per
+    rating, mf_log_reduce, mf_sumsq): the same epochs from the same state.  Same arithmetic up
+    to the summation of the statistic and one rounding per rating: fp64 within 1e-10, fp32
+    within 1e-5."""
     from surprise_amd import _lib
     from surprise_amd.engine import MFEngine
     ts, _ = u1
@@ -367,6 +369,7 @@ def test_checkpoint_log_matches_gradient_log(torch, u1, K, dtype, chunks):
         eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype=dtype,
                        mode="log", n_chunks=chunks, ckpt=ck)
         assert eng.ckpt == ck
+        assert eng.err_in_row == (ck and K != 127)
         eng.set_factors(pu0, qi0)
         eng.run_epochs(4)
         out.append(eng.get_factors())
