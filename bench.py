@@ -198,6 +198,7 @@ def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
         for c in range(eng.n_chunks):
             eng.run_chunk(c)
             eng.sync_items(ctx)
+    t_enq = time.perf_counter() - t0  # (the host's enqueue time: below elapsed unless host-bound)
     torch.cuda.synchronize()
     if ctx is not None:
         ctx.barrier()
@@ -212,13 +213,13 @@ def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
             ev["done"].record(eng.stream)
             recs.append(ev)
     torch.cuda.synchronize()
-    phases = {}
+    phases = {"host_enqueue_ms": t_enq / max(steps, 1) * 1e3}
     if recs:
         span = lambda a, b: float(np.mean([e[a].elapsed_time(e[b]) for e in recs]))
         n = eng.n_chunks
-        phases = {"pre_ms": span("begin", "start") * n, "epoch_kernel_ms": span("start", "end") * n,
+        phases.update({"pre_ms": span("begin", "start") * n, "epoch_kernel_ms": span("start", "end") * n,
                   "replay_ms": span("end", "end_r") * n, "fold_sync_ms": span("end_r", "done") * n,
-                  "step_gpu_ms": span("begin", "done") * n, "instrumented_steps": len(recs) // n}
+                  "step_gpu_ms": span("begin", "done") * n, "instrumented_steps": len(recs) // n})
     return elapsed, phases
 
 

@@ -363,6 +363,20 @@ const char *mf_last_error(void);
  * from the sources next to it. */
 const char *mf_source_hash(void);
 
+/* ---- stream ordering without marker packets (the two-stream SVD step)
+ * A HIP event recorded on a stream is a marker packet in its queue; the kernel queued after it
+ * starts ~7 us late.  mf_launch_event(ev) binds ev to the NEXT mf_log_apply / mf_log_replay
+ * launch of the calling thread as that dispatch's stop event (hipExtLaunchKernel): ev completes
+ * with the kernel and the queue holds no marker.  The others are thin wrappers so that a
+ * binding needs no HIP headers: create / destroy / record an event (timing disabled), and make
+ * a stream wait for one.  Replace the torch.cuda.Event record / wait_event pairs of the
+ * engine's fork / join (no reference counterpart: the reference is single-threaded). */
+int mf_event_create(void **event);
+int mf_event_destroy(void *event);
+int mf_event_record(void *event, void *stream);
+int mf_stream_wait_event(void *stream, void *event);
+int mf_launch_event(void *event);
+
 #ifdef __cplusplus
 }
 #endif

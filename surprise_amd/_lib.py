@@ -79,6 +79,11 @@ SIGNATURES = {
     "mf_svdpp_user_implicit": [ctypes.POINTER(MfCsr), _vp, _i32, _vp, _i32, _i32, _vp],
     "mf_selftest_wave_sum": [_vp, _vp, _i32, _i32, _vp],
     "mf_selftest_xcc": [_vp, _i32, _vp],
+    "mf_event_create": [ctypes.POINTER(ctypes.c_void_p)],
+    "mf_event_destroy": [_vp],
+    "mf_event_record": [_vp, _vp],
+    "mf_stream_wait_event": [_vp, _vp],
+    "mf_launch_event": [_vp],
     "mf_version": [],
     "mf_last_error": [],
     "mf_source_hash": [],

@@ -20,6 +20,7 @@
 //     (no LDS round trip), leaving the sum in every lane.
 // No MFMA: the path is gather/scatter-bound.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -1707,6 +1708,8 @@ template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
 
 namespace mf_ext {
 thread_local char g_err[256] = "";
+// mf_launch_event: the event the next mf_log_apply / mf_log_replay launch of this thread signals
+thread_local hipEvent_t g_stop_event = nullptr;
 }
 
 namespace {
@@ -2091,49 +2094,79 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     int apply, double *__restrict__ stat_next, const double *__restrict__ user_sq, int64_t n_sq,
     int sq_cols)
 {
-    if (stat_next && blockIdx.x == 0) {
-        if (user_sq) {  // the next chunk's {sum |p_u|^2, count} (every epoch kernel has finished)
+    // the next chunk's {sum |p_u|^2, count}: the launch's extra last block (every epoch kernel
+    // has finished), so that no item block waits behind the sum
+    if (stat_next && blockIdx.x == gridDim.x - 1) {
+        if (user_sq) {
             block_sum_sq(user_sq, n_sq, sq_cols, stat_next);
         } else if (threadIdx.x < 2) {
             stat_next[threadIdx.x] = 0.0;  // (cleared for the next chunk's mf_sumsq)
         }
+        return;
     }
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    const int64_t n_waves = ((int64_t)(gridDim.x - (stat_next ? 1 : 0)) * kBlock) / kWave;
     double eta_fac = 0, l_fac = 0, l_bias = 0;
     if (count_rule) {
         eta_fac = lr_fac * (p2stat[0] / p2stat[1] + reg_fac);
         l_fac = log1p(-eta_fac);
         l_bias = log1p(-eta_bias);
     }
+    constexpr int kU = MF_APPLY_U;  // independent piece loads in flight per group
     for (int64_t i = wave; i < n_items; i += n_waves) {
+        // every load that does not depend on another first: both groups' piece ranges, the
+        // count and the item row; then the first kU pieces of each group together
+        const int a0 = item_piece_ptr ? item_piece_ptr[i] : (int)i;
+        const int a1 = item_piece_ptr ? item_piece_ptr[i + 1] : (int)i + 1;
+        const int b0 = sums2 ? item_piece_ptr2[i] : 0, b1 = sums2 ? item_piece_ptr2[i + 1] : 0;
+        const double N = totals ? (double)totals[i] : 0.0;
+        T q[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const int c = lane + kWave * v;
+            q[v] = apply && c < ld ? qb[i * ld + c] : T(0);
+        }
+        auto load = [&](const T *__restrict__ sp, int pc, int p1, T (&g)[kU][V]) {
+#pragma unroll
+            for (int a = 0; a < kU; ++a)
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    g[a][v] = (pc + a < p1 && lane + kWave * v < ld)
+                                  ? sp[(int64_t)(pc + a) * ld + lane + kWave * v] : T(0);
+        };
         T acc[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) acc[v] = T(0);
+        auto add = [&](T (&g)[kU][V]) {
+#pragma unroll
+            for (int a = 0; a < kU; ++a)
+#pragma unroll
+                for (int v = 0; v < V; ++v) acc[v] += g[a][v];
+        };
         // the item's pieces in sums, then (split log) its pieces in sums2, in that fixed order
-        for (int part = 0; part < (sums2 ? 2 : 1); ++part) {
-            const T *__restrict__ sp = part ? sums2 : sums;
-            const int32_t *__restrict__ ipp = part ? item_piece_ptr2 : item_piece_ptr;
-            const int p0 = ipp ? ipp[i] : (int)i;
-            const int p1 = ipp ? ipp[i + 1] : (int)i + 1;
-            constexpr int kU = MF_APPLY_U;  // independent loads in flight
-            for (int pc = p0; pc < p1; pc += kU) {
-                T g[kU][V];
-#pragma unroll
-                for (int a = 0; a < kU; ++a)
-#pragma unroll
-                    for (int v = 0; v < V; ++v)
-                        g[a][v] = (pc + a < p1 && lane + kWave * v < ld)
-                                      ? sp[(int64_t)(pc + a) * ld + lane + kWave * v] : T(0);
-#pragma unroll
-                for (int a = 0; a < kU; ++a)
-#pragma unroll
-                    for (int v = 0; v < V; ++v) acc[v] += g[a][v];
+        T ga[kU][V], gb[kU][V];
+        load(sums, a0, a1, ga);
+        if (sums2) load(sums2, b0, b1, gb);
+        add(ga);
+        for (int pc = a0 + kU; pc < a1; pc += kU) {
+            load(sums, pc, a1, ga);
+            add(ga);
+        }
+        if (sums2) {
+            add(gb);
+            for (int pc = b0 + kU; pc < b1; pc += kU) {
+                load(sums2, pc, b1, gb);
+                add(gb);
             }
         }
-        const double N = totals ? (double)totals[i] : 0.0;
+        // the count-aware weights (one per column kind, the same for every factor column)
+        double w_fac = 1.0, w_bias = 1.0;
+        if (count_rule && N > 1.0) {
+            w_fac = -expm1(N * l_fac) / (N * eta_fac);
+            w_bias = -expm1(N * l_bias) / (N * eta_bias);
+        }
 #pragma unroll
         for (int v = 0; v < V; ++v) {
             const int c = lane + kWave * v;
@@ -2142,13 +2175,10 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
             if (delta_out) delta_out[x] = acc[v];
             if (apply && (c < n_fac || c == bias_col)) {
                 const bool b = c == bias_col;
-                double w = 1.0;
-                if (count_rule && N > 1.0)
-                    w = -expm1(N * (b ? l_bias : l_fac)) / (N * (b ? eta_bias : eta_fac));
+                const double w = b ? w_bias : w_fac;
                 // the log holds gradients g_k = err_k pe_k: sum_k d_k = lr (S - N reg q)
-                const T q = qb[x];
-                const T d = (T)(b ? lr_b : lr_f) * (acc[v] - (T)N * (T)(b ? reg_b : reg_f) * q);
-                qb[x] = q + (T)w * d;
+                const T d = (T)(b ? lr_b : lr_f) * (acc[v] - (T)N * (T)(b ? reg_b : reg_f) * q[v]);
+                qb[x] = q[v] + (T)w * d;
             }
         }
     }
@@ -3168,6 +3198,27 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
     return dtype == MF_F32 ? by_mode(float{}) : by_mode(double{});
 }
 
+// hipLaunchKernelGGL, or -- after mf_launch_event(ev) on this thread -- the same launch with ev
+// bound to the dispatch as its stop event (hipExtLaunchKernelGGL): ev completes with the kernel,
+// no marker packet follows it in the queue (a marker costs the next kernel ~7 us of queue time)
+// The pending event is taken at the entry point (StopEvent); an entry point that returns without
+// launching records it on its stream instead, so "ev completes after the call's work" holds.
+struct StopEvent {
+    hipEvent_t ev;
+    hipStream_t st;
+    explicit StopEvent(void *stream) : ev(mf_ext::g_stop_event), st((hipStream_t)stream) { mf_ext::g_stop_event = nullptr; }
+    ~StopEvent() { if (ev) (void)hipEventRecord(ev, st); }
+    hipEvent_t take() { hipEvent_t e = ev; ev = nullptr; return e; }
+};
+
+template <typename F, typename... Args>
+void launch_ev(hipEvent_t ev, F kernel, dim3 grid, dim3 block, hipStream_t st, Args... args) {
+    if (ev)
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, st, nullptr, ev, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
+}
+
 int elementwise_grid(int64_t total) {
     int64_t b = (total + kBlock - 1) / kBlock;
     if (b > 8192) b = 8192;
@@ -3190,6 +3241,46 @@ static const char kSourceHash[] = "surprise_amd-src-sha256:" MF_SOURCE_HASH;
 const char *mf_source_hash(void) { return kSourceHash + 24; }
 
 const char *mf_last_error(void) { return g_err; }
+
+int mf_event_create(void **event)
+{
+    if (!event) return set_err(MF_E_ARG, "null event");
+    hipEvent_t ev = nullptr;
+    if (const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming); e != hipSuccess)
+        return set_err((int)e, "hipEventCreateWithFlags failed");
+    *event = (void *)ev;
+    return 0;
+}
+
+int mf_event_destroy(void *event)
+{
+    if (!event) return 0;
+    if (const hipError_t e = hipEventDestroy((hipEvent_t)event); e != hipSuccess)
+        return set_err((int)e, "hipEventDestroy failed");
+    return 0;
+}
+
+int mf_event_record(void *event, void *stream)
+{
+    if (!event) return set_err(MF_E_ARG, "null event");
+    if (const hipError_t e = hipEventRecord((hipEvent_t)event, (hipStream_t)stream); e != hipSuccess)
+        return set_err((int)e, "hipEventRecord failed");
+    return 0;
+}
+
+int mf_stream_wait_event(void *stream, void *event)
+{
+    if (!event) return set_err(MF_E_ARG, "null event");
+    if (const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0); e != hipSuccess)
+        return set_err((int)e, "hipStreamWaitEvent failed");
+    return 0;
+}
+
+int mf_launch_event(void *event)
+{
+    mf_ext::g_stop_event = (hipEvent_t)event;
+    return 0;
+}
 
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
@@ -3298,6 +3389,7 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
                   const int32_t *ck_pos, const int32_t *piece_beg, int64_t n_pieces, void *sums,
                   const int32_t *piece_item, int32_t flags, int32_t dtype, void *stream)
 {
+    StopEvent stop(stream);  // (mf_launch_event)
     if (n_pieces < 0 || ldq < n_factors + 1 || n_factors < 0) return set_err(MF_E_ARG, "bad shape");
     const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
     if (n_pieces == 0) return 0;
@@ -3318,7 +3410,7 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
             if constexpr (V > kLaMaxG) {
                 return set_err(MF_E_UNSUPPORTED, "checkpoint log: row too long");
             } else {
-                hipLaunchKernelGGL((log_replay_kernel<T, V>), dim3(g), dim3(kBlock), 0, st,
+                launch_ev(stop.take(), (log_replay_kernel<T, V>), dim3(g), dim3(kBlock), st,
                                    (const T *)qlog, (const T *)elog, ldq, n_factors, csr->items,
                                    (const T *)qb, csr->n_items, (T)hp->lr_pu,
                                    (T)(1.0 / (1.0 - hp->lr_pu * hp->reg_pu)), perm,
@@ -3375,6 +3467,7 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
                  double *stat_next, const double *user_sq, int64_t n_users, int32_t dtype,
                  void *stream)
 {
+    StopEvent stop(stream);  // (mf_launch_event)
     if (stat_next && stat_next == p2stat) return set_err(MF_E_ARG, "stat_next aliases p2stat");
     if (user_sq && (!stat_next || n_users < 0)) return set_err(MF_E_ARG, "user_sq needs stat_next");
     if (sums2 && !item_piece_ptr2) return set_err(MF_E_ARG, "sums2 needs item_piece_ptr2");
@@ -3387,7 +3480,8 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
     if (apply && (!totals || !hp)) return set_err(MF_E_ARG, "apply needs totals and hp");
     if (n_items == 0 || (!apply && !delta_out)) return 0;
     if (!sums || (apply && !qb)) return set_err(MF_E_ARG, "null argument");
-    const int g = grid_for_waves(default_waves(n_items));
+    // (+1: the block that sums / clears stat_next)
+    const int g = grid_for_waves(default_waves(n_items)) + (stat_next ? 1 : 0);
     hipStream_t st = (hipStream_t)stream;
     const double eta_b = count_rule ? hp->lr_bi * (1.0 + hp->reg_bi) : 0.0;
     const double lr_c = count_rule ? hp->lr_qi : 0.0, reg_c = count_rule ? hp->reg_qi : 0.0;
@@ -3396,7 +3490,7 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
         return dispatch_v<T>(ld, [&](auto vc) -> int {
-            hipLaunchKernelGGL((log_apply_kernel<T, decltype(vc)::value>), dim3(g), dim3(kBlock), 0,
+            launch_ev(stop.take(), (log_apply_kernel<T, decltype(vc)::value>), dim3(g), dim3(kBlock),
                                st, (T *)qb, n_items, ld, n_factors, bias_col, (const T *)sums,
                                item_piece_ptr, (const T *)sums2, item_piece_ptr2, totals,
                                count_rule, eta_b, lr_c, reg_c, lr_f,

@@ -19,11 +19,25 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
 from . import _lib
 from .dist import ItemSync, chunk_users, item_counts
+
+
+def _new_event():
+    """A native HIP event (timing disabled) for the engine's fork / join."""
+    ev = ctypes.c_void_p()
+    _lib.call("mf_event_create", ctypes.byref(ev))
+    return ev
+
+
+def _free_events(evs):
+    lib = _lib.load()
+    for ev in evs:
+        lib.mf_event_destroy(ev)
 
 PIECE_ROWS = 64  # log rows summed by one wave of mf_log_reduce
 SVDPP_WAVES_PER_CU = int(os.environ.get("SURPRISE_AMD_SVDPP_WPC", "4"))
@@ -156,6 +170,7 @@ class Predictor:
 
     def user_implicit(self):
         """imp[u] = sum_{j in I_u} yj[j] / sqrt|I_u| on device (SVDpp.estimate :518-520)."""
+        self._fork_bound = False  # (main-stream work after the last fold: MFEngine's fork)
         imp = self.torch.zeros(self.n_users, self.ld, dtype=self.tdt, device=self.dev)
         _lib.call("mf_svdpp_user_implicit", ctypes.byref(self._csr), self._ptr(self.yj),
                   self.ld, self._ptr(imp), self.K, self.dtype,
@@ -163,6 +178,7 @@ class Predictor:
         return imp
 
     def _predict_dev(self, u, i, global_mean, imp=None):
+        self._fork_bound = False
         t = self.torch
         n = len(u)
         du = t.from_numpy(np.ascontiguousarray(u, np.int32)).to(self.dev)
@@ -323,6 +339,10 @@ class MFEngine(ItemSync, Predictor):
         self.heavy_xcd = int(os.environ.get("SURPRISE_AMD_HEAVY_XCD", "1"), 0) & 0xFF
         self.lpt = int(os.environ.get("SURPRISE_AMD_LPT", str(self.LPT_PER_SIMD)))
         self.heavy_replay_all = os.environ.get("SURPRISE_AMD_HEAVY_REPLAY_ALL", "1") != "0"
+        # rows per piece of the heavy group's log (its replay runs on the step's longest path)
+        self.heavy_piece = int(os.environ.get("SURPRISE_AMD_HEAVY_PIECE", str(PIECE_ROWS)))
+        if not 1 <= self.heavy_piece <= PIECE_ROWS:
+            raise ValueError("SURPRISE_AMD_HEAVY_PIECE must be in [1, %d]" % PIECE_ROWS)
         # checkpoint log with MF_EPOCH_ERR_IN_ROW where the row has room: each pair's two errors
         # ride in its checkpoint row's padding (the replay gathers no elog entries)
         e0 = ((self.K + 2) & ~1) if self.dtype == _lib.MF_F32 else self.K + 1
@@ -332,6 +352,14 @@ class MFEngine(ItemSync, Predictor):
         _pu = []
         pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
         self.side = torch.cuda.Stream(device=dev) if self.ckpt and heavy > 0 else None
+        # the fork / join between the two streams as native events bound to the kernels that
+        # complete them (mf_launch_event: no marker packet in the main stream's queue);
+        # SURPRISE_AMD_NATIVE_EVENTS=0: torch.cuda.Event record / wait_event
+        self._nev = None
+        if self.side is not None and os.environ.get("SURPRISE_AMD_NATIVE_EVENTS", "1") != "0":
+            self._nev = {k: _new_event() for k in ("fork", "join")}
+            weakref.finalize(self, _free_events, list(self._nev.values()))
+        self._fork_bound = False  # the last mf_log_apply on the main stream completes "fork"
         self.sched = []
         self._totals_local = []
         self.logs = []  # "log" mode: per chunk, the item grouping of the log (log_layout)
@@ -344,8 +372,9 @@ class MFEngine(ItemSync, Predictor):
                 continue
             parts = split_heavy(c, row_ptr, heavy) if self.side is not None else [c]
             lgs = []
-            for us in parts:
-                perm, pb, ipp, cnt = log_layout(row_ptr, items, us, self.n_items)
+            for gi, us in enumerate(parts):
+                perm, pb, ipp, cnt = log_layout(row_ptr, items, us, self.n_items,
+                                                self.heavy_piece if gi else PIECE_ROWS)
                 lg = dict(sched=to_dev(us), perm=to_dev(perm), pb=to_dev(pb), ipp=to_dev(ipp),
                           n_pieces=len(pb) - 1, cnt=cnt)
                 if self.ckpt:
@@ -472,6 +501,7 @@ class MFEngine(ItemSync, Predictor):
     # ------------------------------------------------------------------ state in / out
     def set_factors(self, pu, qi, bu=None, bi=None, yj=None):
         """Upload host fp64 arrays (n, K) into the padded device tables."""
+        self._fork_bound = False  # (the side stream must wait for this work)
         t = self.torch
         K = self.K
 
@@ -497,6 +527,7 @@ class MFEngine(ItemSync, Predictor):
     def get_factors(self, ctx=None):
         """Host fp64 copies (pu, qi, bu, bi, yj) with the padding columns dropped.  With ctx
         (several ranks) pu / bu are every rank's rows gathered in rank order (all ranks)."""
+        self._fork_bound = False  # (the side stream must wait for this work)
         self.stream.synchronize()
         K = self.K
         h = lambda x: x.to(self.torch.float64).cpu().numpy()
@@ -632,6 +663,7 @@ class MFEngine(ItemSync, Predictor):
         self._wt += 1
         self.work = cur
         self._work_cleared = True  # (written, never accumulated: nothing to clear)
+        launched = True  # (a kernel on the main stream after the last mf_log_apply)
         if not self._sq_valid:
             _lib.call("mf_user_sq", self._ptr(self.pu), self.n_users, self.K, self.ld,
                       self._ptr(self.user_sq), self.dtype, st)
@@ -639,6 +671,9 @@ class MFEngine(ItemSync, Predictor):
             self._sq_valid = True
         elif self._sq_pending:  # (the previous chunk was not folded by mf_log_apply)
             self._sq_reduce(cur, st)
+        else:
+            launched = False
+        fork_bound, self._fork_bound = self._fork_bound and not launched, False
         self._sq_pending = True
         if "start" in ev:
             ev["start"].record(self.stream)
@@ -657,19 +692,30 @@ class MFEngine(ItemSync, Predictor):
             side = self.side
             sh = ctypes.c_void_p(side.cuda_stream)
             lx = (~self.heavy_xcd & 0xFF) if self.heavy_xcd else 0
-            self._ev_record("fork", self.stream)
-            self._ev_wait(side, "fork")
+            if self._nev is None:
+                self._ev_record("fork", self.stream)
+                self._ev_wait(side, "fork")
+            else:  # (bound to the previous chunk's mf_log_apply unless a kernel followed it)
+                if not fork_bound:
+                    _lib.call("mf_event_record", self._nev["fork"], st)
+                _lib.call("mf_stream_wait_event", sh, self._nev["fork"])
             n_h = hv["sched"].numel()  # (the longest path first: the host may lag the GPU)
             self._epoch_sq(hv["sched"], n_h, n_h, st, self.heavy_xcd)
             if "end" in ev:
                 ev["end"].record(self.stream)
             self._epoch_sq(ls, ln, lw, sh, lx)
+            if self._nev is not None:
+                _lib.call("mf_launch_event", self._nev["join"])  # completed by the light replay
             self._reduce_log(lg, self.sums.data_ptr(), sh, lx)
-            self._ev_record("join", side)
+            if self._nev is None:
+                self._ev_record("join", side)
             # (the heavy replay starts when the longest chain ends: by then the light users'
             # work is (nearly) done, so it may spread over every XCD)
             self._reduce_log(hv, sums_h, st, 0 if self.heavy_replay_all else self.heavy_xcd)
-            self._ev_wait(self.stream, "join")
+            if self._nev is None:
+                self._ev_wait(self.stream, "join")
+            else:
+                _lib.call("mf_stream_wait_event", st, self._nev["join"])
         if "end_r" in ev:
             ev["end_r"].record(self.stream)
 
@@ -746,6 +792,8 @@ class MFEngine(ItemSync, Predictor):
         count = self._count_rule()
         sums2 = (ctypes.c_void_p(self.sums.data_ptr() + lg["n_pieces"] * self.ldq *
                                  self.sums.element_size()) if hv is not None else None)
+        if apply:
+            self._bind_fork()
         _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K,
                   self._bias_col, self._ptr(self.sums), self._ptr(lg["ipp"]), sums2,
                   self._ptr(hv["ipp"]) if hv is not None else None,
@@ -753,6 +801,13 @@ class MFEngine(ItemSync, Predictor):
                   self._ptr(self.work), _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM,
                   None if delta_out is None else self._ptr(delta_out), int(apply),
                   *self._stat_args(apply), self.dtype, self._st())
+
+    def _bind_fork(self):
+        """The next mf_log_apply completes the "fork" event the side stream waits for (the item
+        table the next chunk's light users read); call right before that launch."""
+        if self._nev is not None:
+            _lib.call("mf_launch_event", self._nev["fork"])
+            self._fork_bound = True
 
     def _stat_args(self, apply):
         """mf_log_apply's (stat_next, user_sq, n_users): the next chunk's <pu^2> slot -- summed
@@ -843,6 +898,8 @@ class MFEngine(ItemSync, Predictor):
         if self.is_log:  # bufs[0]: the all-reduced sums, then the sum of squares of pu
             count = self._count_rule()
             self.work.copy_(bufs[0][-2:])
+            if not self._snap_tables():
+                self._bind_fork()
             _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K,
                       self._bias_col, self._ptr(bufs[0]), None, None, None,
                       self._ptr(self._totals()[c]),

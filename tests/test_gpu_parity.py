@@ -403,6 +403,41 @@ def test_heavy_user_split_matches_single_launch(torch, u1):
         np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=1e-10, err_msg=k)
 
 
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_native_fork_join_events_equal_torch_events(torch, u1, monkeypatch, chunks):
+    """The split chunk's fork / join as native events bound to the kernels that complete them
+    (mf_launch_event: the fork by the previous chunk's mf_log_apply, the join by the light
+    replay) against torch.cuda.Event record / wait_event: the same kernels in the same stream
+    order, so the fits are bit-identical -- with main-stream work (a batched predict) between
+    epochs, after which the fork must be recorded again."""
+    from surprise_amd.engine import MFEngine
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    K = 100
+    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
+                 reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    rng = np.random.RandomState(3)
+    pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
+    uu = np.arange(ts.n_users, dtype=np.int32) % ts.n_users
+    ii = np.arange(ts.n_users, dtype=np.int32) % ts.n_items
+    out = []
+    for native in ("1", "0"):
+        monkeypatch.setenv("SURPRISE_AMD_NATIVE_EVENTS", native)
+        eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype="float32",
+                       mode="log", n_chunks=chunks, heavy=0.25)
+        assert eng.logs[0]["heavy"] is not None and (eng._nev is not None) == (native == "1")
+        eng.set_factors(pu0, qi0)
+        ests = []
+        eng.run_epochs(2)
+        ests.append(eng.predict(uu, ii, ts.global_mean)[0])
+        eng.run_epochs(2)
+        f = eng.get_factors()
+        f["est"] = np.concatenate(ests)
+        out.append(f)
+    for k in ("pu", "qi", "bu", "bi", "est"):
+        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
+
+
 @pytest.mark.parametrize("K,dtype,heavy", [(100, "float32", 0.25), (20, "float64", 0.0),
                                             (61, "float64", 0.25)])
 def test_errors_in_checkpoint_rows_equal_elog(torch, u1, K, dtype, heavy):

@@ -8,5 +8,5 @@ for spec in "$@"; do
   name=${spec%%=*}; e=${spec#*=}; E=""; [ "$e" != "-" ] && E=$(echo "$e" | tr ',' ' ')
   env $E timeout -k 10 180 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/pv_${TAG}_$name -o run -- python3 bench.py --no-cpu-baseline --no-rmse --no-svdpp --steps 12 --warmup 2 $ARGS > gpurun_out/pv_${TAG}_$name.log 2>&1 || { tail -5 gpurun_out/pv_${TAG}_$name.log; exit 1; }
   echo "== $name ($e): ms/step $(cat gpurun_out/pv_${TAG}_$name.log | python3 -c 'import json,sys; print(round(json.loads([l for l in sys.stdin if l.startswith("{")][-1])["ms_per_step"],4))')"
-  python3 tools/timeline.py gpurun_out/pv_${TAG}_$name 5
+  python3 tools/timeline.py gpurun_out/pv_${TAG}_$name ${TL_N:-5}
 done
