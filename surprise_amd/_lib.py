@@ -84,6 +84,7 @@ SIGNATURES = {
     "mf_event_record": [_vp, _vp],
     "mf_stream_wait_event": [_vp, _vp],
     "mf_launch_event": [_vp],
+    "mf_launch_join": [_vp, _i32, ctypes.c_uint32],
     "mf_version": [],
     "mf_last_error": [],
     "mf_source_hash": [],

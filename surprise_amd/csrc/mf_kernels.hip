@@ -1710,6 +1710,18 @@ namespace mf_ext {
 thread_local char g_err[256] = "";
 // mf_launch_event: the event the next mf_log_apply / mf_log_replay launch of this thread signals
 thread_local hipEvent_t g_stop_event = nullptr;
+// mf_launch_join: the join role of the next mf_log_replay launch of this thread
+struct JoinArgs {
+    uint32_t *words = nullptr;
+    int role = 0;
+    uint32_t epoch = 0;
+};
+thread_local JoinArgs g_join;
+JoinArgs take_join() {
+    const JoinArgs j = g_join;
+    g_join = JoinArgs{};
+    return j;
+}
 }
 
 namespace {
@@ -1983,20 +1995,18 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
 // err (vector gathers once per piece); per rating v_readlane broadcasts, the row gather and 3
 // packed FMAs.  Two groups of MF_REPLAY_U rows are in flight per wave.
 template <typename T, int G>
-__global__ __launch_bounds__(kBlock) void log_replay_kernel(
+__device__ __forceinline__ void log_replay_body(
     const T *__restrict__ ckpt, const T *__restrict__ elog, int ldq, int K,
     const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T inv_ap,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
-    const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int xmask,
-    int err_col, const int32_t *__restrict__ piece_item)
+    const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int err_col,
+    const int32_t *__restrict__ piece_item, const int64_t wave, const int64_t n_waves)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
     constexpr int W = L::W;
     constexpr int kU = MF_REPLAY_U;
     const int lane = threadIdx.x & (kWave - 1);
-    int64_t wave, n_waves;
-    if (!wave_slot(xmask, wave, n_waves)) return;
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), q_oob = (uint32_t)n_items * qrow;
     const rsrc_t q_rs = make_rsrc(qb, q_oob);
     uint32_t cq[G];
@@ -2079,6 +2089,55 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
                 if (c0 + e < ldq) sums[pc * ldq + c0 + e] = c0 + e <= K ? L::get(acc[v], e) : T(0);
         }
     }
+}
+
+// In-kernel join of the two-stream SVD step (mf_launch_join): the light replay (role 1) and the
+// heavy replay (role 2) of one chunk meet without a barrier packet in the main stream's queue.
+// join[0] / join[64]: per-launch arrival counters of roles 1 / 2 (reset by their last block),
+// join[32]: the epoch id of the last light replay that completed, join[96]: set on a timed-out
+// wait.  Role 1: every block arrives after its stores (release); the last one publishes the epoch.
+// Role 2: the last block to arrive waits (one lane, bounded) until the light replay of the same
+// epoch has published, so the kernel queued after the heavy replay (the fold) sees both groups'
+// sums.  Only the LAST block of role 2 waits: every other block has exited, so a light replay
+// that has not started yet still finds room to run.
+constexpr int kJoinSpinMax = 1 << 22;  // (~0.4 s of s_sleep: a wait that never ends is an error)
+__device__ __forceinline__ void join_arrive(uint32_t *join, int role, uint32_t epoch)
+{
+    __syncthreads();  // (every wave's sums stored before the block arrives)
+    if (threadIdx.x != 0) return;
+    uint32_t *arr = join + (role == 1 ? 0 : 64);
+    const uint32_t old = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old != gridDim.x - 1) return;
+    __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (role == 1) {
+        __hip_atomic_store(join + 32, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    for (int spins = 0;; ++spins) {
+        const uint32_t done = __hip_atomic_load(join + 32, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int32_t)(done - epoch) >= 0) break;
+        if (spins >= kJoinSpinMax) {
+            __hip_atomic_store(join + 96, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+template <typename T, int G>
+__global__ __launch_bounds__(kBlock) void log_replay_kernel(
+    const T *__restrict__ ckpt, const T *__restrict__ elog, int ldq, int K,
+    const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T inv_ap,
+    const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
+    const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int xmask,
+    int err_col, const int32_t *__restrict__ piece_item, uint32_t *join, int join_role,
+    uint32_t join_epoch)
+{
+    int64_t wave, n_waves;
+    if (wave_slot(xmask, wave, n_waves))
+        log_replay_body<T, G>(ckpt, elog, ldq, K, items, qb, n_items, lr_pu, inv_ap, perm, ck_pos,
+                              piece_beg, n_pieces, sums, err_col, piece_item, wave, n_waves);
+    if (join) join_arrive(join, join_role, join_epoch);
 }
 
 #ifndef MF_APPLY_U
@@ -3276,6 +3335,13 @@ int mf_stream_wait_event(void *stream, void *event)
     return 0;
 }
 
+int mf_launch_join(void *words, int32_t role, uint32_t epoch)
+{
+    if (words && role != 1 && role != 2) return set_err(MF_E_ARG, "join role must be 1 or 2");
+    mf_ext::g_join = mf_ext::JoinArgs{(uint32_t *)words, words ? role : 0, epoch};
+    return 0;
+}
+
 int mf_launch_event(void *event)
 {
     mf_ext::g_stop_event = (hipEvent_t)event;
@@ -3390,9 +3456,10 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
                   const int32_t *piece_item, int32_t flags, int32_t dtype, void *stream)
 {
     StopEvent stop(stream);  // (mf_launch_event)
+    const mf_ext::JoinArgs join = mf_ext::take_join();  // (mf_launch_join)
     if (n_pieces < 0 || ldq < n_factors + 1 || n_factors < 0) return set_err(MF_E_ARG, "bad shape");
     const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
-    if (n_pieces == 0) return 0;
+    if (n_pieces == 0 && !join.words) return 0;  // (a join still launches: its partner waits)
     if (!qlog || !elog || !csr || !qb || !hp || !perm || !ck_pos || !piece_beg || !sums)
         return set_err(MF_E_ARG, "null argument");
     const int err_col = (flags & MF_EPOCH_ERR_IN_ROW) ? err_column(n_factors, ldq, dtype) : 0;
@@ -3401,7 +3468,7 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
     const int64_t rb = (int64_t)ldq * (dtype == MF_F64 ? 8 : 4);
     if (rb > 512 * kLaMaxG) return set_err(MF_E_UNSUPPORTED, "checkpoint log: ldq * size <= 1 KiB only");
     const int64_t cap = (int64_t)n_cus() * MF_REPLAY_WPC * (xmask ? __builtin_popcount(xmask) : 8) / 8;
-    const int g = grid_for_waves_x(n_pieces < cap ? n_pieces : cap, xmask);
+    const int g = grid_for_waves_x(n_pieces < 1 ? 1 : n_pieces < cap ? n_pieces : cap, xmask);
     hipStream_t st = (hipStream_t)stream;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
@@ -3415,7 +3482,7 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
                                    (const T *)qb, csr->n_items, (T)hp->lr_pu,
                                    (T)(1.0 / (1.0 - hp->lr_pu * hp->reg_pu)), perm,
                                    ck_pos, piece_beg, n_pieces, (T *)sums, xmask, err_col,
-                                   piece_item);
+                                   piece_item, join.words, join.role, join.epoch);
                 return check_launch("log_replay_kernel");
             }
         });

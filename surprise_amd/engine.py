@@ -360,6 +360,13 @@ class MFEngine(ItemSync, Predictor):
             self._nev = {k: _new_event() for k in ("fork", "join")}
             weakref.finalize(self, _free_events, list(self._nev.values()))
         self._fork_bound = False  # the last mf_log_apply on the main stream completes "fork"
+        # ... and the join inside the two replays (mf_launch_join: the heavy replay's last block
+        # waits for the light replay's; no barrier packet before the fold on the main stream);
+        # SURPRISE_AMD_JOIN_FLAG=0: the join as an event the main stream waits for
+        self._join_words = None
+        if self.side is not None and os.environ.get("SURPRISE_AMD_JOIN_FLAG", "1") != "0":
+            self._join_words = torch.zeros(128, dtype=torch.int32, device=dev)
+            self._join_epoch = 0
         self.sched = []
         self._totals_local = []
         self.logs = []  # "log" mode: per chunk, the item grouping of the log (log_layout)
@@ -529,6 +536,9 @@ class MFEngine(ItemSync, Predictor):
         (several ranks) pu / bu are every rank's rows gathered in rank order (all ranks)."""
         self._fork_bound = False  # (the side stream must wait for this work)
         self.stream.synchronize()
+        if getattr(self, "_join_words", None) is not None and int(self._join_words[96]) != 0:
+            raise _lib.SurpriseAMDError("the in-kernel join of the two replays timed out: the "
+                                        "item folds since are invalid")
         K = self.K
         h = lambda x: x.to(self.torch.float64).cpu().numpy()
         pu, bu = self.pu[:, :K], self.bu
@@ -704,17 +714,23 @@ class MFEngine(ItemSync, Predictor):
             if "end" in ev:
                 ev["end"].record(self.stream)
             self._epoch_sq(ls, ln, lw, sh, lx)
-            if self._nev is not None:
+            jw = self._join_words
+            if jw is not None:
+                self._join_epoch = (self._join_epoch + 1) & 0xFFFFFFFF
+                _lib.call("mf_launch_join", self._ptr(jw), 1, self._join_epoch)
+            elif self._nev is not None:
                 _lib.call("mf_launch_event", self._nev["join"])  # completed by the light replay
             self._reduce_log(lg, self.sums.data_ptr(), sh, lx)
-            if self._nev is None:
+            if jw is None and self._nev is None:
                 self._ev_record("join", side)
             # (the heavy replay starts when the longest chain ends: by then the light users'
             # work is (nearly) done, so it may spread over every XCD)
+            if jw is not None:  # (it ends once the light replay of this chunk has published)
+                _lib.call("mf_launch_join", self._ptr(jw), 2, self._join_epoch)
             self._reduce_log(hv, sums_h, st, 0 if self.heavy_replay_all else self.heavy_xcd)
-            if self._nev is None:
+            if jw is None and self._nev is None:
                 self._ev_wait(self.stream, "join")
-            else:
+            elif jw is None:
                 _lib.call("mf_stream_wait_event", st, self._nev["join"])
         if "end_r" in ev:
             ev["end_r"].record(self.stream)

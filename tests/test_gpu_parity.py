@@ -404,12 +404,12 @@ def test_heavy_user_split_matches_single_launch(torch, u1):
 
 
 @pytest.mark.parametrize("chunks", [1, 3])
-def test_native_fork_join_events_equal_torch_events(torch, u1, monkeypatch, chunks):
-    """The split chunk's fork / join as native events bound to the kernels that complete them
-    (mf_launch_event: the fork by the previous chunk's mf_log_apply, the join by the light
-    replay) against torch.cuda.Event record / wait_event: the same kernels in the same stream
-    order, so the fits are bit-identical -- with main-stream work (a batched predict) between
-    epochs, after which the fork must be recorded again."""
+def test_native_fork_and_kernel_join_equal_torch_events(torch, u1, monkeypatch, chunks):
+    """The split chunk's fork as a native event bound to the previous chunk's mf_log_apply
+    (mf_launch_event) and its join inside the two replays (mf_launch_join: the heavy replay's
+    last block waits for the light replay's) against torch.cuda.Event record / wait_event: the
+    same kernels on the same data, so the fits are bit-identical -- with main-stream work (a
+    batched predict) between epochs, after which the fork must be recorded again."""
     from surprise_amd.engine import MFEngine
     ts, _ = u1
     row_ptr, items, ratings = ts.csr()
@@ -423,9 +423,11 @@ def test_native_fork_join_events_equal_torch_events(torch, u1, monkeypatch, chun
     out = []
     for native in ("1", "0"):
         monkeypatch.setenv("SURPRISE_AMD_NATIVE_EVENTS", native)
+        monkeypatch.setenv("SURPRISE_AMD_JOIN_FLAG", native)
         eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype="float32",
                        mode="log", n_chunks=chunks, heavy=0.25)
         assert eng.logs[0]["heavy"] is not None and (eng._nev is not None) == (native == "1")
+        assert (eng._join_words is not None) == (native == "1")
         eng.set_factors(pu0, qi0)
         ests = []
         eng.run_epochs(2)
