@@ -379,12 +379,12 @@ int mf_launch_event(void *event);
 
 /* mf_launch_join(words, role, epoch): the next mf_log_replay launch of the calling thread takes
  * part in an in-kernel join (no barrier packet in the main stream's queue): role 1 (the light
- * replay on the side stream) publishes `epoch` into words[32] when its last block has stored its
- * sums; role 2 (the heavy replay on the main stream) ends only when words[32] >= epoch, so the
- * mf_log_apply queued after it sees both groups' sums.  words: >= 128 zeroed uint32 of device
- * memory owned by the caller, one per pair of streams; epoch: increasing per chunk (wraps).
- * words[96] is set if a wait timed out (~0.4 s): the fold is then invalid and the caller must
- * fail.  words = NULL: no join. */
+ * replay on the side stream) publishes `epoch` into words[576] when its last block has stored its
+ * sums; role 2 (the heavy replay on the main stream) ends only when words[576] >= epoch, so the
+ * mf_log_apply queued after it sees both groups' sums.  words: >= 1024 zeroed uint32 of device
+ * memory owned by the caller, one per pair of streams (the arrival counters live there too);
+ * epoch: increasing per chunk (wraps).  words[608] is set if a wait timed out (~0.4 s): the fold
+ * is then invalid and the caller must fail.  words = NULL: no join. */
 int mf_launch_join(void *words, int32_t role, uint32_t epoch);
 
 #ifdef __cplusplus

@@ -2000,7 +2000,8 @@ __device__ __forceinline__ void log_replay_body(
     const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T inv_ap,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
     const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int err_col,
-    const int32_t *__restrict__ piece_item, const int64_t wave, const int64_t n_waves)
+    const int32_t *__restrict__ piece_item, const int64_t wave, const int64_t n_waves,
+    const bool wt)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -2086,38 +2087,61 @@ __device__ __forceinline__ void log_replay_body(
             const int c0 = (lane + kWave * v) * W;
 #pragma unroll
             for (int e = 0; e < W; ++e)
-                if (c0 + e < ldq) sums[pc * ldq + c0 + e] = c0 + e <= K ? L::get(acc[v], e) : T(0);
+                if (c0 + e < ldq) {
+                    const T x = c0 + e <= K ? L::get(acc[v], e) : T(0);
+                    if (wt)  // (written through to the agent's coherence point: mf_launch_join)
+                        __hip_atomic_store(&sums[pc * ldq + c0 + e], x, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    else
+                        sums[pc * ldq + c0 + e] = x;
+                }
         }
     }
 }
 
 // In-kernel join of the two-stream SVD step (mf_launch_join): the light replay (role 1) and the
 // heavy replay (role 2) of one chunk meet without a barrier packet in the main stream's queue.
-// join[0] / join[64]: per-launch arrival counters of roles 1 / 2 (reset by their last block),
-// join[32]: the epoch id of the last light replay that completed, join[96]: set on a timed-out
-// wait.  Role 1: every block arrives after its stores (release); the last one publishes the epoch.
+// Per-launch arrival counters of roles 1 / 2 (reset by their last arrivals), the epoch id of the
+// last light replay that completed and a timed-out-wait flag (layout below).  Role 1: every block arrives after its stores (release); the last one publishes the epoch.
 // Role 2: the last block to arrive waits (one lane, bounded) until the light replay of the same
 // epoch has published, so the kernel queued after the heavy replay (the fold) sees both groups'
 // sums.  Only the LAST block of role 2 waits: every other block has exited, so a light replay
-// that has not started yet still finds room to run.
+// that has not started yet still finds room to run.  Role 1's sums are stored as agent-scope
+// atomic stores (written through each XCD's L2) and every block waits for its stores before it
+// arrives with a RELAXED add: a release fence per block (an L2 write-back each) made the light
+// replay 72 -> 125 us; the only fences are the publishing store's and the waiter's acquire.
 constexpr int kJoinSpinMax = 1 << 22;  // (~0.4 s of s_sleep: a wait that never ends is an error)
+// word layout (uint32, each counter on its own 128-byte line): role r's arrival counters for the
+// eight residue classes of blockIdx (mod 8) at kJoinSub<r> + 32 c, its top counter at kJoinTop<r>;
+// the published epoch at kJoinFlag, the timeout flag at kJoinErr.  Two levels: ~G/8 same-address
+// atomics per class in parallel, then <= 8 at the top (one counter for ~1000 blocks serialised
+// the blocks' arrivals behind each other at the end of the launch).
+constexpr int kJoinSub1 = 0, kJoinTop1 = 256, kJoinSub2 = 288, kJoinTop2 = 544;
+constexpr int kJoinFlag = 576, kJoinErr = 608;
+__device__ __forceinline__ bool join_count(uint32_t *w, uint32_t n) {  // true: the n-th arrival
+    const uint32_t old = __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old != n - 1) return false;
+    __hip_atomic_store(w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
 __device__ __forceinline__ void join_arrive(uint32_t *join, int role, uint32_t epoch)
 {
-    __syncthreads();  // (every wave's sums stored before the block arrives)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's stores have completed)
+    __syncthreads();  // (... and every wave's, before the block arrives)
     if (threadIdx.x != 0) return;
-    uint32_t *arr = join + (role == 1 ? 0 : 64);
-    const uint32_t old = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old != gridDim.x - 1) return;
-    __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t G = gridDim.x, c = blockIdx.x & 7;
+    if (!join_count(join + (role == 1 ? kJoinSub1 : kJoinSub2) + 32 * c, (G - c + 7) / 8)) return;
+    if (!join_count(join + (role == 1 ? kJoinTop1 : kJoinTop2), G < 8 ? G : 8)) return;
     if (role == 1) {
-        __hip_atomic_store(join + 32, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(join + kJoinFlag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     for (int spins = 0;; ++spins) {
-        const uint32_t done = __hip_atomic_load(join + 32, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t done = __hip_atomic_load(join + kJoinFlag, __ATOMIC_ACQUIRE,
+                                                __HIP_MEMORY_SCOPE_AGENT);
         if ((int32_t)(done - epoch) >= 0) break;
         if (spins >= kJoinSpinMax) {
-            __hip_atomic_store(join + 96, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(join + kJoinErr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -2136,7 +2160,8 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     int64_t wave, n_waves;
     if (wave_slot(xmask, wave, n_waves))
         log_replay_body<T, G>(ckpt, elog, ldq, K, items, qb, n_items, lr_pu, inv_ap, perm, ck_pos,
-                              piece_beg, n_pieces, sums, err_col, piece_item, wave, n_waves);
+                              piece_beg, n_pieces, sums, err_col, piece_item, wave, n_waves,
+                              join && join_role == 1);
     if (join) join_arrive(join, join_role, join_epoch);
 }
 

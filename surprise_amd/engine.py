@@ -365,7 +365,7 @@ class MFEngine(ItemSync, Predictor):
         # SURPRISE_AMD_JOIN_FLAG=0: the join as an event the main stream waits for
         self._join_words = None
         if self.side is not None and os.environ.get("SURPRISE_AMD_JOIN_FLAG", "1") != "0":
-            self._join_words = torch.zeros(128, dtype=torch.int32, device=dev)
+            self._join_words = torch.zeros(1024, dtype=torch.int32, device=dev)
             self._join_epoch = 0
         self.sched = []
         self._totals_local = []
@@ -536,7 +536,7 @@ class MFEngine(ItemSync, Predictor):
         (several ranks) pu / bu are every rank's rows gathered in rank order (all ranks)."""
         self._fork_bound = False  # (the side stream must wait for this work)
         self.stream.synchronize()
-        if getattr(self, "_join_words", None) is not None and int(self._join_words[96]) != 0:
+        if getattr(self, "_join_words", None) is not None and int(self._join_words[608]) != 0:
             raise _lib.SurpriseAMDError("the in-kernel join of the two replays timed out: the "
                                         "item folds since are invalid")
         K = self.K

@@ -403,19 +403,21 @@ def test_heavy_user_split_matches_single_launch(torch, u1):
         np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=1e-10, err_msg=k)
 
 
-@pytest.mark.parametrize("chunks", [1, 3])
-def test_native_fork_and_kernel_join_equal_torch_events(torch, u1, monkeypatch, chunks):
+@pytest.mark.parametrize("which,chunks", [("u1", 1), ("u1", 3), ("ml1m", 1)])
+def test_native_fork_and_kernel_join_equal_torch_events(torch, request, monkeypatch, which,
+                                                          chunks):
     """The split chunk's fork as a native event bound to the previous chunk's mf_log_apply
     (mf_launch_event) and its join inside the two replays (mf_launch_join: the heavy replay's
     last block waits for the light replay's) against torch.cuda.Event record / wait_event: the
     same kernels on the same data, so the fits are bit-identical -- with main-stream work (a
     batched predict) between epochs, after which the fork must be recorded again."""
     from surprise_amd.engine import MFEngine
-    ts, _ = u1
+    ts, _ = request.getfixturevalue(which)
     row_ptr, items, ratings = ts.csr()
     K = 100
     hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
                  reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    heavy = 0.25 if which == "u1" else None  # (ML-1M: the default split, 128 heaviest users)
     rng = np.random.RandomState(3)
     pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
     uu = np.arange(ts.n_users, dtype=np.int32) % ts.n_users
@@ -425,7 +427,7 @@ def test_native_fork_and_kernel_join_equal_torch_events(torch, u1, monkeypatch, 
         monkeypatch.setenv("SURPRISE_AMD_NATIVE_EVENTS", native)
         monkeypatch.setenv("SURPRISE_AMD_JOIN_FLAG", native)
         eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype="float32",
-                       mode="log", n_chunks=chunks, heavy=0.25)
+                       mode="log", n_chunks=chunks, heavy=heavy)
         assert eng.logs[0]["heavy"] is not None and (eng._nev is not None) == (native == "1")
         assert (eng._join_words is not None) == (native == "1")
         eng.set_factors(pu0, qi0)
