@@ -360,11 +360,12 @@ class MFEngine(ItemSync, Predictor):
             self._nev = {k: _new_event() for k in ("fork", "join")}
             weakref.finalize(self, _free_events, list(self._nev.values()))
         self._fork_bound = False  # the last mf_log_apply on the main stream completes "fork"
-        # ... and the join inside the two replays (mf_launch_join: the heavy replay's last block
-        # waits for the light replay's; no barrier packet before the fold on the main stream);
-        # SURPRISE_AMD_JOIN_FLAG=0: the join as an event the main stream waits for
+        # the join as an event the main stream waits for; SURPRISE_AMD_JOIN_FLAG=1: inside the two
+        # replays instead (mf_launch_join: the heavy replay's last block waits for the light
+        # replay's; no barrier packet before the fold) -- measured equal (the write-through
+        # stores of the light replay cost what the barrier packet did), so off by default
         self._join_words = None
-        if self.side is not None and os.environ.get("SURPRISE_AMD_JOIN_FLAG", "1") != "0":
+        if self.side is not None and os.environ.get("SURPRISE_AMD_JOIN_FLAG", "0") != "0":
             self._join_words = torch.zeros(1024, dtype=torch.int32, device=dev)
             self._join_epoch = 0
         self.sched = []
