@@ -2168,7 +2168,7 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
 #ifndef MF_APPLY_U
 #define MF_APPLY_U 16  // mf_log_apply: piece rows in flight per wave (a popular item has ~60)
 #endif
-template <typename T, int V>
+template <typename T, int V, bool TWO>  // TWO: a split chunk (sums2, the heavy group's pieces)
 __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     T *__restrict__ qb, int n_items, int ld, int n_fac, int bias_col, const T *__restrict__ sums,
     const int32_t *__restrict__ item_piece_ptr, const T *__restrict__ sums2,
@@ -2204,7 +2204,7 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
         // count and the item row; then the first kU pieces of each group together
         const int a0 = item_piece_ptr ? item_piece_ptr[i] : (int)i;
         const int a1 = item_piece_ptr ? item_piece_ptr[i + 1] : (int)i + 1;
-        const int b0 = sums2 ? item_piece_ptr2[i] : 0, b1 = sums2 ? item_piece_ptr2[i + 1] : 0;
+        const int b0 = TWO ? item_piece_ptr2[i] : 0, b1 = TWO ? item_piece_ptr2[i + 1] : 0;
         const double N = totals ? (double)totals[i] : 0.0;
         T q[V];
 #pragma unroll
@@ -2230,19 +2230,26 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
                 for (int v = 0; v < V; ++v) acc[v] += g[a][v];
         };
         // the item's pieces in sums, then (split log) its pieces in sums2, in that fixed order
-        T ga[kU][V], gb[kU][V];
+        T ga[kU][V];
         load(sums, a0, a1, ga);
-        if (sums2) load(sums2, b0, b1, gb);
-        add(ga);
-        for (int pc = a0 + kU; pc < a1; pc += kU) {
-            load(sums, pc, a1, ga);
+        if constexpr (TWO) {
+            T gb[kU][V];
+            load(sums2, b0, b1, gb);
             add(ga);
-        }
-        if (sums2) {
+            for (int pc = a0 + kU; pc < a1; pc += kU) {
+                load(sums, pc, a1, ga);
+                add(ga);
+            }
             add(gb);
             for (int pc = b0 + kU; pc < b1; pc += kU) {
                 load(sums2, pc, b1, gb);
                 add(gb);
+            }
+        } else {
+            add(ga);
+            for (int pc = a0 + kU; pc < a1; pc += kU) {
+                load(sums, pc, a1, ga);
+                add(ga);
             }
         }
         // the count-aware weights (one per column kind, the same for every factor column)
@@ -3582,7 +3589,15 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
         return dispatch_v<T>(ld, [&](auto vc) -> int {
-            launch_ev(stop.take(), (log_apply_kernel<T, decltype(vc)::value>), dim3(g), dim3(kBlock),
+            if (sums2)
+                launch_ev(stop.take(), (log_apply_kernel<T, decltype(vc)::value, true>), dim3(g), dim3(kBlock),
+                               st, (T *)qb, n_items, ld, n_factors, bias_col, (const T *)sums,
+                               item_piece_ptr, (const T *)sums2, item_piece_ptr2, totals,
+                               count_rule, eta_b, lr_c, reg_c, lr_f,
+                               reg_f, lr_b, reg_b, p2stat, (T *)delta_out, apply, stat_next,
+                               user_sq, (int64_t)n_users, n_factors);
+            else
+                launch_ev(stop.take(), (log_apply_kernel<T, decltype(vc)::value, false>), dim3(g), dim3(kBlock),
                                st, (T *)qb, n_items, ld, n_factors, bias_col, (const T *)sums,
                                item_piece_ptr, (const T *)sums2, item_piece_ptr2, totals,
                                count_rule, eta_b, lr_c, reg_c, lr_f,
