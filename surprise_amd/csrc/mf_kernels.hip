@@ -1779,7 +1779,7 @@ __device__ __forceinline__ void block_sum_sq(const double *__restrict__ sq, int6
 {
     __shared__ double part[kBlock];
     double acc = 0;
-    constexpr int kU = 8;
+    constexpr int kU = 32;  // loads in flight per thread (the sum order does not depend on it)
     for (int64_t i0 = threadIdx.x; i0 < n; i0 += (int64_t)kU * kBlock) {
         double v[kU];
 #pragma unroll
@@ -2178,9 +2178,9 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     int apply, double *__restrict__ stat_next, const double *__restrict__ user_sq, int64_t n_sq,
     int sq_cols)
 {
-    // the next chunk's {sum |p_u|^2, count}: the launch's extra last block (every epoch kernel
-    // has finished), so that no item block waits behind the sum
-    if (stat_next && blockIdx.x == gridDim.x - 1) {
+    // the next chunk's {sum |p_u|^2, count}: the launch's extra FIRST block, which does no item
+    // (dispatched first: at 2M users the one-block sum is the launch's longest piece of work)
+    if (stat_next && blockIdx.x == 0) {
         if (user_sq) {
             block_sum_sq(user_sq, n_sq, sq_cols, stat_next);
         } else if (threadIdx.x < 2) {
@@ -2189,9 +2189,10 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
         return;
     }
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
+    const int blk0 = stat_next ? 1 : 0;  // (block 0: the statistic)
+    const int64_t wave = (int64_t)(blockIdx.x - blk0) * (kBlock / kWave) +
                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int64_t n_waves = ((int64_t)(gridDim.x - (stat_next ? 1 : 0)) * kBlock) / kWave;
+    const int64_t n_waves = ((int64_t)(gridDim.x - blk0) * kBlock) / kWave;
     double eta_fac = 0, l_fac = 0, l_bias = 0;
     if (count_rule) {
         eta_fac = lr_fac * (p2stat[0] / p2stat[1] + reg_fac);
