@@ -57,10 +57,15 @@ def parse():
     p.add_argument("--algo", default=None, choices=["svd", "svdpp"])
     p.add_argument("--factors", type=int, default=None)
     p.add_argument("--mode", default="auto")
+    p.add_argument("--dtype", default=None, choices=["f32", "f64"],
+                   help="device arithmetic; default f64 (the reference's: mf.pyx:207-227) for "
+                        "ml-1m, f32 for c4 / c5 (fp64 K=128 item rows exceed the 1 KiB "
+                        "lookahead layout and the fp64 log would not fit C4 on one GPU)")
     p.add_argument("--chunks", type=int, default=1)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rmse", action="store_true")
     p.add_argument("--no-svdpp", action="store_true", help="skip the SVD++ C3 leg")
+    p.add_argument("--no-predict", action="store_true", help="skip the batched test() leg")
     p.add_argument("--users", type=int, default=0,
                    help="c4 / c5: train only the first N users of the shape (a user-prefix "
                         "subsample that keeps every item; 0 = all)")
@@ -76,7 +81,13 @@ def parse():
     a.algo = a.algo or algo
     a.factors = a.factors or K
     a.scaling = scaling
+    a.legs = a.dtype is None  # the default run adds the other precision's leg (N=1, ml-1m)
+    a.dtype = a.dtype or ("f64" if a.shape == "ml-1m" else "f32")
     return a
+
+
+TORCH_DTYPE = {"f32": "float32", "f64": "float64"}
+ELEM_BYTES = {"f32": 4, "f64": 8}
 
 
 def algorithmic_bytes_per_update(algo, K, s=4):
@@ -239,8 +250,11 @@ def sum_over_ranks(ctx, xs, torch):
     return t.cpu().tolist()
 
 
-def traffic_for(algo, K, shape):
-    path = os.path.join(ROOT, "profiles", "traffic_%s_k%d_%s.json" % (algo, K, shape))
+def traffic_for(algo, K, shape, dtype="f32"):
+    """Measured HBM-side bytes per step (profiles/traffic_<algo>_k<K>_<shape>[_f64].json, written
+    by tools/profile.sh from separate rocprofv3 --pmc passes)."""
+    name = "traffic_%s_k%d_%s%s.json" % (algo, K, shape, "" if dtype == "f32" else "_" + dtype)
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
@@ -249,6 +263,20 @@ def traffic_for(algo, K, shape):
 
 
 # ---------------------------------------------------------------------------- CPU baseline
+def physical_cores():
+    """Physical cores of the host (distinct (package, core id) pairs of /proc/cpuinfo)."""
+    seen, pkg = set(), None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                pkg = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                seen.add((pkg, line.split(":", 1)[1].strip()))
+    except OSError:
+        pass
+    return len(seen) or os.cpu_count()
+
+
 def cpu_baselines(csr, n_items, K, n_train):
     """The fp64 C restatement (oracle/) on this host: one pinned core (in-process affinity) for
     ~10 s, then every core of this process's share at once (one pinned child process per core,
@@ -285,6 +313,8 @@ def cpu_baselines(csr, n_items, K, n_train):
     compute = max(o["seconds"] for o in outs)
     cal = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["calibration"]
     ratio = cal["oracle_over_reference"]
+    phys = physical_cores()
+    per_core_loaded = ups / compute / len(share)
     return {
         "value": ups / compute, "unit": "rating-updates/s", "cores": len(share), "kind": "port",
         "sample": "fp64 C restatement of SVD.sgd (oracle/mf_oracle.c <- mf.pyx:241-262), SVD K=%d, "
@@ -294,6 +324,14 @@ def cpu_baselines(csr, n_items, K, n_train):
         "single_core": {"value": rate1, "cores": 1, "pinned": True,
                         "sample": "%d epochs on core %d (%.1fs)" % (e, share[0], t1),
                         "cython_equivalent_derived": rate1 / ratio},
+        "node_physical_cores": phys,
+        "all_cores_derived": {
+            "value": per_core_loaded * phys, "cores": phys,
+            "note": "NOT measured: the per-core rate under the %d-process load x the node's "
+                    "physical cores. This pool caps one GPU's job at its CPU share (%d CPUs; "
+                    "os.cpu_count() shows the whole host), so the node's other cores are not "
+                    "ours to load; the extrapolation assumes linear scaling (optimistic for the "
+                    "CPU: 128 processes share the memory system)" % (len(share), BOX_CPU_SHARE)},
         "calibration_oracle_over_cython": ratio,
         "calibration_note": "the restatement / compiled reference Cython rate, both timed in the "
                             "build container on the same fold (tests/golden/golden.json)",
@@ -301,6 +339,19 @@ def cpu_baselines(csr, n_items, K, n_train):
 
 
 # ---------------------------------------------------------------------------- main
+def roofline_of(algo, K, dtype, n_train, ms_step, shape):
+    """SURVEY 8(d) algorithmic bytes of a step / the step time, against the HBM peak."""
+    B = algorithmic_bytes_per_update(algo, K, ELEM_BYTES[dtype])
+    achieved = B * n_train / (ms_step * 1e-3) / 1e9
+    traffic, tinfo = traffic_for(algo, K, shape, dtype)
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "algorithmic_bytes_per_update": B, "updates_per_step": n_train,
+            "algorithmic_bytes_per_step": B * n_train,
+            "traffic_breakdown": tinfo.get("per_kernel") if tinfo else None,
+            "traffic_source": tinfo.get("source") if tinfo else None}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -325,16 +376,14 @@ def main():
     tot, cnt = sum_over_ranks(ctx, [float(ratings.sum()), float(n_train)], torch)
     gm = tot / cnt
     K, algo = args.factors, args.algo
-    svdpp = algo == "svdpp"
-    hyper = hyper_for(algo, gm)
-    mode = args.mode if args.mode != "auto" else ("atomic" if svdpp else "log")
+    mode = args.mode if args.mode != "auto" else ("atomic" if algo == "svdpp" else "log")
     n_users = len(row_ptr) - 1
 
-    def make_engine(a=algo, k=K, md=mode):
+    def make_engine(a=algo, k=K, md=mode, dt=args.dtype):
         pu, qi, yj = init_tables(args.shape, rank, n_users, n_items, k, a == "svdpp",
                                  getattr(workload, "user_lo", 0))
         eng = MFEngine(csr, n_items, k, algo=a, hyper=hyper_for(a, gm), mode=md,
-                       n_chunks=args.chunks, world=world)
+                       dtype=TORCH_DTYPE[dt], n_chunks=args.chunks, world=world)
         eng.set_factors(pu, qi, yj=yj)
         eng._prepare(ctx)  # global per-item counts (all ranks)
         return eng
@@ -347,14 +396,11 @@ def main():
     updates = sum_over_ranks(ctx, [float(n_train)], torch)[0] * args.steps
     value = updates / elapsed
     ms_step = elapsed / args.steps * 1e3
-    B = algorithmic_bytes_per_update(algo, K)
-    bytes_step = B * n_train  # this rank's algorithmic bytes per step
-    achieved = bytes_step / (ms_step * 1e-3) / 1e9
-    traffic, tinfo = traffic_for(algo, K, args.shape)
+    headline = (algo, K, args.shape) == ("svd", 100, "ml-1m")
 
     result = {
         "metric": "rating-updates/sec/GPU, SVD n_factors=100; RMSE delta vs Cython ref"
-        if (algo, K, args.shape) == ("svd", 100, "ml-1m") else
+        if headline else
         "rating-updates/sec, %s n_factors=%d (%s)" % (algo.upper(), K, args.shape),
         "value": value,
         "unit": "rating-updates/s",
@@ -365,40 +411,36 @@ def main():
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": args.dtype,
         "data": "synthetic planted ratings (surprise_amd.synthetic, seed 0): " + desc,
-        "config": {"workload": "%s n_factors=%d, one epoch per step over %d training ratings per "
-                               "GPU (rank 0), mode=%s, chunks/epoch=%d, %s scaling over %d GPU(s)"
-                               % (algo.upper(), K, n_train, mode, eng.n_chunks, args.scaling,
-                                  world),
-                   "shape": args.shape, "algo": algo, "n_factors": K,
+        "config": {"workload": "%s n_factors=%d %s, one epoch per step over %d training ratings "
+                               "per GPU (rank 0), mode=%s, chunks/epoch=%d, %s scaling over %d "
+                               "GPU(s)" % (algo.upper(), K, args.dtype, n_train, mode,
+                                           eng.n_chunks, args.scaling, world),
+                   "shape": args.shape, "algo": algo, "n_factors": K, "dtype": args.dtype,
                    "train_ratings_rank0": n_train, "users_total": n_users_global,
-                   "items": n_items, "ld": default_ld(K, 0),
+                   "items": n_items, "ld": default_ld(K, 1 if args.dtype == "f64" else 0),
                    "parallelism": "users sharded x%d (contiguous ranges), item tables replicated, "
                                   "one SUM all-reduce per epoch-chunk" % world},
         "per_gpu_value": value / world,
         "device_bytes_per_rank_max": dev_bytes,
     }
-    result["roofline"] = {
-        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+    rl = roofline_of(algo, K, args.dtype, n_train, ms_step, args.shape)
+    rl.update({
         "kernel": "one epoch step (%s): %s" % (
             mode, "mf_ckpt_epoch_kernel (heavy + light users) + log_replay_kernel (both groups) "
                   "+ log_apply_kernel" if mode == "log"
             else "mf_epoch_kernel + y fold (+ merge)"),
-        "algorithmic_bytes_per_update": B, "updates_per_step": n_train,
-        "algorithmic_bytes_per_step": bytes_step,
         "phases_gpu_ms": phases,
-        "traffic_breakdown": tinfo.get("per_kernel") if tinfo else None,
-        "traffic_source": tinfo.get("source") if tinfo else None,
         "note": "achieved = algorithmic bytes of a step (SURVEY 8(d): a gather + scatter of the "
-                "user and item rows per rating) / the measured step time (<= 1 by construction). "
-                "ML-1M's tables (pu 2.7 MB, qb 1.7 MB) are L2/MALL-resident: the HBM-side bytes "
-                "(`traffic`: every kernel's 2 x FETCH_SIZE + WRITE_SIZE per step, PMC, MALL hits "
-                "included) are mostly the checkpoint log written and re-read, and the step is "
-                "bound by the heaviest user's sequential chain (1805 ratings), not by HBM",
-    }
+                "user and item rows per rating, s = %d bytes per element) / the measured step "
+                "time. ML-1M's tables are L2/MALL-resident: the HBM-side bytes (`traffic`: every "
+                "kernel's 2 x FETCH_SIZE + WRITE_SIZE per step, PMC) are mostly the checkpoint "
+                "log written and re-read, and the step is bound by the heaviest user's "
+                "sequential chain (1805 ratings), not by HBM" % ELEM_BYTES[args.dtype]})
+    result["roofline"] = rl
 
+    oracle_cache = {}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and algo == "svd":
         result["cpu_baseline"] = cpu_baselines(csr, n_items, K, n_train)
         cb = result["cpu_baseline"]
@@ -407,27 +449,47 @@ def main():
 
     if not args.no_rmse:
         result["rmse"] = rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch,
-                                  make_engine)
+                                  make_engine, oracle_cache)
 
-    if (world == 1 and args.shape == "ml-1m" and algo == "svd" and K == 100
-            and not args.no_svdpp):
-        del eng
-        pp = make_engine("svdpp", 100, "atomic")
-        e2, ph2 = run_steps(pp, None, max(10, args.steps // 2), 2, torch)
-        n2 = max(10, args.steps // 2)
-        b2 = algorithmic_bytes_per_update("svdpp", 100)
-        result["svdpp_c3"] = {
-            "config": "BASELINE configs[2]: SVD++ n_factors=100 (atomic q rows, deferred y fold) "
-                      "on the same fold, one epoch per step",
-            "value": n_train * n2 / e2, "unit": "rating-updates/s", "steps": n2,
-            "ms_per_step": e2 / n2 * 1e3, "phases_gpu_ms": ph2,
-            "roofline": {"achieved": b2 * n_train / (e2 / n2) / 1e9, "peak": HBM_PEAK_GBS,
-                         "frac": b2 * n_train / (e2 / n2) / 1e9 / HBM_PEAK_GBS,
-                         "algorithmic_bytes_per_update": b2}}
-        t2, ti2 = traffic_for("svdpp", 100, "ml-1m")
-        result["svdpp_c3"]["roofline"].update(
-            traffic=t2, traffic_breakdown=ti2.get("per_kernel") if ti2 else None,
-            traffic_source=ti2.get("source") if ti2 else None)
+    small = world == 1 and args.shape == "ml-1m" and K == 100
+    if small and args.legs and headline:
+        # the other precision on the same fold and steps (the fp32 product option)
+        other = "f32" if args.dtype == "f64" else "f64"
+        eng = None
+        e32 = make_engine(dt=other)
+        el2, ph = run_steps(e32, None, args.steps, args.warmup, torch)
+        del e32
+        ms2 = el2 / args.steps * 1e3
+        leg = {"dtype": other, "value": n_train * args.steps / el2, "ms_per_step": ms2,
+               "roofline": roofline_of(algo, K, other, n_train, ms2, args.shape)}
+        leg["roofline"]["phases_gpu_ms"] = ph
+        if not args.no_rmse:
+            leg["rmse"] = rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world,
+                                   torch, lambda: make_engine(dt=other), oracle_cache)
+        result["%s_leg" % other] = leg
+
+    if small and algo == "svd" and not args.no_svdpp:
+        eng = None
+        pp_legs = {}
+        for dt in ([args.dtype] + ([d for d in ("f64", "f32") if d != args.dtype]
+                                   if args.legs else [])):
+            pp = make_engine("svdpp", 100, "atomic", dt)
+            n2 = max(10, args.steps // 2)
+            e2, ph2 = run_steps(pp, None, n2, 2, torch)
+            del pp
+            rl2 = roofline_of("svdpp", 100, dt, n_train, e2 / n2 * 1e3, args.shape)
+            rl2["phases_gpu_ms"] = ph2
+            pp_legs[dt] = {"value": n_train * n2 / e2, "unit": "rating-updates/s", "steps": n2,
+                           "ms_per_step": e2 / n2 * 1e3, "roofline": rl2}
+        result["svdpp_c3"] = dict(
+            config="BASELINE configs[2]: SVD++ n_factors=100 (atomic q rows, deferred y fold) "
+                   "on the same fold, one epoch per step", **pp_legs[args.dtype])
+        for dt, leg in pp_legs.items():
+            if dt != args.dtype:
+                result["svdpp_c3"]["%s_leg" % dt] = leg
+
+    if small and headline and args.legs and not args.no_predict:
+        result["predict"] = predict_leg(csr, test, n_items, gm, torch)
 
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -436,11 +498,55 @@ def main():
         ctx.dist.destroy_process_group()
 
 
-def rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch, make_engine):
+def oracle_rmse(args, csr, test, n_items, K, gm, cache):
+    """Held-out RMSE of the fp64 sequential oracle -- the reference loop restated (SVD:
+    mf.pyx:241-262; SVD++: its exact per-user form of :463-498) -- on the same CSR and initial
+    factors (computed once per run)."""
+    if "rmse" in cache:
+        return cache["rmse"], cache["seconds"]
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    E = args.rmse_epochs
+    svdpp = args.algo == "svdpp"
+    tu, ti, tr = test
+    tu, ti = np.asarray(tu, np.int32), np.asarray(ti, np.int32)
+    row_ptr, items, ratings = csr
+    pu, qi, yj = init_tables(args.shape, 0, len(row_ptr) - 1, n_items, K, svdpp)
+    h = hyper_for(args.algo, gm)
+    hp = orc.hyper(**{k: v for k, v in h.items() if k != "global_mean"})
+    t0 = time.perf_counter()
+    if svdpp:
+        pu, qi, yj, bu, bi = orc.svdpp_sgd(row_ptr, items, ratings, n_items, K, E, gm, hp, pu,
+                                           qi, yj, affine=True)
+        e = orc.svdpp_predict(tu, ti, row_ptr, items, K, gm, pu, qi, yj, bu, bi)
+        imp = np.zeros(len(tu), bool)
+    else:
+        pu, qi, bu, bi = orc.svd_sgd(row_ptr, items, ratings, n_items, K, E, True, gm, hp,
+                                     pu, qi)
+        e, imp = orc.svd_predict(tu, ti, K, True, gm, pu, qi, bu, bi)
+    cache["seconds"] = time.perf_counter() - t0
+    cache["rmse"] = orc.rmse(tr, orc.finish_estimates(e, imp, gm, 0, (1, 5)))
+    return cache["rmse"], cache["seconds"]
+
+
+def scale_golden(args, E):
+    """The committed fp64-oracle held-out RMSE of this c4 / c5-shard workload after E epochs
+    (tests/golden/scale_golden.json, made by tests/golden/make_scale_golden.py), or None."""
+    key = {"c4": "c4", "c5": "c5shard"}.get(args.shape)
+    path = os.path.join(ROOT, "tests", "golden", "scale_golden.json")
+    if key is None or not os.path.exists(path):
+        return None
+    g = json.load(open(path)).get(key)
+    if g is None or (g["users"] or 0) != (args.users or 0) or E > len(g["rmse_by_epoch"]):
+        return None
+    return g
+
+
+def rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch, make_engine,
+             oracle_cache):
     """A full fit (--rmse-epochs, 20 by default) through the same engine, held-out RMSE over all
-    ranks; at N=1 on ML-1M (or with --oracle) also the fp64 sequential oracle -- the reference
-    loop restated (SVD: mf.pyx:241-262; SVD++: its exact per-user form of :463-498) -- on the
-    same CSR and initial factors."""
+    ranks; at N=1 on ML-1M (or with --oracle) also the fp64 sequential oracle on the same CSR and
+    initial factors; c4 / c5-shard: the committed oracle value (scale_golden.json)."""
     E = args.rmse_epochs
     eng = make_engine()
     eng.run_epochs(E, ctx)
@@ -452,31 +558,58 @@ def rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch, mak
     se, n, se_mu = sum_over_ranks(ctx, [float(((tr - est) ** 2).sum()), float(len(tr)),
                                         float(((tr - gm) ** 2).sum())], torch)
     out = {"gpu": (se / n) ** .5, "global_mean_baseline": (se_mu / n) ** .5,
-           "fit": "%s K=%d E=%d (%s) through the bench engine, %d held-out ratings over %d "
-                  "rank(s)" % (args.algo.upper(), K, E, mode, int(n), world)}
+           "fit": "%s K=%d E=%d %s (%s) through the bench engine, %d held-out ratings over %d "
+                  "rank(s)" % (args.algo.upper(), K, E, eng.tdt, mode, int(n), world)}
     del eng
     if world == 1 and (args.shape == "ml-1m" or args.oracle):
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as orc
-        row_ptr, items, ratings = csr
-        pu, qi, yj = init_tables(args.shape, 0, len(row_ptr) - 1, n_items, K, svdpp)
-        h = hyper_for(args.algo, gm)
-        hp = orc.hyper(**{k: v for k, v in h.items() if k != "global_mean"})
-        t0 = time.perf_counter()
-        if svdpp:
-            pu, qi, yj, bu, bi = orc.svdpp_sgd(row_ptr, items, ratings, n_items, K, E, gm, hp, pu,
-                                               qi, yj, affine=True)
-            e = orc.svdpp_predict(tu, ti, row_ptr, items, K, gm, pu, qi, yj, bu, bi)
-            imp = np.zeros(len(tu), bool)
-        else:
-            pu, qi, bu, bi = orc.svd_sgd(row_ptr, items, ratings, n_items, K, E, True, gm, hp,
-                                         pu, qi)
-            e, imp = orc.svd_predict(tu, ti, K, True, gm, pu, qi, bu, bi)
-        out["oracle_seconds"] = time.perf_counter() - t0
-        e = orc.finish_estimates(e, imp, gm, 0, (1, 5))
-        out["reference_oracle_fp64"] = orc.rmse(tr, e)
-        out["delta"] = out["gpu"] - out["reference_oracle_fp64"]
+        ref, secs = oracle_rmse(args, csr, test, n_items, K, gm, oracle_cache)
+        out["oracle_seconds"] = secs
+        out["reference_oracle_fp64"] = ref
+        out["delta"] = out["gpu"] - ref
         out["tolerance"] = 1e-3
+    else:
+        g = scale_golden(args, E)
+        if g is not None:
+            out["reference_oracle_fp64"] = g["rmse_by_epoch"][E - 1]
+            out["reference_source"] = ("tests/golden/scale_golden.json (%s; data fingerprint %s)"
+                                       % (g["generator"], g["data_fingerprint"]))
+            out["delta"] = out["gpu"] - out["reference_oracle_fp64"]
+            out["tolerance"] = 1e-3
+    return out
+
+
+def predict_leg(csr, test, n_items, gm, torch):
+    """the batched device test() / test_metrics() of fitted SVD and SVD++ models
+    (the public classes, default dtype) over the held-out fold, against the reference's
+    per-prediction path (AlgoBase.predict -> estimate: algo_base.py:101-218, mf.pyx:269-299 /
+    :506-522; 6.6 us per SVD prediction measured in the survey container)."""
+    from surprise_amd import SVD, SVDpp
+    from surprise_amd.trainset import Trainset
+    row_ptr, items, ratings = csr
+    ts = Trainset.from_csr(row_ptr, items, ratings, n_items)
+    tu, ti, tr = test
+    testset = list(zip(np.asarray(tu).tolist(), np.asarray(ti).tolist(),
+                       np.asarray(tr, np.float64).tolist()))
+    out = {"held_out": len(testset), "reference_us_per_prediction": 6.6,
+           "reference_note": "SVD: AlgoBase.predict per rating (SURVEY 3.2, measured in the "
+                             "build container); SVD++ re-sums y_j over I_u per call"}
+    for name, klass, k in (("svd", SVD, 100), ("svdpp", SVDpp, 100)):
+        algo = klass(n_factors=k, n_epochs=20, random_state=0).fit(ts)
+        leg = {"dtype": algo.dtype}
+        for fn in ("test", "test_metrics"):
+            getattr(algo, fn)(testset[:1000])  # warm (device tables, implicit term)
+            t0 = time.perf_counter()
+            reps = 3
+            for _ in range(reps):
+                r = getattr(algo, fn)(testset)
+            dt = (time.perf_counter() - t0) / reps
+            leg[fn] = {"seconds": dt, "predictions_per_s": len(testset) / dt,
+                       "us_per_prediction": dt / len(testset) * 1e6}
+            if fn == "test_metrics":
+                leg[fn]["rmse"] = r[0]
+        leg["speedup_vs_reference_test"] = 6.6 / leg["test"]["us_per_prediction"]
+        out[name] = leg
+        del algo
     return out
 
 

@@ -82,11 +82,13 @@ typedef struct mf_csr {
  *               zero padding included); each user's segment must be < 2^30
  *               bytes (|I_u| * ldq * sizeof(dtype)).  Other modes: NULL.
  *   elog      : NULL, or (MF_MODE_LOG, ldq * sizeof(dtype) <= 1 KiB) the checkpoint form of the
- *               log: device [nnz + mf_ckpt_interval()] errors, elog[k] = err_k, and qlog row k
- *               holds [p_u | 1 | 0..] AFTER rating k (= before rating k + 1; for a user's odd
- *               last rating the final row) only where k - row_ptr[u] is even (other rows are
- *               not written); mf_log_replay rebuilds the gradients.  Requires
- *               1 - lr_pu * reg_pu != 0 (the replay undoes one step).  About half the log bytes.
+ *               log: device [nnz + mf_ckpt_interval()] errors, elog[k] = err_k, and qlog holds
+ *               one PACKED row per pair of a user's ratings: pair m (ratings row_ptr[u] + 2m,
+ *               + 2m + 1) is qlog row (row_ptr[u] + u + 1) / 2 + m and holds [p_u | 1 | 0..]
+ *               AFTER the pair's first rating (= before its second; for a user's odd last
+ *               rating the final row); qlog then has (row_ptr[n_users] + n_users + 1) / 2 rows
+ *               (about half of nnz); mf_log_replay rebuilds the gradients.  Requires
+ *               1 - lr_pu * reg_pu != 0 (the replay undoes one step).
  *   n_waves   : wavefronts to launch (<= 0: library default = fill the GPU);
  *               1 with MF_MODE_PLAIN gives the exact sequential reference order when
  *               sched = 0..n_users-1.
@@ -156,9 +158,10 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
 /*
  * Delta-log merge, step 1 for the checkpoint form (mf_svd_epoch with elog): the same sums as
  * mf_log_reduce would give on the gradient log, sums[p][c] = sum over the piece's ratings k of
- * err_k * p_k[c] (c <= n_factors; 0 above), where p_k comes from the pair's checkpoint row
- * c_k = ck_pos[x] (x = the rating's index in perm; c_k = k - ((k - row_ptr[u]) mod 2)), which
- * holds p_{c_k + 1}: for k = c_k + 1 the row itself, for k = c_k the epoch kernel's step undone,
+ * err_k * p_k[c] (c <= n_factors; 0 above), where p_k comes from its pair's packed checkpoint
+ * row: ck_pos[x] = 2 * row + (k - row_ptr[u]) mod 2 (x = the rating's index in perm; row as in
+ * mf_svd_epoch's elog), which holds the user row after the pair's first rating c: for k = c + 1
+ * (odd) the row itself, for k = c the epoch kernel's step undone,
  * p_k = (row - err_k * lr_pu * q_{item(k)}) / ap (ap = 1 - lr_pu * reg_pu on factor columns;
  * q from the snapshot table qb; every rating of a piece has the same item) -- call it before
  * mf_log_apply.  piece_item (nullable): the item of each piece (else read through perm and the

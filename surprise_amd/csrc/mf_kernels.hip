@@ -127,9 +127,12 @@ Hyper<T> cast_hyper(const mf_hyper_t *h) {
 
 // ---------------------------------------------------------------- wavefront primitives
 
+// (bound_ctrl: a lane whose source lane is out of its row reads 0 -- the permutations below stay
+// inside a row, row_bcast:15 has no source for row 0 -- so the compiler needs no old value: no
+// v_mov of a zero before every 32-bit DPP move, which for fp64 sums was 2 of every 5 instructions)
 template <int CTRL>
 __device__ __forceinline__ int dpp_i32(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
 }
 
 // 32-bit lane exchange pattern applied to a float / double.
@@ -797,6 +800,12 @@ __device__ __forceinline__ void epoch_body(
 // checkpoint interval of the SVD log (elog != NULL): one user row per pair of ratings (the
 // replay's inverse step needs exactly 2)
 constexpr int kCkpt = 2;
+// The checkpoint rows are packed: pair m (ratings 2m, 2m + 1 of the user) of the user whose
+// ratings start at CSR position s = row_ptr[u] is row ck_row0(s, u) + m.  ((s + u + 1) / 2 grows
+// by >= ceil(n_u / 2) from one user to the next: no per-user table, at most one spare row per
+// user; the log holds ck_row0(nnz, n_users) rows.)  Written rows are contiguous, so every cache
+// line of a user's rows is written whole (row stride 2 left half-written lines between rows).
+__host__ __device__ __forceinline__ int64_t ck_row0(int64_t s, int64_t u) { return (s + u + 1) >> 1; }
 #ifndef MF_LA_MAX_G
 #define MF_LA_MAX_G 2  // lookahead body / checkpoint log for rows of up to 2 lane groups (1 KiB)
 #endif
@@ -903,10 +912,10 @@ __device__ __forceinline__ void epoch_body_la(
             L::set(ap[v], e, fac ? T(1) - hp.lr_pu * hp.reg_pu : T(1));
         }
     }
-    // err_col > 0: lane d < kB of a bank's err vector goes to row d & ~1 (its pair's checkpoint),
-    // column err_col + (d & 1)
+    // err_col > 0: lane d < kB of a bank's err vector goes to its pair's checkpoint row (the
+    // bank's row d / 2), column err_col + (d & 1)
     const uint32_t ce = (ER && lane < kB)
-                            ? (uint32_t)(((lane & ~1) * ldq + err_col + (lane & 1)) * sizeof(T))
+                            ? (uint32_t)(((lane >> 1) * ldq + err_col + (lane & 1)) * sizeof(T))
                             : kLogOob;
     const T lr_bu = biased ? hp.lr_bu : T(0);
     const T abu = T(1) - lr_bu * hp.reg_bu;
@@ -921,7 +930,9 @@ __device__ __forceinline__ void epoch_body_la(
         if (n * 2 > prio_len) __builtin_amdgcn_s_setprio(3);
         else if (n * 4 > prio_len) __builtin_amdgcn_s_setprio(2);
         else if (n * 8 > prio_len) __builtin_amdgcn_s_setprio(1);
-        const rsrc_t l_rs = make_rsrc(qlog + s * ldq, (uint32_t)n * qrow);
+        // CK: the user's checkpoint rows, one per pair, packed (ck_row0); else row k per rating
+        const rsrc_t l_rs = CK ? make_rsrc(qlog + ck_row0(s, u) * ldq, (uint32_t)((n + 1) / 2) * qrow)
+                               : make_rsrc(qlog + s * ldq, (uint32_t)n * qrow);
         const rsrc_t e_rs = make_rsrc(CK && !ER ? elog + s : qlog, (uint32_t)n * sizeof(T));
         const int32_t *__restrict__ it = items + s;
         const T *__restrict__ rt = ratings + s;
@@ -975,12 +986,12 @@ __device__ __forceinline__ void epoch_body_la(
                 for (int x = 0; x < kLg; ++x)
 #pragma unroll
                     for (int v = 0; v < G; ++v)
-                        L::template sts<MF_LOG_AUX>(l_rs, cl[v], (uint32_t)(j0p + x * kCkpt) * qrow,
+                        L::template sts<MF_LOG_AUX>(l_rs, cl[v], (uint32_t)(j0p / kCkpt + x) * qrow,
                                                     lg[x][v]);
                 // err_k: into its pair's row (columns err_col, err_col + 1; the row stores above
                 // leave those columns alone) or to elog[k]; one store per bank either way
                 if constexpr (ER)
-                    Buf<T>::template st<0>(l_rs, ce + (uint32_t)j0p * qrow, ev);
+                    Buf<T>::template st<0>(l_rs, ce + (uint32_t)(j0p / kCkpt) * qrow, ev);
                 else
                     Buf<T>::template st<0>(e_rs, lane < kB ? (uint32_t)(j0p + lane) * sizeof(T) : kLogOob, ev);
                 return;
@@ -2028,8 +2039,9 @@ __device__ __forceinline__ void log_replay_body(
     for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
         const int beg = piece_beg[pc], cnt = piece_beg[pc + 1] - beg;  // 1 <= cnt <= 64
         const int xl = beg + (lane < cnt ? lane : cnt - 1);
-        const int k_l = perm[xl], c_l = ck_pos[xl];  // lane x: rating x and its pair's row
-        const int odd_l = k_l - c_l;                  // 1: k = c + 1 (the row as stored)
+        // lane x: rating x, its pair's (packed) checkpoint row and parity (ck_pos = 2 row + odd)
+        const int k_l = perm[xl], ck_l = ck_pos[xl];
+        const int c_l = ck_l >> 1, odd_l = ck_l & 1;  // odd 1: k = c + 1 (the row as stored)
         // err_k: gathered from elog, or (err_col > 0) read from the row below
         const T ek_l = lane < cnt && err_col <= 0 ? elog[k_l] : T(0);  // lanes >= cnt: weight 0
         // the piece's item row (snapshot) -> D = lrp o q_i
@@ -3322,7 +3334,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 910; }
+int mf_version(void) { return 920; }
 
 #ifndef MF_SOURCE_HASH
 #define MF_SOURCE_HASH "unknown"

@@ -150,13 +150,24 @@ def chain_schedule(users, row_ptr, n_chains, user_cost=16):
     return out.ravel()
 
 
-def ckpt_positions(row_ptr, perm, interval, pos_user=None):
-    """Checkpoint position of every log position (mf_log_replay's ck_pos): for rating k of user
-    u, k - ((k - row_ptr[u]) mod interval).  pos_user: position_users(row_ptr), if at hand."""
+def ck_row0(row_ptr):
+    """First packed checkpoint row of every user, (row_ptr[u] + u + 1) // 2 (the kernels'
+    ck_row0): pair m of user u is row ck_row0[u] + m; the log holds ck_row0[n_users] rows."""
+    row_ptr = np.asarray(row_ptr, np.int64)
+    return (row_ptr + np.arange(len(row_ptr), dtype=np.int64) + 1) >> 1
+
+
+def ckpt_positions(row_ptr, perm, interval=2, pos_user=None):
+    """mf_log_replay's ck_pos of every log position: 2 * (packed checkpoint row of the rating's
+    pair) + (the rating's parity within its user).  pos_user: position_users(row_ptr), if at
+    hand."""
+    if interval != 2:
+        raise ValueError("the checkpoint log stores one row per pair of ratings")
     row_ptr = np.asarray(row_ptr, np.int64)
     k = np.asarray(perm, np.int64)
     u = (position_users(row_ptr) if pos_user is None else pos_user)[k]
-    return (k - ((k - row_ptr[u]) % interval)).astype(np.int32)
+    j = k - row_ptr[u]
+    return (2 * (ck_row0(row_ptr)[u] + (j >> 1)) + (j & 1)).astype(np.int32)
 
 
 class Predictor:
@@ -346,8 +357,9 @@ class MFEngine(ItemSync, Predictor):
         # checkpoint log with MF_EPOCH_ERR_IN_ROW where the row has room: each pair's two errors
         # ride in its checkpoint row's padding (the replay gathers no elog entries)
         e0 = ((self.K + 2) & ~1) if self.dtype == _lib.MF_F32 else self.K + 1
-        self.err_in_row = (self.ckpt and e0 + 2 <= self.ldq
-                           and os.environ.get("SURPRISE_AMD_ERR_IN_ROW", "1") != "0")
+        # (read-only after construction: elog is sized for it)
+        self._err_in_row = (self.ckpt and e0 + 2 <= self.ldq
+                            and os.environ.get("SURPRISE_AMD_ERR_IN_ROW", "1") != "0")
         C = _lib.load().mf_ckpt_interval() if self.ckpt else 0
         _pu = []
         pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
@@ -469,15 +481,21 @@ class MFEngine(ItemSync, Predictor):
             if len(deg) and int(deg.max()) * ldq * esz >= (1 << 30):
                 raise _lib.SurpriseAMDError("a user's delta-log segment would exceed 1 GiB; "
                                             "use mode='atomic'")
-            self.qlog = z(max(k_hi - k_lo, 1), ldq)
-            # the kernels index the log by absolute CSR position k
-            self._qlog_base = self.qlog.data_ptr() - k_lo * ldq * esz
+            if self.ckpt:  # one packed row per pair of ratings (ck_row0)
+                rows = int(ck_row0(row_ptr)[-1])
+                if rows >= (1 << 30):
+                    raise _lib.SurpriseAMDError("checkpoint log too large for 32-bit positions")
+                self.qlog = z(max(rows, 1), ldq)
+                self._qlog_base = self.qlog.data_ptr()
+            else:  # the gradient log: the kernels index it by absolute CSR position k
+                self.qlog = z(max(k_hi - k_lo, 1), ldq)
+                self._qlog_base = self.qlog.data_ptr() - k_lo * ldq * esz
             # per chunk: the main group's piece sums, then the heavy group's
             self.sums = z(max(lg["n_pieces"] + (lg["heavy"]["n_pieces"] if lg["heavy"] else 0)
                               for lg in self.logs), ldq)
-            if self.ckpt:
-                self.elog = z(k_hi - k_lo + 64)
-                self._elog_base = self.elog.data_ptr() - k_lo * esz
+            if self.ckpt:  # (errors in the rows: elog is never read or written)
+                self.elog = z(64 if self.err_in_row else k_hi - k_lo + 64)
+                self._elog_base = self.elog.data_ptr() - (0 if self.err_in_row else k_lo * esz)
         snap_q = self.world > 1 and self.mode != _lib.MF_MODE_LOG
         self.qb_s = z(I, ldq) if snap_q else None
         self.yj_s = z(I, ld) if (self.world > 1 and self.yj is not None) else None
@@ -485,6 +503,11 @@ class MFEngine(ItemSync, Predictor):
         self._hyper = _lib.MfHyper(**(hyper or {}))
         if not self.biased:
             self._hyper.global_mean = 0.0
+
+    @property
+    def err_in_row(self):
+        """Checkpoint log with each pair's errors in its row's padding (MF_EPOCH_ERR_IN_ROW)."""
+        return self._err_in_row
 
     LPT_PER_SIMD = 0      # checkpoint-log epoch: LPT user chains per SIMD (0: one wave per user;
                           # measured at ML-1M: 1 / 2 / 4 chains per SIMD no faster than 0)

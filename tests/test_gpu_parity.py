@@ -444,10 +444,11 @@ def test_native_fork_and_kernel_join_equal_torch_events(torch, request, monkeypa
 
 @pytest.mark.parametrize("K,dtype,heavy", [(100, "float32", 0.25), (20, "float64", 0.0),
                                             (61, "float64", 0.25)])
-def test_errors_in_checkpoint_rows_equal_elog(torch, u1, K, dtype, heavy):
+def test_errors_in_checkpoint_rows_equal_elog(torch, u1, monkeypatch, K, dtype, heavy):
     """MF_EPOCH_ERR_IN_ROW (each pair's errors stored in its checkpoint row's padding, read back
-    by the replay from the loaded row) against the errors in elog: the same values reach the same
-    operations, so the fits are bit-identical (split and unsplit chunks)."""
+    by the replay from the loaded row) against the errors in elog (SURPRISE_AMD_ERR_IN_ROW=0):
+    the same values reach the same operations, so the fits are bit-identical (split and unsplit
+    chunks)."""
     from surprise_amd.engine import MFEngine
     ts, _ = u1
     row_ptr, items, ratings = ts.csr()
@@ -457,10 +458,10 @@ def test_errors_in_checkpoint_rows_equal_elog(torch, u1, K, dtype, heavy):
     pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
     out = []
     for in_row in (True, False):
+        monkeypatch.setenv("SURPRISE_AMD_ERR_IN_ROW", "1" if in_row else "0")
         eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype=dtype,
                        mode="log", heavy=heavy)
-        assert eng.ckpt and eng.err_in_row
-        eng.err_in_row = in_row
+        assert eng.ckpt and eng.err_in_row == in_row
         eng.set_factors(pu0, qi0)
         eng.run_epochs(3)
         out.append(eng.get_factors())

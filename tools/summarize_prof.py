@@ -85,7 +85,9 @@ if fetch and write and bench_line:
                          "passes of %d epochs, every kernel of the step)" % (tag, PMC_STEPS),
                "workload": cfg["workload"]}
     summary["traffic"] = traffic
-    name = "traffic_%s_k%d_%s.json" % (cfg["algo"], cfg["n_factors"], cfg.get("shape", "ml-1m"))
+    dt = cfg.get("dtype", "f32")
+    name = "traffic_%s_k%d_%s%s.json" % (cfg["algo"], cfg["n_factors"], cfg.get("shape", "ml-1m"),
+                                         "" if dt == "f32" else "_" + dt)
     with open(os.path.join(prof, name), "w") as f:
         json.dump(traffic, f, indent=1)
 hit, miss = pmc("l2", "TCC_HIT_sum"), pmc("l2", "TCC_MISS_sum")
