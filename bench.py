@@ -48,6 +48,14 @@ SHAPE_DEFAULTS = {  # shape -> (algo, n_factors, scaling)
 }
 
 
+_T0 = time.time()
+
+
+def note(msg):
+    """Progress on stderr (a long run keeps writing: the GPU pool's watchdog sees it alive)."""
+    print("[bench %6.1fs] %s" % (time.time() - _T0, msg), file=sys.stderr, flush=True)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -62,6 +70,8 @@ def parse():
                         "ml-1m, f32 for c4 / c5 (fp64 K=128 item rows exceed the 1 KiB "
                         "lookahead layout and the fp64 log would not fit C4 on one GPU)")
     p.add_argument("--chunks", type=int, default=1)
+    p.add_argument("--merge", default=None, choices=["count", "recency"],
+                   help="log schedule's item fold (default: the engine's)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rmse", action="store_true")
     p.add_argument("--no-svdpp", action="store_true", help="skip the SVD++ C3 leg")
@@ -363,6 +373,7 @@ def main():
     csr, test, n_items, n_users_global, desc = workload(args, rank, world)
     row_ptr, items, ratings = csr
     n_train = int(row_ptr[-1])
+    note("workload ready: %d training ratings on rank %d" % (n_train, rank))
 
     import torch
     from surprise_amd.dist import DistContext
@@ -383,14 +394,17 @@ def main():
         pu, qi, yj = init_tables(args.shape, rank, n_users, n_items, k, a == "svdpp",
                                  getattr(workload, "user_lo", 0))
         eng = MFEngine(csr, n_items, k, algo=a, hyper=hyper_for(a, gm), mode=md,
-                       dtype=TORCH_DTYPE[dt], n_chunks=args.chunks, world=world)
+                       dtype=TORCH_DTYPE[dt], n_chunks=args.chunks, world=world,
+                       **({"merge": args.merge} if args.merge else {}))
         eng.set_factors(pu, qi, yj=yj)
         eng._prepare(ctx)  # global per-item counts (all ranks)
         return eng
 
     torch.cuda.reset_peak_memory_stats()
     eng = make_engine()
+    note("engine ready")
     elapsed, phases = run_steps(eng, ctx, args.steps, args.warmup, torch)
+    note("timed steps done")
     elapsed = max_over_ranks(ctx, elapsed, torch)
     dev_bytes = max_over_ranks(ctx, float(torch.cuda.max_memory_allocated()), torch)
     updates = sum_over_ranks(ctx, [float(n_train)], torch)[0] * args.steps
@@ -450,6 +464,7 @@ def main():
     if not args.no_rmse:
         result["rmse"] = rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch,
                                   make_engine, oracle_cache)
+        note("rmse leg done")
 
     small = world == 1 and args.shape == "ml-1m" and K == 100
     if small and args.legs and headline:
@@ -529,6 +544,17 @@ def oracle_rmse(args, csr, test, n_items, K, gm, cache):
     return cache["rmse"], cache["seconds"]
 
 
+def data_fingerprint(csr, test):
+    """sha256[:16] over the training CSR and the held-out triples (user, item as int32; rating
+    as float64): ties a committed golden value to the exact synthetic data it was made on."""
+    import hashlib
+    h = hashlib.sha256()
+    tu, ti, tr = test
+    for a in (*csr, np.asarray(tu, np.int32), np.asarray(ti, np.int32), np.asarray(tr, np.float64)):
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()[:16]
+
+
 def scale_golden(args, E):
     """The committed fp64-oracle held-out RMSE of this c4 / c5-shard workload after E epochs
     (tests/golden/scale_golden.json, made by tests/golden/make_scale_golden.py), or None."""
@@ -569,6 +595,9 @@ def rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch, mak
         out["tolerance"] = 1e-3
     else:
         g = scale_golden(args, E)
+        if g is not None and world == 1 and data_fingerprint(csr, test) != g["data_fingerprint"]:
+            raise SystemExit("the %s workload differs from the one scale_golden.json was made on"
+                             % args.shape)
         if g is not None:
             out["reference_oracle_fp64"] = g["rmse_by_epoch"][E - 1]
             out["reference_source"] = ("tests/golden/scale_golden.json (%s; data fingerprint %s)"

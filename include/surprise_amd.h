@@ -119,12 +119,18 @@ int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
  * exact per-user affine form: per user, one gather of y_j (j in I_u), the sequential rating
  * loop with u_impl maintained incrementally, and one affine write-back y_j <- A y_j + c
  * (stores in MF_MODE_PLAIN, float atomics of (A-1) y_j + c otherwise).  yj [n_items][ldu].
- * Always biased (SVDpp has no option).
+ * Always biased (SVDpp has no option).  status (nullable device int32, MF_EPOCH_SVDPP_HELPERS
+ * only; zeroed by the caller, OR-ed by the kernel): bit MF_HX_HELPER_TIMEOUT -- a helper wave
+ * waited past its bound and stopped, q deltas were lost, the item table is invalid;
+ * bit MF_HX_CHAIN_FALLBACK -- a chain found no room in its ring within the bound and issued a
+ * bank's atomics itself (results intact).  Every wait is bounded: nothing hangs the GPU.
  */
+#define MF_HX_HELPER_TIMEOUT 1
+#define MF_HX_CHAIN_FALLBACK 2
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
                    const mf_hyper_t *hp, int32_t mode, void *qlog, void *ycbuf, int32_t n_waves,
-                   int32_t flags, int32_t dtype, void *stream);
+                   int32_t flags, int32_t *status, int32_t dtype, void *stream);
 
 /*
  * SVD++ deferred y update (MF_MODE_ATOMIC with ycbuf != NULL in mf_svdpp_epoch): the epoch kernel
@@ -147,13 +153,33 @@ int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *
              int32_t dtype, void *stream);
 
 /*
+ * Recency weights of a chunk's logged gradients (mf_log_reduce / mf_log_replay, then
+ * mf_log_apply with MF_MERGE_RECENCY): the gradient of a rating at position pos among the
+ * chunk's N ratings of its item (users in order, every rank) is weighted by (1 - eta)^(N-1-pos),
+ * eta = lr_qi (<p^2> + reg_qi) in factor columns and lr_bi (1 + reg_bi) in the bias column
+ * (n_factors), <p^2> = p2stat[0] / p2stat[1] -- the sequential reference's steps on the row, to
+ * first order.
+ */
+typedef struct mf_recency {
+    const int32_t *rpos;    /* [perm entries] the rating's position among this rank's ratings of
+                               its item in the chunk (users in order)                         */
+    const int32_t *pos0;    /* [n_items], nullable: the chunk's ratings of the item on earlier
+                               ranks (added to rpos)                                          */
+    const int32_t *totals;  /* [n_items] N: the chunk's ratings of the item on every rank      */
+    const double *p2stat;   /* {sum p^2, count} at the chunk start, every rank                */
+} mf_recency_t;
+
+/*
  * Delta-log merge, step 1 (MF_MODE_LOG): sums[p][c] = sum_{x in [piece_beg[p], piece_beg[p+1])}
- * qlog[perm[x]][c] for c < n_cols (zero for n_cols <= c < ld), summed in x order.  perm lists the
- * chunk's log rows grouped by item; an item's rows are cut into consecutive pieces of 1..64 rows.
+ * w_x qlog[perm[x]][c] for c < n_cols (zero for n_cols <= c < ld), summed in x order.  perm lists
+ * the chunk's log rows grouped by item; an item's rows are cut into consecutive pieces of 1..64
+ * rows.  rec NULL: w = 1; else the recency weights (piece_item and hp required; the bias column
+ * is n_cols - 1).
  */
 int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *perm,
-                  const int32_t *piece_beg, int64_t n_pieces, void *sums, int32_t dtype,
-                  void *stream);
+                  const int32_t *piece_beg, int64_t n_pieces, void *sums,
+                  const int32_t *piece_item, const mf_hyper_t *hp, const mf_recency_t *rec,
+                  int32_t dtype, void *stream);
 
 /*
  * Delta-log merge, step 1 for the checkpoint form (mf_svd_epoch with elog): the same sums as
@@ -167,11 +193,13 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
  * mf_log_apply.  piece_item (nullable): the item of each piece (else read through perm and the
  * CSR items).  Requires ldq * sizeof(dtype) <= 1 KiB.  flags: bits 8..15 an XCD mask as in
  * mf_svd_epoch (MF_EPOCH_XCD_SHIFT), 0 = every XCD; MF_EPOCH_ERR_IN_ROW: errors in the rows.
+ * rec (nullable): each gradient err_k * p_k weighted by its recency weight (mf_recency_t).
  */
 int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_factors,
                   const mf_csr_t *csr, const void *qb, const mf_hyper_t *hp, const int32_t *perm,
                   const int32_t *ck_pos, const int32_t *piece_beg, int64_t n_pieces, void *sums,
-                  const int32_t *piece_item, int32_t flags, int32_t dtype, void *stream);
+                  const int32_t *piece_item, const mf_recency_t *rec, int32_t flags,
+                  int32_t dtype, void *stream);
 
 /*
  * mf_svd_epoch in MF_MODE_LOG with the checkpoint log (elog != NULL, the lookahead body), also
@@ -208,7 +236,9 @@ int mf_ckpt_interval(void);
  *   MF_MERGE_SUM:   w = 1;
  *   MF_MERGE_COUNT: w = (1 - (1-eta)^N) / (N eta), N = totals[i] (ratings of item i in the chunk,
  *                   all ranks), eta = lr_bi (1 + reg_bi) in bias_col and lr_qi (<p^2> + reg_qi)
- *                   in factor columns, <p^2> = p2stat[0] / p2stat[1] (mf_sumsq's two doubles).
+ *                   in factor columns, <p^2> = p2stat[0] / p2stat[1] (mf_sumsq's two doubles);
+ *   MF_MERGE_RECENCY: the sums carry the recency weights (mf_recency_t); adds
+ *                   lr o (S_i - W reg o qb[i]) with W = (1 - (1-eta)^N) / eta, the weights' sum.
  * stat_next (nullable, 2 device doubles, not p2stat): user_sq NULL: set to {0, 0} -- the next
  * chunk's mf_sumsq accumulator, cleared here instead of by a separate fill; user_sq != NULL
  * (mf_svd_epoch_sq's array, n_users rows): set to mf_user_sq_reduce's {sum, n_users * n_factors}
@@ -227,6 +257,7 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
 #define MF_MERGE_COUNT 1 /* count-aware: SUM while a row's steps are small, count-weighted MEAN
                             once they saturate (item factors and biases)                           */
 #define MF_MERGE_MEAN  2 /* count-weighted MEAN: sum_r (n_r / N) d_r (SVD++ implicit factors)      */
+#define MF_MERGE_RECENCY 3 /* mf_log_apply: sums weighted by recency (mf_recency_t), the default  */
 
 /*
  * Item-side merge of an epoch-chunk across ranks for MF_MODE_PLAIN /
@@ -339,8 +370,8 @@ int mf_predict(int64_t n, const int32_t *u, const int32_t *i, const void *pu, co
  * (default_prediction(), the trainset mean), minus `offset`, clipped to [lo, hi]; the true rating
  * is r[x] - offset.  Accumulates out[0] += sum err^2, out[1] += sum |err|, out[2] += n (three
  * device doubles, zeroed by the caller): rmse = sqrt(out[0]/out[2]), mae = out[1]/out[2].
- * est and r are dtype.  Replaces the per-Prediction Python loop of the reference's
- * test() + rmse() (algo_base.py:191-218).
+ * est is dtype, r is always fp64 (the reference's r_ui - est is fp64).  Replaces the
+ * per-Prediction Python loop of the reference's test() + rmse() (algo_base.py:191-218).
  */
 int mf_rating_errors(int64_t n, const void *est, const int32_t *impossible, const void *r,
                      double fallback, double offset, double lo, double hi, double *out,
@@ -350,6 +381,12 @@ int mf_rating_errors(int64_t n, const void *est, const int32_t *impossible, cons
  * yj is replica 0, imp is [n_users][ldu]. */
 int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, int32_t ldu, void *imp,
                            int32_t n_factors, int32_t dtype, void *stream);
+
+/* *ok = 1 if the current device deals workgroups round-robin over 8 XCDs (workgroup b on XCD
+ * b mod 8, read from the XCC_ID register; checked once per device): the layout the XCD masks
+ * of mf_svd_epoch / mf_log_replay (flags bits 8..15) assume.  Masked launches are refused
+ * (MF_E_UNSUPPORTED) where it does not hold. */
+int mf_xcd_layout(int32_t *ok);
 
 /* Self-test of the XCD id register: out[b] = HW_REG_XCC_ID of workgroup b, b < n_blocks. */
 int mf_selftest_xcc(int32_t *out, int32_t n_blocks, void *stream);

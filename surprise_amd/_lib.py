@@ -17,7 +17,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "surprise_amd.h")
 MF_F32, MF_F64 = 0, 1
 MF_MODE_PLAIN, MF_MODE_ATOMIC, MF_MODE_LOG = 0, 1, 2
 MODES = {"plain": MF_MODE_PLAIN, "atomic": MF_MODE_ATOMIC, "log": MF_MODE_LOG}
-MF_MERGE_SUM, MF_MERGE_COUNT, MF_MERGE_MEAN = 0, 1, 2
+MF_MERGE_SUM, MF_MERGE_COUNT, MF_MERGE_MEAN, MF_MERGE_RECENCY = 0, 1, 2, 3
 MF_EPOCH_DUP_ITEMS = 1
 MF_EPOCH_XCD_SHIFT = 8  # flags bits 8..15: XCD mask (include/surprise_amd.h)
 MF_EPOCH_SVDPP_HELPERS = 2
@@ -41,6 +41,11 @@ class MfCsr(ctypes.Structure):
                 ("n_items", ctypes.c_int32)]
 
 
+class MfRecency(ctypes.Structure):
+    _fields_ = [("rpos", ctypes.c_void_p), ("pos0", ctypes.c_void_p), ("totals", ctypes.c_void_p),
+                ("p2stat", ctypes.c_void_p)]
+
+
 _vp, _i32, _i64, _dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
 
 # name -> argtypes (all return int except mf_last_error)
@@ -48,7 +53,7 @@ SIGNATURES = {
     "mf_svd_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32, _i32,
                      ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_svdpp_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp, _i32,
-                       ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _i32, _vp],
+                       ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _vp, _i32, _vp],
     "mf_svdpp_y_fold": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32,
                         _vp],
     "mf_svd_epoch_sq": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32,
@@ -56,9 +61,11 @@ SIGNATURES = {
     "mf_sumsq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
     "mf_user_sq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
     "mf_user_sq_reduce": [_vp, _i64, _i32, _vp, _vp],
-    "mf_log_reduce": [_vp, _i32, _i32, _vp, _vp, _i64, _vp, _i32, _vp],
+    "mf_log_reduce": [_vp, _i32, _i32, _vp, _vp, _i64, _vp, _vp, ctypes.POINTER(MfHyper),
+                      ctypes.POINTER(MfRecency), _i32, _vp],
     "mf_log_replay": [_vp, _vp, _i32, _i32, ctypes.POINTER(MfCsr), _vp,
-                      ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _vp],
+                      ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _vp,
+                      ctypes.POINTER(MfRecency), _i32, _i32, _vp],
     "mf_ckpt_interval": [],
     "mf_log_apply": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
                      ctypes.POINTER(MfHyper), _vp, _i32, _vp, _i32, _vp, _vp, _i64, _i32, _vp],
@@ -79,6 +86,7 @@ SIGNATURES = {
     "mf_svdpp_user_implicit": [ctypes.POINTER(MfCsr), _vp, _i32, _vp, _i32, _i32, _vp],
     "mf_selftest_wave_sum": [_vp, _vp, _i32, _i32, _vp],
     "mf_selftest_xcc": [_vp, _i32, _vp],
+    "mf_xcd_layout": [ctypes.POINTER(ctypes.c_int32)],
     "mf_event_create": [ctypes.POINTER(ctypes.c_void_p)],
     "mf_event_destroy": [_vp],
     "mf_event_record": [_vp, _vp],
@@ -140,6 +148,14 @@ def require_gpu():
             "There is no CPU fallback for the training path.")
     load()
     return torch
+
+
+def xcd_layout_ok() -> bool:
+    """The 8-XCD round-robin workgroup dispatch the XCD-masked launches assume (mf_xcd_layout,
+    checked once per device on the GPU)."""
+    ok = ctypes.c_int32(0)
+    call("mf_xcd_layout", ctypes.byref(ok))
+    return bool(ok.value)
 
 
 def header_symbols(path: str = HEADER_PATH):

@@ -25,6 +25,7 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <mutex>
 #include <type_traits>
 
 #include "../../include/surprise_amd.h"
@@ -39,16 +40,13 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    bool hx, double *psq, int err_col, void *stream);
+                    bool hx, double *psq, int err_col, int32_t *status, void *stream);
 }  // namespace mf_ext
 
 namespace {
 
 constexpr int kWave = 64;
 constexpr int kBlock = 256;  // 4 waves per workgroup
-#ifndef MF_EXP_YATOM
-#define MF_EXP_YATOM 1
-#endif
 #ifndef MF_PF
 #define MF_PF 8
 #endif
@@ -705,16 +703,12 @@ __device__ __forceinline__ void epoch_body(
             if (FULL) {  // real rows only: the row offset rides in soffset, no address math
 #pragma unroll
                 for (int v = 0; v < G; ++v) {
-#ifndef MF_EXP_NO_LOG_STORE
                     if (LOG) L::template sts<0>(l_rs, cl[v], (uint32_t)(j0 + d) * qrow, qd[v]);
-#endif
                     if (MODE == kPlain) L::template sts<0>(q_rs, cq[v], off, stv[v]);
                 }
-#ifndef MF_EXP_NO_QATOM
                 if (ATOM)
 #pragma unroll
                     for (int u = 0; u < U; ++u) atom_add1(q_rs, qb, q_oob, cq1[u], off, qd1[u]);
-#endif
             } else {     // masked slots: push the offset past the table / log segment
                 const uint32_t moff = valid ? off : off + q_oob;
 #pragma unroll
@@ -762,11 +756,7 @@ __device__ __forceinline__ void epoch_body(
         __builtin_amdgcn_s_setprio(0);
 
         // SVD++ (3): y_j <- A y_j + c for every j in I_u
-#ifdef MF_EXP_NO_YWALK2
-        if (false) {
-#else
         if (PP) {
-#endif
             // c obeys the same recurrence as imp (c' = decay c + lr_yj err q / sqrt n) from 0
             // instead of imp0, so c = (imp - A imp0) / sqrt n: no per-rating c update
             vec cacc[G];
@@ -785,7 +775,7 @@ __device__ __forceinline__ void epoch_body(
                 for (int a = 0; a < kYB; ++a)
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-                        if (YATOM && MF_EXP_YATOM)
+                        if (YATOM)
                             atom_add1(y_rs, yj, y_oob, cy1[u], ro[a], (A - T(1)) * g[a][u] + cacc1[u]);
                         else
                             Buf<T>::template st<0>(y_rs, ro[a] + cy1[u], A * g[a][u] + cacc1[u]);
@@ -978,9 +968,6 @@ __device__ __forceinline__ void epoch_body_la(
             }
         };
         auto flush = [&](const int j0p) {  // log rows j0p .. j0p + kB - 1
-#if defined(MF_EXP_LA_NO_STORE)  // timing experiment only: no log written (wrong results)
-            return;
-#endif
             if constexpr (CK) {
 #pragma unroll
                 for (int x = 0; x < kLg; ++x)
@@ -996,29 +983,12 @@ __device__ __forceinline__ void epoch_body_la(
                     Buf<T>::template st<0>(e_rs, lane < kB ? (uint32_t)(j0p + lane) * sizeof(T) : kLogOob, ev);
                 return;
             }
-#if defined(MF_EXP_PAIR_STORE)  // timing experiment only: 2 rows per dwordx4 (wrong layout)
-#pragma unroll
-            for (int d = 0; d < kB; d += 2)
-#pragma unroll
-                for (int v = 0; v < G; ++v) {
-                    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-                    const auto a = __builtin_bit_cast(unsigned long long, lg[d][v]);
-                    const auto b = __builtin_bit_cast(unsigned long long, lg[d + 1][v]);
-                    u4 w = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
-                    __builtin_amdgcn_raw_buffer_store_b128(w, l_rs, cl[v] < kLogOob ? 2 * cl[v] : kLogOob,
-                                                           (uint32_t)(j0p + d) * qrow, 0);
-                }
-#else
 #pragma unroll
             for (int d = 0; d < kB; ++d) {
-#if defined(MF_EXP_HALF_STORE)  // timing experiment only: every other row
-                if (d & 1) continue;
-#endif
 #pragma unroll
                 for (int v = 0; v < G; ++v)
                     L::template sts<MF_LOG_AUX>(l_rs, cl[v], (uint32_t)(j0p + d) * qrow, lg[d][v]);
             }
-#endif
         };
         {
             uint32_t go0;
@@ -1197,16 +1167,28 @@ struct PPRing {
     int tail[kHxHelpers];
 };
 
+// ring hand-off: the count is stored with release and read with acquire (workgroup scope: on
+// gfx950 an s_waitcnt lgkmcnt(0) around the LDS access, no vmcnt wait), so the slots' rows are
+// ordered before / after it by the memory model, not by the hardware's LDS ordering alone
 __device__ __forceinline__ int lds_load(int *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void lds_store(int *p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// hx status word bits (mf_svdpp_epoch's status): a helper timed out waiting for rows (it exits;
+// rows later pushed for it are lost: the chunk's item rows are invalid) / a chain found no room
+// in the ring within the bound and issued that bank's atomics itself (results intact)
+constexpr int32_t kHxHelperTimeout = MF_HX_HELPER_TIMEOUT, kHxChainFallback = MF_HX_CHAIN_FALLBACK;
+__device__ __forceinline__ void set_status(int32_t *status, int32_t bit) {
+    if (status && (threadIdx.x & (kWave - 1)) == 0)  // (a vector atomic, written through)
+        __hip_atomic_fetch_or(status, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // helper wave h of a chain: issue the atomics of the slots t = h (mod kHxHelpers)
 template <typename T, int G>
-__device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_items)
+__device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_items,
+                               int32_t *status)
 {
     constexpr int R = PPRing<T, G>::R;
     constexpr int U = Lane1<T, G>::U;
@@ -1231,7 +1213,10 @@ __device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_
                 if (t >= hd) break;
             } else {
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > kSpinMax) break;
+                if (++spins > kSpinMax) {  // (never hang the GPU: report and stop)
+                    set_status(status, kHxHelperTimeout);
+                    break;
+                }
                 continue;
             }
         }
@@ -1240,24 +1225,15 @@ __device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_
         for (int tt = t + ((h - t % kHxHelpers) + kHxHelpers) % kHxHelpers; tt < hd;
              tt += kHxHelpers) {
             const int slot = tt % R;
-#if defined(MF_EXP_ATOM_SPREAD)  // timing experiment only (wrong results): rows spread uniformly
-            const uint32_t off = (uint32_t)(((uint32_t)(blockIdx.x * 131 + tt * 7919)) % n_items) * qrow;
-#else
             const uint32_t off = __builtin_amdgcn_readfirstlane(ring->off[slot]);
-#endif
             T v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) v[u] = img[slot * kSlotT + lane + kWave * u];
-#if !defined(MF_EXP_NO_QATOM)
 #pragma unroll
             for (int u = 0; u < U; ++u) atom_add1(q_rs, qb, q_oob, cq1[u], off, v[u]);
-#else
-            asm volatile("" ::"v"(v[0]), "s"(off));
-#endif
         }
         t = hd;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slots' reads have returned
-        lds_store(&ring->tail[h], t);
+        lds_store(&ring->tail[h], t);  // (release: the slots' reads before the count)
     }
 }
 
@@ -1282,7 +1258,8 @@ __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *ycbuf, int K,
-    Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, PPRing<T, G> *ring)
+    Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, PPRing<T, G> *ring,
+    int32_t *status)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -1367,11 +1344,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
             T acc1[U];
 #pragma unroll
             for (int uu = 0; uu < U; ++uu) acc1[uu] = T(0);
-#if defined(MF_EXP_NO_YGATHER)  // timing experiment only (wrong results): u_impl = 0
-            for (int x0 = 0; x0 < 0; x0 += kWave) {
-#else
             for (int x0 = 0; x0 < n; x0 += kWave) {
-#endif
                 const int gid = it[x0 + lane < n ? x0 + lane : n - 1];
                 const int cnt = n - x0 < kWave ? n - x0 : kWave;
                 for (int x = 0; x < cnt; x += kYB) {
@@ -1415,9 +1388,19 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 for (int v = 0; v < G; ++v) bank[bk][d][v] = L::template lds<kSc1>(q_rs, cq[v], off);
             }
         };
+        auto atomics = [&]() {  // the previous bank's q deltas as float atomics, from this wave
+#pragma unroll
+            for (int d = 0; d < kB; ++d) {
+                T d1[U];
+                to_lane1<G>(dl[d], d1);
+#pragma unroll
+                for (int uu = 0; uu < U; ++uu) atom_add1(q_rs, qb, q_oob, cq1[uu], dlo[d], d1[uu]);
+            }
+        };
         auto flush = [&]() {  // the float atomics of the previous bank's ratings
             if constexpr (HX) {  // ... handed to the helper waves through the ring
                 constexpr int R = PPRing<T, G>::R;
+                bool room = false;
                 for (int spins = 0; spins < kSpinMax; ++spins) {  // room for kB rows
                     int m = lds_load(&ring->tail[0]);
 #pragma unroll
@@ -1425,10 +1408,17 @@ __device__ __forceinline__ void epoch_body_pp_la(
                         const int th = lds_load(&ring->tail[h]);
                         m = th < m ? th : m;
                     }
-                    if (pushed + kB - m <= R) break;
+                    if (pushed + kB - m <= R) {
+                        room = true;
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
                 }
-                asm volatile("" ::: "memory");
+                if (!room) {  // (no unconsumed slot is ever overwritten: this bank's atomics here)
+                    set_status(status, kHxChainFallback);
+                    atomics();
+                    return;
+                }
 #pragma unroll
                 for (int d = 0; d < kB; ++d) {
                     const int slot = (pushed + d) % R;
@@ -1437,19 +1427,9 @@ __device__ __forceinline__ void epoch_body_pp_la(
                     ring->off[slot] = dlo[d];
                 }
                 pushed += kB;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows before the count
-                lds_store(&ring->head, pushed);
+                lds_store(&ring->head, pushed);  // (release: the rows before the count)
             } else {
-#pragma unroll
-                for (int d = 0; d < kB; ++d) {
-                    T d1[U];
-                    to_lane1<G>(dl[d], d1);
-#if !defined(MF_EXP_NO_QATOM)
-#pragma unroll
-                    for (int uu = 0; uu < U; ++uu)
-                        atom_add1(q_rs, qb, q_oob, cq1[uu], dlo[d], d1[uu]);
-#endif
-                }
+                atomics();
             }
         };
         {
@@ -1578,10 +1558,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
         const int u = sched[w];
         if (u >= 0) do_user(u);  // (HX schedules are padded with -1)
     }
-    if constexpr (HX) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        lds_store(&ring->done, 1);
-    }
+    if constexpr (HX) lds_store(&ring->done, 1);
 }
 
 #ifndef MF_LA
@@ -1605,7 +1582,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
         if (elog) {  // deferred y (elog = ycbuf)
             epoch_body_pp_la<T, G, false>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu,
                                           qb, ldq, yj, elog, K, hp, n_items, n_waves_req, xmask,
-                                          nullptr);
+                                          nullptr, nullptr);
             return;
         }
     }
@@ -1629,7 +1606,7 @@ __global__ __launch_bounds__(kBlock) void mf_ckpt_epoch_kernel(MF_EPOCH_PARAMS)
 
 // SVD++ with helper waves (MF_SVDPP_HELPERS): workgroup = chain wave 0 + kHxHelpers atomic waves
 template <typename T, int G>
-__global__ __launch_bounds__(kBlock) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS)
+__global__ __launch_bounds__(kBlock) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS, int32_t *status)
 {
     __shared__ PPRing<T, G> ring;
     const int w = threadIdx.x / kWave;
@@ -1641,13 +1618,10 @@ __global__ __launch_bounds__(kBlock) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS)
     __syncthreads();
     if (w == 0) {
         epoch_body_pp_la<T, G, true>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
-                                     yj, elog, K, hp, n_items, n_waves_req, 0, &ring);
-        if (blockIdx.x >= n_waves_req) {  // (no chain in this workgroup)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            lds_store(&ring.done, 1);
-        }
+                                     yj, elog, K, hp, n_items, n_waves_req, 0, &ring, status);
+        if (blockIdx.x >= n_waves_req) lds_store(&ring.done, 1);  // (no chain in this workgroup)
     } else {
-        pp_ring_helper<T, G>(&ring, w - 1, qb, ldq, n_items);
+        pp_ring_helper<T, G>(&ring, w - 1, qb, ldq, n_items, status);
     }
 }
 
@@ -1659,7 +1633,7 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    bool hx, double *psq, int err_col, void *stream)
+                    bool hx, double *psq, int err_col, int32_t *status, void *stream)
 {
     if ((psq || err_col) && (PP || M != kLog || !elog))
         return set_err(MF_E_UNSUPPORTED, "user_sq / errors in rows: the SVD checkpoint log only");
@@ -1681,7 +1655,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
                                    (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
-                                   cast_hyper<T>(hp), csr->n_items, waves, 0, nullptr, 0);
+                                   cast_hyper<T>(hp), csr->n_items, waves, 0, nullptr, 0, status);
                 return check_launch("mf_svdpp_hx_kernel");
             }
         } else {
@@ -1713,7 +1687,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
 template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
     void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, bool, double *,
-    int, void *);
+    int, int32_t *, void *);
 }  // namespace mf_ext
 #else  // the main translation unit
 
@@ -1927,14 +1901,66 @@ __global__ __launch_bounds__(kBlock) void item_affine_kernel(T *tab, T *snap, in
 // 1/(N eta) for items whose row would have converged within the chunk (plain SUM
 // diverges on ML-1M).  eta as in mf_item_merge.
 
+// The recency-weighted fold (MF_MERGE_RECENCY): the reference applies an item's N steps of a
+// chunk one after the other, each on the row the previous ones left.  To first order (the step
+// d_k = lr (err_k p_k - reg q) taken at the chunk-start row, the row's own decay eta = lr (<p^2>
+// + reg) per step, as in the count-aware weight) the sequential result is
+//     q_N - q_0 = sum_k (1 - eta)^(N - 1 - k) d_k       (k = the step's position, users in order)
+// -- later steps count more, exactly as they do in the reference; the count-aware weight is this
+// with every step given the mean weight.  The replay / reduce weight each rating's gradient by
+// its (1 - eta)^(N - 1 - pos) (eta of the bias column for the bias, of the factor columns else),
+// and mf_log_apply adds lr (S - reg q sum_k (1 - eta)^(N-1-k)).
+struct Recency {
+    const int32_t *rpos;    // per log entry (parallel to perm): position among this rank's
+                            // ratings of the chunk of the same item, users in order; NULL: off
+    const int32_t *pos0;    // per item: the chunk's ratings of the item on earlier ranks (NULL: 0)
+    const int32_t *totals;  // per item: N, the chunk's ratings of the item on every rank
+    const double *p2stat;   // {sum p^2, count} at the chunk start (every rank)
+    double lr_qi, reg_qi, eta_b;
+};
+
+// log(1 - eta) of the factor columns and of the bias column
+__device__ __forceinline__ void recency_logs(const Recency &rc, double &l_q, double &l_b)
+{
+    const double n = rc.p2stat[1];
+    const double p2 = n > 0 ? rc.p2stat[0] / n : 0.0;
+    l_q = log1p(-rc.lr_qi * (p2 + rc.reg_qi));
+    l_b = log1p(-rc.eta_b);
+}
+
+// this lane's entry x of a piece of `item`: (1 - eta)^(N - 1 - pos) for both column kinds
+template <typename T>
+__device__ __forceinline__ void recency_weights(const Recency &rc, double l_q, double l_b,
+                                                int item, int x, T &wf, T &wb)
+{
+    const double back = (double)(rc.totals[item] - 1 - rc.rpos[x] - (rc.pos0 ? rc.pos0[item] : 0));
+    wf = (T)exp(back * l_q);
+    wb = (T)exp(back * l_b);
+}
+
+// per lane and lane group: 1 in the element that holds column c_bias, else 0
+template <typename T, int G>
+__device__ __forceinline__ void bias_selector(int c_bias, typename Lane8<T>::vec (&bsel)[G])
+{
+    using L = Lane8<T>;
+    const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+    for (int v = 0; v < G; ++v)
+#pragma unroll
+        for (int e = 0; e < L::W; ++e)
+            L::set(bsel[v], e, (lane + kWave * v) * L::W + e == c_bias ? T(1) : T(0));
+}
+
 // One wave per piece (<= 64 rows): the piece's log-row indices arrive with ONE vector load
 // (lane l holds perm[beg + l]) and are broadcast with v_readlane, so the row gathers carry no
 // scalar-load round trips; rows are read 16 at a time in the 8-byte lane layout of the epoch
-// kernel (one dwordx2 per lane per 512 B of row).
-template <typename T, int G>
+// kernel (one dwordx2 per lane per 512 B of row).  REC: each row weighted by its recency weight.
+template <typename T, int G, bool REC>
 __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
     const T *__restrict__ qlog, int ld, int n_cols, const int32_t *__restrict__ perm,
-    const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums)
+    const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums,
+    const int32_t *__restrict__ items, const int32_t *__restrict__ piece_item, Recency rc,
+    int bias_col)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -1943,9 +1969,21 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
+    double l_q = 0, l_b = 0;
+    vec bsel[G];
+    if constexpr (REC) {
+        recency_logs(rc, l_q, l_b);
+        bias_selector<T, G>(bias_col, bsel);
+    }
     for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
         const int beg = piece_beg[pc], cnt = piece_beg[pc + 1] - beg;  // 1 <= cnt <= 64
-        const int myk = perm[beg + (lane < cnt ? lane : cnt - 1)];
+        const int xr = beg + (lane < cnt ? lane : cnt - 1);
+        const int myk = perm[xr];
+        T wf_l = T(1), wb_l = T(1);
+        if constexpr (REC) {
+            const int item = piece_item ? piece_item[pc] : items[readlane(myk, 0)];
+            recency_weights(rc, l_q, l_b, item, xr, wf_l, wb_l);
+        }
         vec acc[G];
 #pragma unroll
         for (int v = 0; v < G; ++v) acc[v] = L::splat(T(0));
@@ -1964,9 +2002,18 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
             }
 #pragma unroll
             for (int a = 0; a < kU; ++a)
-                if (x + a < cnt)
+                if (x + a < cnt) {
+                    if constexpr (REC) {
+                        const int xa = x + a < kWave ? x + a : kWave - 1;
+                        const T wf = readlane(wf_l, xa), wb = readlane(wb_l, xa);
 #pragma unroll
-                    for (int v = 0; v < G; ++v) acc[v] += g[a][v];
+                        for (int v = 0; v < G; ++v)
+                            acc[v] += (L::splat(wf) + (wb - wf) * bsel[v]) * g[a][v];
+                    } else {
+#pragma unroll
+                        for (int v = 0; v < G; ++v) acc[v] += g[a][v];
+                    }
+                }
         }
 #pragma unroll
         for (int v = 0; v < G; ++v) {
@@ -2005,14 +2052,14 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
 // One wave per piece (<= 64 ratings): lane x holds rating x's checkpoint offset, parity and
 // err (vector gathers once per piece); per rating v_readlane broadcasts, the row gather and 3
 // packed FMAs.  Two groups of MF_REPLAY_U rows are in flight per wave.
-template <typename T, int G>
+template <typename T, int G, bool REC>
 __device__ __forceinline__ void log_replay_body(
     const T *__restrict__ ckpt, const T *__restrict__ elog, int ldq, int K,
     const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T inv_ap,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
     const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int err_col,
     const int32_t *__restrict__ piece_item, const int64_t wave, const int64_t n_waves,
-    const bool wt)
+    const bool wt, const Recency &rc)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -2036,6 +2083,12 @@ __device__ __forceinline__ void log_replay_body(
             L::set(iap[v], e, fac ? inv_ap : T(1));
         }
     }
+    double l_q = 0, l_b = 0;
+    vec bsel[G];
+    if constexpr (REC) {
+        recency_logs(rc, l_q, l_b);
+        bias_selector<T, G>(K, bsel);
+    }
     for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
         const int beg = piece_beg[pc], cnt = piece_beg[pc + 1] - beg;  // 1 <= cnt <= 64
         const int xl = beg + (lane < cnt ? lane : cnt - 1);
@@ -2046,7 +2099,10 @@ __device__ __forceinline__ void log_replay_body(
         const T ek_l = lane < cnt && err_col <= 0 ? elog[k_l] : T(0);  // lanes >= cnt: weight 0
         // the piece's item row (snapshot) -> D = lrp o q_i
         // (piece_item: the item id without the perm -> items hop on the piece's critical path)
-        const uint32_t qoff = (uint32_t)(piece_item ? piece_item[pc] : items[readlane(k_l, 0)]) * qrow;
+        const int item = piece_item ? piece_item[pc] : items[readlane(k_l, 0)];
+        const uint32_t qoff = (uint32_t)item * qrow;
+        T wf_l = T(1), wb_l = T(1);  // (REC: lane x's recency weights)
+        if constexpr (REC) recency_weights(rc, l_q, l_b, item, xl, wf_l, wb_l);
         vec D[G];
 #pragma unroll
         for (int v = 0; v < G; ++v) D[v] = lrp[v] * L::template lds<0>(q_rs, cq[v], qoff);
@@ -2078,10 +2134,20 @@ __device__ __forceinline__ void log_replay_body(
                 } else {
                     ek = readlane(ek_l, x);
                 }
+                if constexpr (REC) {  // (the weights scale the gradient, not the undone step)
+                    const T wf = readlane(wf_l, x), wb = readlane(wb_l, x);
+                    const T ef = ek * wf, eb = ek * wb;
 #pragma unroll
-                for (int v = 0; v < G; ++v) {
-                    const vec pc_ = iap[v] * (p[y][v] - ek * D[v]);  // p_c from p_{c+1}
-                    acc[v] += ek * (odd ? p[y][v] : pc_);           // g_k = err_k p_k, in order
+                    for (int v = 0; v < G; ++v) {
+                        const vec pc_ = iap[v] * (p[y][v] - ek * D[v]);
+                        acc[v] += (L::splat(ef) + (eb - ef) * bsel[v]) * (odd ? p[y][v] : pc_);
+                    }
+                } else {
+#pragma unroll
+                    for (int v = 0; v < G; ++v) {
+                        const vec pc_ = iap[v] * (p[y][v] - ek * D[v]);  // p_c from p_{c+1}
+                        acc[v] += ek * (odd ? p[y][v] : pc_);           // g_k = err_k p_k, in order
+                    }
                 }
             }
         };
@@ -2160,20 +2226,20 @@ __device__ __forceinline__ void join_arrive(uint32_t *join, int role, uint32_t e
     }
 }
 
-template <typename T, int G>
+template <typename T, int G, bool REC>
 __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     const T *__restrict__ ckpt, const T *__restrict__ elog, int ldq, int K,
     const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T inv_ap,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
     const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int xmask,
     int err_col, const int32_t *__restrict__ piece_item, uint32_t *join, int join_role,
-    uint32_t join_epoch)
+    uint32_t join_epoch, Recency rc)
 {
     int64_t wave, n_waves;
     if (wave_slot(xmask, wave, n_waves))
-        log_replay_body<T, G>(ckpt, elog, ldq, K, items, qb, n_items, lr_pu, inv_ap, perm, ck_pos,
-                              piece_beg, n_pieces, sums, err_col, piece_item, wave, n_waves,
-                              join && join_role == 1);
+        log_replay_body<T, G, REC>(ckpt, elog, ldq, K, items, qb, n_items, lr_pu, inv_ap, perm,
+                                   ck_pos, piece_beg, n_pieces, sums, err_col, piece_item, wave,
+                                   n_waves, join && join_role == 1, rc);
     if (join) join_arrive(join, join_role, join_epoch);
 }
 
@@ -2265,12 +2331,15 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
                 add(ga);
             }
         }
-        // the count-aware weights (one per column kind, the same for every factor column)
+        // the count-aware weights (one per column kind, the same for every factor column);
+        // recency (count_rule 2): the sums arrive weighted, the reg term takes the weights' sum
+        // sum_k (1 - eta)^(N-1-k) = (1 - (1 - eta)^N) / eta = w N
         double w_fac = 1.0, w_bias = 1.0;
         if (count_rule && N > 1.0) {
             w_fac = -expm1(N * l_fac) / (N * eta_fac);
             w_bias = -expm1(N * l_bias) / (N * eta_bias);
         }
+        const bool rec = count_rule == 2;
 #pragma unroll
         for (int v = 0; v < V; ++v) {
             const int c = lane + kWave * v;
@@ -2281,8 +2350,13 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
                 const bool b = c == bias_col;
                 const double w = b ? w_bias : w_fac;
                 // the log holds gradients g_k = err_k pe_k: sum_k d_k = lr (S - N reg q)
-                const T d = (T)(b ? lr_b : lr_f) * (acc[v] - (T)N * (T)(b ? reg_b : reg_f) * q[v]);
-                qb[x] = q[v] + (T)w * d;
+                if (rec) {
+                    qb[x] = q[v] + (T)(b ? lr_b : lr_f) *
+                                       (acc[v] - (T)(w * N) * (T)(b ? reg_b : reg_f) * q[v]);
+                } else {
+                    const T d = (T)(b ? lr_b : lr_f) * (acc[v] - (T)N * (T)(b ? reg_b : reg_f) * q[v]);
+                    qb[x] = q[v] + (T)w * d;
+                }
             }
         }
     }
@@ -3069,10 +3143,10 @@ __global__ __launch_bounds__(kBlock) void y_apply_kernel(
 // accuracy.rmse / mae over the batched estimates (algo_base.py:148-169 finishing, accuracy.py:
 // 22-90): est -> fallback where impossible, minus the reader offset, clipped to the rating scale,
 // against r - offset; out[0] += sum err^2, out[1] += sum |err|, out[2] += count (fp64).
-template <typename T>
+template <typename T>  // (est in the model's dtype; the true ratings always fp64, as r_ui is)
 __global__ __launch_bounds__(kBlock) void rating_errors_kernel(
     int64_t n, const T *__restrict__ est, const int32_t *__restrict__ impossible,
-    const T *__restrict__ r, double fallback, double offset, double lo, double hi,
+    const double *__restrict__ r, double fallback, double offset, double lo, double hi,
     double *__restrict__ out)
 {
     __shared__ double part[2][kBlock / kWave];
@@ -3083,7 +3157,7 @@ __global__ __launch_bounds__(kBlock) void rating_errors_kernel(
         e -= offset;
         e = e < lo ? lo : (e > hi ? hi : e);  // (NaN -> hi, as np.fmax(lo, np.fmin(hi, e)))
         e = e == e ? e : hi;
-        const double d = ((double)r[x] - offset) - e;
+        const double d = (r[x] - offset) - e;
         se += d * d;
         ae += d < 0 ? -d : d;
     }
@@ -3210,6 +3284,41 @@ int n_cus() {
     return n_cu;
 }
 
+// The dispatch layout the XCD masks assume (wave_slot): 8 XCDs, workgroup b on XCD b mod 8.
+// Checked once per device with the XCC_ID register (xcc_selftest_kernel); a launch with an XCD
+// mask is refused where it does not hold (e.g. a partitioned device): its waves would otherwise
+// exit or share user slots, silently training some users twice and others never.
+int xcd_layout_ok()
+{
+    static std::mutex mu;
+    static int state[64] = {};  // per device: 0 unknown, 1 verified, -1 not this layout
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    std::lock_guard<std::mutex> lock(mu);
+    if (state[dev] == 0) {
+        constexpr int kN = 512;
+        int32_t *d = nullptr, h[kN];
+        bool ok = n_cus() % 8 == 0 && hipMalloc((void **)&d, sizeof(h)) == hipSuccess;
+        if (ok) {
+            hipLaunchKernelGGL(xcc_selftest_kernel, dim3(kN), dim3(kWave), 0, (hipStream_t)0, d, kN);
+            ok = hipGetLastError() == hipSuccess &&
+                 hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess;
+            for (int b = 0; ok && b < kN; ++b) ok = h[b] == b % 8;
+            (void)hipFree(d);
+        }
+        state[dev] = ok ? 1 : -1;
+    }
+    return state[dev] > 0;
+}
+
+int check_xmask(int xmask)
+{
+    if ((xmask & 0xFF) && !xcd_layout_ok())
+        return set_err(MF_E_UNSUPPORTED, "XCD masks need 8 XCDs dealt workgroups round-robin "
+                                         "(mf_xcd_layout)");
+    return 0;
+}
+
 // Default grid: enough waves to hold every scheduled user, capped at 16 waves per CU.
 int64_t default_waves(int64_t n_sched) {
     const int64_t cap = (int64_t)n_cus() * 16;
@@ -3261,16 +3370,29 @@ int err_column(int K, int ldq, int dtype)
     return c + 2 <= ldq ? c : 0;
 }
 
+// the kernels' recency inputs (rec NULL: off)
+int make_recency(const mf_recency_t *rec, const mf_hyper_t *hp, Recency &rc)
+{
+    rc = Recency{};
+    if (!rec) return 0;
+    if (!rec->rpos || !rec->totals || !rec->p2stat || !hp)
+        return set_err(MF_E_ARG, "recency weights need rpos, totals, p2stat and hp");
+    rc = Recency{rec->rpos, rec->pos0, rec->totals, rec->p2stat, hp->lr_qi, hp->reg_qi,
+                 hp->lr_bi * (1.0 + hp->reg_bi)};
+    return 0;
+}
+
 template <bool PP>
 int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                  int32_t biased, const mf_hyper_t *hp, int32_t mode, int32_t n_waves, int32_t flags,
-                 int32_t dtype, void *stream, double *psq = nullptr)
+                 int32_t dtype, void *stream, double *psq = nullptr, int32_t *status = nullptr)
 {
     const bool dups = flags & MF_EPOCH_DUP_ITEMS;
     const bool hx = flags & MF_EPOCH_SVDPP_HELPERS;
     const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
     if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, qlog, dtype)) return rc;
+    if (int rc = check_xmask(xmask)) return rc;
     int err_col = 0;
     if (flags & MF_EPOCH_ERR_IN_ROW) {
         if (PP || mode != MF_MODE_LOG || !elog)
@@ -3290,7 +3412,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         constexpr int M = decltype(mode_c)::value;
         return mf_ext::launch_epoch_tm<T, M, PP>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj,
                                                   qlog, elog, K, biased, hp, waves, dups, xmask,
-                                                  hx, psq, err_col, stream);
+                                                  hx, psq, err_col, status, stream);
     };
     auto by_mode = [&](auto tag_t) -> int {
         switch (mode) {
@@ -3417,10 +3539,11 @@ int mf_svd_epoch_sq(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
                    const mf_hyper_t *hp, int32_t mode, void *qlog, void *ycbuf, int32_t n_waves,
-                   int32_t flags, int32_t dtype, void *stream)
+                   int32_t flags, int32_t *status, int32_t dtype, void *stream)
 {
     return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, ycbuf,
-                              n_factors, 1, hp, mode, n_waves, flags, dtype, stream);
+                              n_factors, 1, hp, mode, n_waves, flags, dtype, stream, nullptr,
+                              status);
 }
 
 int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *out, int32_t dtype,
@@ -3474,19 +3597,30 @@ int mf_user_sq_reduce(const double *user_sq, int64_t n_rows, int32_t n_cols, dou
 }
 
 int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *perm,
-                  const int32_t *piece_beg, int64_t n_pieces, void *sums, int32_t dtype,
-                  void *stream)
+                  const int32_t *piece_beg, int64_t n_pieces, void *sums,
+                  const int32_t *piece_item, const mf_hyper_t *hp, const mf_recency_t *rec,
+                  int32_t dtype, void *stream)
 {
-    if (n_pieces < 0 || ld < 1 || n_cols < 0 || n_cols > ld) return set_err(MF_E_ARG, "bad shape");
+    if (n_pieces < 0 || ld < 1 || n_cols < 1 || n_cols > ld) return set_err(MF_E_ARG, "bad shape");
     if (n_pieces == 0) return 0;
     if (!qlog || !perm || !piece_beg || !sums) return set_err(MF_E_ARG, "null argument");
+    Recency rc;
+    if (int e = make_recency(rec, hp, rc)) return e;
+    if (rec && !piece_item) return set_err(MF_E_ARG, "recency weights need piece_item");
     const int g = grid_for_waves(default_waves(n_pieces));
     hipStream_t st = (hipStream_t)stream;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
         return dispatch_g<T>(ld, [&](auto gc) -> int {
-            hipLaunchKernelGGL((log_reduce_kernel<T, decltype(gc)::value>), dim3(g), dim3(kBlock), 0,
-                               st, (const T *)qlog, ld, n_cols, perm, piece_beg, n_pieces, (T *)sums);
+            constexpr int V = decltype(gc)::value;
+            if (rec)
+                hipLaunchKernelGGL((log_reduce_kernel<T, V, true>), dim3(g), dim3(kBlock), 0, st,
+                                   (const T *)qlog, ld, n_cols, perm, piece_beg, n_pieces,
+                                   (T *)sums, (const int32_t *)nullptr, piece_item, rc, n_cols - 1);
+            else
+                hipLaunchKernelGGL((log_reduce_kernel<T, V, false>), dim3(g), dim3(kBlock), 0, st,
+                                   (const T *)qlog, ld, n_cols, perm, piece_beg, n_pieces,
+                                   (T *)sums, (const int32_t *)nullptr, piece_item, rc, n_cols - 1);
             return check_launch("log_reduce_kernel");
         });
     };
@@ -3498,12 +3632,14 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
 int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_factors,
                   const mf_csr_t *csr, const void *qb, const mf_hyper_t *hp, const int32_t *perm,
                   const int32_t *ck_pos, const int32_t *piece_beg, int64_t n_pieces, void *sums,
-                  const int32_t *piece_item, int32_t flags, int32_t dtype, void *stream)
+                  const int32_t *piece_item, const mf_recency_t *rec, int32_t flags,
+                  int32_t dtype, void *stream)
 {
     StopEvent stop(stream);  // (mf_launch_event)
     const mf_ext::JoinArgs join = mf_ext::take_join();  // (mf_launch_join)
     if (n_pieces < 0 || ldq < n_factors + 1 || n_factors < 0) return set_err(MF_E_ARG, "bad shape");
     const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
+    if (int rc = check_xmask(xmask)) return rc;
     if (n_pieces == 0 && !join.words) return 0;  // (a join still launches: its partner waits)
     if (!qlog || !elog || !csr || !qb || !hp || !perm || !ck_pos || !piece_beg || !sums)
         return set_err(MF_E_ARG, "null argument");
@@ -3512,6 +3648,8 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
         return set_err(MF_E_UNSUPPORTED, "MF_EPOCH_ERR_IN_ROW: no spare columns");
     const int64_t rb = (int64_t)ldq * (dtype == MF_F64 ? 8 : 4);
     if (rb > 512 * kLaMaxG) return set_err(MF_E_UNSUPPORTED, "checkpoint log: ldq * size <= 1 KiB only");
+    Recency rc;
+    if (int e = make_recency(rec, hp, rc)) return e;
     const int64_t cap = (int64_t)n_cus() * MF_REPLAY_WPC * (xmask ? __builtin_popcount(xmask) : 8) / 8;
     const int g = grid_for_waves_x(n_pieces < 1 ? 1 : n_pieces < cap ? n_pieces : cap, xmask);
     hipStream_t st = (hipStream_t)stream;
@@ -3522,12 +3660,13 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
             if constexpr (V > kLaMaxG) {
                 return set_err(MF_E_UNSUPPORTED, "checkpoint log: row too long");
             } else {
-                launch_ev(stop.take(), (log_replay_kernel<T, V>), dim3(g), dim3(kBlock), st,
+                auto kern = rec ? log_replay_kernel<T, V, true> : log_replay_kernel<T, V, false>;
+                launch_ev(stop.take(), kern, dim3(g), dim3(kBlock), st,
                                    (const T *)qlog, (const T *)elog, ldq, n_factors, csr->items,
                                    (const T *)qb, csr->n_items, (T)hp->lr_pu,
                                    (T)(1.0 / (1.0 - hp->lr_pu * hp->reg_pu)), perm,
                                    ck_pos, piece_beg, n_pieces, (T *)sums, xmask, err_col,
-                                   piece_item, join.words, join.role, join.epoch);
+                                   piece_item, join.words, join.role, join.epoch, rc);
                 return check_launch("log_replay_kernel");
             }
         });
@@ -3585,8 +3724,10 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
     if (sums2 && !item_piece_ptr2) return set_err(MF_E_ARG, "sums2 needs item_piece_ptr2");
     if (n_items < 0 || ld < 1 || n_factors < 0 || n_factors > ld || bias_col >= ld)
         return set_err(MF_E_ARG, "bad shape");
-    if (rule != MF_MERGE_SUM && rule != MF_MERGE_COUNT) return set_err(MF_E_ARG, "bad merge rule");
-    const int count_rule = rule == MF_MERGE_COUNT;
+    if (rule != MF_MERGE_SUM && rule != MF_MERGE_COUNT && rule != MF_MERGE_RECENCY)
+        return set_err(MF_E_ARG, "bad merge rule");
+    // (0 plain sum, 1 count-aware weight, 2 recency: sums weighted by the replay / reduce)
+    const int count_rule = rule == MF_MERGE_COUNT ? 1 : (rule == MF_MERGE_RECENCY ? 2 : 0);
     if (count_rule && (!totals || !hp || !p2stat))
         return set_err(MF_E_ARG, "count-aware rule needs totals, hp, p2stat");
     if (apply && (!totals || !hp)) return set_err(MF_E_ARG, "apply needs totals and hp");
@@ -3902,8 +4043,8 @@ int mf_rating_errors(int64_t n, const void *est, const int32_t *impossible, cons
     hipStream_t st = (hipStream_t)stream;
     if (dtype == MF_F32)
         hipLaunchKernelGGL(rating_errors_kernel<float>, dim3(g), dim3(kBlock), 0, st, n,
-                           (const float *)est, impossible, (const float *)r, fallback, offset, lo,
-                           hi, out);
+                           (const float *)est, impossible, (const double *)r, fallback, offset,
+                           lo, hi, out);
     else if (dtype == MF_F64)
         hipLaunchKernelGGL(rating_errors_kernel<double>, dim3(g), dim3(kBlock), 0, st, n,
                            (const double *)est, impossible, (const double *)r, fallback, offset,
@@ -3933,6 +4074,13 @@ int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, int32_t ldu, voi
     if (dtype == MF_F32) return run(float{});
     if (dtype == MF_F64) return run(double{});
     return set_err(MF_E_ARG, "bad dtype");
+}
+
+int mf_xcd_layout(int32_t *ok)
+{
+    if (!ok) return set_err(MF_E_ARG, "null argument");
+    *ok = xcd_layout_ok();
+    return 0;
 }
 
 int mf_selftest_xcc(int32_t *out, int32_t n_blocks, void *stream)

@@ -56,28 +56,15 @@ def local_csr(csr, lo: int, hi: int):
     return (row_ptr[lo:hi + 1] - k0, np.asarray(items)[k0:k1], np.asarray(ratings)[k0:k1])
 
 
-def chunk_users(users, row_ptr, n_chunks: int, order: str = "deal"):
+def chunk_users(users, row_ptr, n_chunks: int):
     """Split a rank's users into n_chunks epoch-chunks of ~equal rating count, each sorted
-    heaviest-first (the order the waves take them).
-      "deal": users sorted by degree (descending) are dealt round-robin, so every chunk gets a
-              similar mix of heavy and light users (every chunk's critical path is about the
-              heaviest user's chain);
-      "band": contiguous degree bands -- chunk 0 the heaviest users, the last chunk the
-              lightest; the chunks' critical paths are the bands' heaviest chains, so the
-              epoch's sequential chain grows far less than n_chunks-fold."""
+    heaviest-first (the order the waves take them): users sorted by degree (descending) are
+    dealt round-robin, so every chunk gets a similar mix of heavy and light users (every
+    chunk's critical path is about the heaviest user's chain)."""
     users = np.asarray(users, dtype=np.int64)
     deg = np.diff(np.asarray(row_ptr, dtype=np.int64))[users]
     srt = users[np.argsort(-deg, kind="stable")]
-    if order == "deal":
-        return [srt[c::n_chunks].astype(np.int32) for c in range(n_chunks)]
-    if order != "band":
-        raise ValueError("chunk order must be 'deal' or 'band', got %r" % (order,))
-    cum = np.cumsum(np.sort(deg)[::-1])
-    tot = int(cum[-1]) if len(cum) else 0
-    cuts = np.searchsorted(cum, [tot * c // n_chunks for c in range(1, n_chunks)], side="left")
-    bounds = np.concatenate([[0], np.minimum(cuts + 1, len(srt)), [len(srt)]]).astype(np.int64)
-    bounds = np.maximum.accumulate(bounds)
-    return [srt[bounds[c]:bounds[c + 1]].astype(np.int32) for c in range(n_chunks)]
+    return [srt[c::n_chunks].astype(np.int32) for c in range(n_chunks)]
 
 
 def item_counts(users, row_ptr, items, n_items: int):

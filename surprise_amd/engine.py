@@ -40,7 +40,8 @@ def _free_events(evs):
         lib.mf_event_destroy(ev)
 
 PIECE_ROWS = 64  # log rows summed by one wave of mf_log_reduce
-SVDPP_WAVES_PER_CU = int(os.environ.get("SURPRISE_AMD_SVDPP_WPC", "4"))
+SVDPP_WAVES_PER_CU = 4  # SVD++ without helper waves: users in flight per CU
+HX_CHAINS_PER_CU = 2  # SVD++ helper-wave launch: user chains per CU (1 / 3 / 4 measured slower)
 
 
 def _pad64(n: int, dtype: int) -> int:
@@ -53,7 +54,7 @@ def default_ld(n_factors: int, dtype: int) -> int:
     return _pad64(n_factors, dtype)
 
 
-ITEM_ROW_ALIGN = int(os.environ.get("SURPRISE_AMD_QALIGN", "64"))  # bytes (timing experiments)
+ITEM_ROW_ALIGN = 64  # bytes
 
 
 def default_ldq(n_factors: int, dtype: int) -> int:
@@ -96,6 +97,22 @@ def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS):
     offs = np.concatenate([[0], np.cumsum(counts)])
     item_piece_ptr, piece_beg = piece_bounds(offs, counts, piece_rows)
     return perm, piece_beg.astype(np.int32), item_piece_ptr, counts.astype(np.int32)
+
+
+def item_positions(row_ptr, items, users, n_items):
+    """Position of each rating of `users` among their ratings of the same item, users in order
+    (the order the reference applies them): (ks, pos) with ks the CSR positions, ascending."""
+    row_ptr = np.asarray(row_ptr, np.int64)
+    users = np.sort(np.asarray(users, np.int64))
+    starts, lens = row_ptr[users], row_ptr[users + 1] - row_ptr[users]
+    tot = int(lens.sum())
+    ks = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(tot)
+    it = np.asarray(items)[ks]
+    order = stable_argsort(it)
+    off = np.concatenate([[0], np.cumsum(np.bincount(it, minlength=n_items))])
+    pos = np.empty(tot, np.int32)
+    pos[order] = np.arange(tot) - off[it[order]]
+    return ks, pos
 
 
 def piece_bounds(offs, counts, piece_rows=PIECE_ROWS):
@@ -214,15 +231,17 @@ class Predictor:
         """(rmse, mae, n) of the estimates against r (test() + accuracy.rmse / mae, finished as
         AlgoBase.predict does) -- estimates and errors never leave the device."""
         t = self.torch
+        if len(u) == 0:  # (accuracy.rmse / mae raise on an empty prediction list)
+            raise ValueError("Prediction list is empty.")
         est, bad = self._predict_dev(u, i, global_mean, imp)
-        dr = t.from_numpy(np.ascontiguousarray(r, np.float64)).to(self.dev, self.tdt)
+        dr = t.from_numpy(np.ascontiguousarray(r, np.float64)).to(self.dev)  # (fp64 always)
         out = t.zeros(3, dtype=t.float64, device=self.dev)
         fb = float(global_mean if fallback is None else fallback)
         _lib.call("mf_rating_errors", len(u), self._ptr(est), self._ptr(bad), self._ptr(dr), fb,
                   float(offset), float(rating_scale[0]), float(rating_scale[1]), self._ptr(out),
                   self.dtype, ctypes.c_void_p(self.stream.cuda_stream))
         se, ae, n = out.cpu().tolist()
-        return (se / n) ** .5 if n else float("nan"), ae / n if n else float("nan"), int(n)
+        return (se / n) ** .5, ae / n, int(n)
 
 
 class PredictTables(Predictor):
@@ -266,9 +285,27 @@ class MFEngine(ItemSync, Predictor):
     def __init__(self, csr, n_items, n_factors, *, algo="svd", hyper=None, biased=True,
                  dtype="float32", mode="log", n_chunks=1, deterministic=False,
                  user_order=None, n_waves=0, device=None, ld=None, world=1, merge="count",
-                 ckpt=None, heavy=None, chunk_order=None):
+                 ckpt=True, heavy=None, err_in_row=True, events="native", join="event",
+                 helpers=True, ydefer=True):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
-        trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers."""
+        trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
+
+        Schedule options (the defaults are the measured-best product paths; each alternative
+        is held to the default or to its oracle by a GPU test, DESIGN.md 'Switches'):
+          ckpt        SVD log: the checkpoint form (one user row per pair of ratings, rebuilt by
+                      mf_log_replay) where rows fit 1 KiB; False: the gradient log
+          heavy       split each chunk's heaviest users into their own launch on a second
+                      stream (>= 1: that many users; < 1: those with >= heavy * the top degree;
+                      0: no split; None: 128 on a full MI355X for small epochs)
+          err_in_row  checkpoint log: each pair's errors in its row's padding (else elog)
+          events      "native": the split's fork / join as HIP events bound to the kernels that
+                      complete them (mf_launch_event); "torch": torch.cuda.Event record / wait
+          join        "event": the main stream waits for the side stream's event; "kernel": the
+                      heavy replay's last block waits for the light replay (mf_launch_join)
+          helpers     SVD++ atomic mode: one user chain per workgroup whose q atomics three
+                      helper waves issue (MF_EPOCH_SVDPP_HELPERS)
+          ydefer      SVD++ atomic mode: the users' y updates folded per item after the chunk
+                      (mf_svdpp_y_fold) instead of float atomics at each user's end"""
         torch = _lib.require_gpu()
         self.torch = torch
         self.algo = algo
@@ -292,9 +329,11 @@ class MFEngine(ItemSync, Predictor):
         if self.deterministic:
             mode, n_chunks, n_waves = "plain", 1, 1
         self.mode = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
+        # the log fold's recency weights (MF_MERGE_RECENCY, log mode only)
+        self.recency = merge == "recency" and self.mode == _lib.MF_MODE_LOG
         self.n_chunks = max(1, int(n_chunks))
-        if chunk_order is None:
-            chunk_order = os.environ.get("SURPRISE_AMD_CHUNK_ORDER", "deal")
+        if events not in ("native", "torch") or join not in ("event", "kernel"):
+            raise ValueError("events must be 'native' or 'torch', join 'event' or 'kernel'")
         self.n_waves = int(n_waves)
         if self.n_waves <= 0 and algo == "svdpp" and not self.deterministic:
             # SVD++ with shared item rows: at most SVDPP_WAVES_PER_CU users in flight per CU.
@@ -305,7 +344,10 @@ class MFEngine(ItemSync, Predictor):
             props = torch.cuda.get_device_properties(torch.cuda.current_device())
             self.n_waves = SVDPP_WAVES_PER_CU * props.multi_processor_count
         self.world = int(world)
+        if merge not in ("count", "recency", "sum"):
+            raise ValueError("merge must be 'count', 'recency' or 'sum', got %r" % (merge,))
         self.merge_rule = merge
+        self._ctx = None
         self.stream = torch.cuda.current_stream(self.dev)
         esz = 8 if self.dtype == _lib.MF_F64 else 4
 
@@ -324,15 +366,13 @@ class MFEngine(ItemSync, Predictor):
             order = np.asarray(user_order if user_order is not None else self.users, np.int32)
             chunks = [order]
         else:
-            chunks = chunk_users(self.users, row_ptr, self.n_chunks, chunk_order)
+            chunks = chunk_users(self.users, row_ptr, self.n_chunks)
         to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
         self._row_ptr_h, self._items_h = row_ptr, np.asarray(items, np.int32)
         self._chunk_users = [np.asarray(c, np.int32) for c in chunks]
         esz_q = self.ldq * esz
-        # SVD with one-group rows logs in checkpoint form (a user row every mf_ckpt_interval()
-        # ratings + err per rating; mf_log_replay rebuilds the gradients)
-        if ckpt is None:
-            ckpt = os.environ.get("SURPRISE_AMD_CKPT", "1") != "0"
+        # SVD with rows of <= 1 KiB logs in checkpoint form (a user row per pair of ratings + the
+        # errors; mf_log_replay rebuilds the gradients)
         # (the replay undoes one user step, dividing by ap = 1 - lr_pu reg_pu: kept well away
         # from 0, else the gradient log)
         h = dict(hyper or {})
@@ -343,41 +383,34 @@ class MFEngine(ItemSync, Predictor):
         # users (their sequential chains bound a small epoch) on one XCD beside the rest on the
         # other seven, whose log replay then overlaps the heavy chains
         if heavy is None:
-            env = os.environ.get("SURPRISE_AMD_HEAVY")
-            heavy = float(env) if env is not None else self._auto_heavy(row_ptr)
-        # the heavy launch keeps to the XCDs of this mask and the rest to the others (disjoint
-        # L2s: the rest's log replay then does not evict the heavy chains' item rows)
-        self.heavy_xcd = int(os.environ.get("SURPRISE_AMD_HEAVY_XCD", "1"), 0) & 0xFF
-        self.lpt = int(os.environ.get("SURPRISE_AMD_LPT", str(self.LPT_PER_SIMD)))
-        self.heavy_replay_all = os.environ.get("SURPRISE_AMD_HEAVY_REPLAY_ALL", "1") != "0"
-        # rows per piece of the heavy group's log (its replay runs on the step's longest path)
-        self.heavy_piece = int(os.environ.get("SURPRISE_AMD_HEAVY_PIECE", str(PIECE_ROWS)))
-        if not 1 <= self.heavy_piece <= PIECE_ROWS:
-            raise ValueError("SURPRISE_AMD_HEAVY_PIECE must be in [1, %d]" % PIECE_ROWS)
+            heavy = self._auto_heavy(row_ptr)
+        # the heavy launch keeps to XCD 0 and the rest to the other seven (disjoint L2s: the
+        # rest's log replay then does not evict the heavy chains' item rows) -- where the device
+        # deals workgroups round-robin over 8 XCDs (mf_xcd_layout), else no XCD masks
+        self.heavy_xcd = 1 if heavy > 0 and _lib.xcd_layout_ok() else 0
         # checkpoint log with MF_EPOCH_ERR_IN_ROW where the row has room: each pair's two errors
         # ride in its checkpoint row's padding (the replay gathers no elog entries)
         e0 = ((self.K + 2) & ~1) if self.dtype == _lib.MF_F32 else self.K + 1
         # (read-only after construction: elog is sized for it)
-        self._err_in_row = (self.ckpt and e0 + 2 <= self.ldq
-                            and os.environ.get("SURPRISE_AMD_ERR_IN_ROW", "1") != "0")
+        self._err_in_row = self.ckpt and e0 + 2 <= self.ldq and bool(err_in_row)
         C = _lib.load().mf_ckpt_interval() if self.ckpt else 0
         _pu = []
         pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
         self.side = torch.cuda.Stream(device=dev) if self.ckpt and heavy > 0 else None
         # the fork / join between the two streams as native events bound to the kernels that
         # complete them (mf_launch_event: no marker packet in the main stream's queue);
-        # SURPRISE_AMD_NATIVE_EVENTS=0: torch.cuda.Event record / wait_event
+        # events="torch": torch.cuda.Event record / wait_event
         self._nev = None
-        if self.side is not None and os.environ.get("SURPRISE_AMD_NATIVE_EVENTS", "1") != "0":
+        if self.side is not None and events == "native":
             self._nev = {k: _new_event() for k in ("fork", "join")}
             weakref.finalize(self, _free_events, list(self._nev.values()))
         self._fork_bound = False  # the last mf_log_apply on the main stream completes "fork"
-        # the join as an event the main stream waits for; SURPRISE_AMD_JOIN_FLAG=1: inside the two
-        # replays instead (mf_launch_join: the heavy replay's last block waits for the light
-        # replay's; no barrier packet before the fold) -- measured equal (the write-through
-        # stores of the light replay cost what the barrier packet did), so off by default
+        # the join as an event the main stream waits for; join="kernel": inside the two replays
+        # instead (mf_launch_join: the heavy replay's last block waits for the light replay's;
+        # no barrier packet before the fold) -- measured equal (the write-through stores of the
+        # light replay cost what the barrier packet did), so off by default
         self._join_words = None
-        if self.side is not None and os.environ.get("SURPRISE_AMD_JOIN_FLAG", "0") != "0":
+        if self.side is not None and join == "kernel":
             self._join_words = torch.zeros(1024, dtype=torch.int32, device=dev)
             self._join_epoch = 0
         self.sched = []
@@ -391,27 +424,28 @@ class MFEngine(ItemSync, Predictor):
                     item_counts(c, row_ptr, items, self.n_items).astype(np.int32))
                 continue
             parts = split_heavy(c, row_ptr, heavy) if self.side is not None else [c]
+            # (recency, a split chunk: each rating's position among the chunk's ratings of its
+            # item, indexed by CSR position; one group: its perm is already in that order)
+            kpos = None
+            if self.recency and len(parts) > 1:
+                ks, pos = item_positions(row_ptr, items, c, self.n_items)
+                kpos = np.zeros(int(row_ptr[-1]), np.int32)
+                kpos[ks] = pos
             lgs = []
-            for gi, us in enumerate(parts):
-                perm, pb, ipp, cnt = log_layout(row_ptr, items, us, self.n_items,
-                                                self.heavy_piece if gi else PIECE_ROWS)
+            for us in parts:
+                perm, pb, ipp, cnt = log_layout(row_ptr, items, us, self.n_items)
                 lg = dict(sched=to_dev(us), perm=to_dev(perm), pb=to_dev(pb), ipp=to_dev(ipp),
                           n_pieces=len(pb) - 1, cnt=cnt)
                 if self.ckpt:
                     lg["ck"] = to_dev(ckpt_positions(row_ptr, perm, C, pos_user()))
-                    # the item of every piece (mf_log_replay's piece_item)
-                    lg["pitem"] = to_dev(np.repeat(np.arange(self.n_items, dtype=np.int32),
-                                                   np.diff(ipp)))
+                # the item of every piece (mf_log_replay's / mf_log_reduce's piece_item)
+                lg["pitem"] = to_dev(np.repeat(np.arange(self.n_items, dtype=np.int32),
+                                               np.diff(ipp)))
+                if self.recency:
+                    lg["rpos"] = to_dev(kpos[perm] if kpos is not None else
+                                        np.arange(len(perm), dtype=np.int64) -
+                                        np.repeat(pb[ipp[:-1]], cnt)).astype(np.int32)
                 lgs.append(lg)
-            if self.ckpt and self.lpt > 0 and len(parts[0]) <= self.LPT_MAX_USERS:
-                # the (light) group's epoch as LPT chains: lpt waves per SIMD of its XCDs, each
-                # taking a balanced list of users heaviest-first (the heavy group: one wave each)
-                props = torch.cuda.get_device_properties(self.dev)
-                n_x = 8 - bin(self.heavy_xcd).count("1") if len(lgs) > 1 and self.heavy_xcd else 8
-                chains = max(1, self.lpt * 4 * props.multi_processor_count * n_x // 8)
-                lgs[0]["chain"] = to_dev(chain_schedule(parts[0], row_ptr, chains,
-                                                        self.LPT_USER_COST))
-                lgs[0]["n_chains"] = chains
             main = lgs[0]
             main["heavy"] = lgs[1] if len(lgs) > 1 else None
             self.sched.append(main["sched"])
@@ -419,21 +453,20 @@ class MFEngine(ItemSync, Predictor):
             self._totals_local.append(sum(lg.pop("cnt") for lg in lgs).astype(np.int32))
         self.counts = [to_dev(t) for t in self._totals_local]  # this rank's n_r per chunk
         # SVD++ in atomic mode: the end-of-user y update deferred to a per-item fold after each
-        # chunk (mf_svdpp_y_fold; SURPRISE_AMD_YDEFER=0: float atomics at each user's end)
+        # chunk (mf_svdpp_y_fold; ydefer=False: float atomics at each user's end)
         self.ydefer = (algo == "svdpp" and self.mode == _lib.MF_MODE_ATOMIC
-                       and not self.deterministic
-                       and os.environ.get("SURPRISE_AMD_YDEFER", "1") != "0")
+                       and not self.deterministic and bool(ydefer))
         # ... with helper waves (rows <= 1 KiB, no repeated items): one user chain per CU whose
         # q atomics the workgroup's other three waves issue (mf_svdpp_epoch flag
         # MF_EPOCH_SVDPP_HELPERS); the chains take users in a longest-first balanced layout
         self.dup_items = int(_has_duplicate_items(row_ptr, items))
-        self.hx = (self.ydefer and self.ldq * esz <= 1024 and not self.dup_items
-                   and os.environ.get("SURPRISE_AMD_SVDPP_HX", "1") != "0")
+        self.hx = self.ydefer and self.ldq * esz <= 1024 and not self.dup_items and bool(helpers)
         self.hx_sched = []
+        # the helper-wave launch's status word (mf_svdpp_epoch): checked in get_factors
+        self._hx_status = torch.zeros(1, dtype=torch.int32, device=dev) if self.hx else None
         if self.hx:
             props = torch.cuda.get_device_properties(self.dev)
-            self.hx_chains = int(os.environ.get("SURPRISE_AMD_HX_PER_CU", "2")) * \
-                props.multi_processor_count
+            self.hx_chains = HX_CHAINS_PER_CU * props.multi_processor_count
             for us in self.sched:
                 self.hx_sched.append(to_dev(chain_schedule(us.cpu().numpy(), row_ptr,
                                                            self.hx_chains)))
@@ -509,10 +542,6 @@ class MFEngine(ItemSync, Predictor):
         """Checkpoint log with each pair's errors in its row's padding (MF_EPOCH_ERR_IN_ROW)."""
         return self._err_in_row
 
-    LPT_PER_SIMD = 0      # checkpoint-log epoch: LPT user chains per SIMD (0: one wave per user;
-                          # measured at ML-1M: 1 / 2 / 4 chains per SIMD no faster than 0)
-    LPT_USER_COST = int(os.environ.get("SURPRISE_AMD_LPT_COST", "16"))  # per-user cost, ratings
-    LPT_MAX_USERS = 200_000  # (a host-side heap pass; larger epochs are bandwidth-bound anyway)
     HEAVY_USERS = 128     # users in the heavy launch (measured: 64 0.231, 128 0.224, 256 0.232 ms)
     HEAVY_MAX_NNZ = 8_000_000
 
@@ -563,6 +592,9 @@ class MFEngine(ItemSync, Predictor):
         if getattr(self, "_join_words", None) is not None and int(self._join_words[608]) != 0:
             raise _lib.SurpriseAMDError("the in-kernel join of the two replays timed out: the "
                                         "item folds since are invalid")
+        if getattr(self, "_hx_status", None) is not None and int(self._hx_status[0]) & 1:
+            raise _lib.SurpriseAMDError("an SVD++ helper wave timed out waiting for q deltas and "
+                                        "stopped: item updates were lost (mf_svdpp_epoch status)")
         K = self.K
         h = lambda x: x.to(self.torch.float64).cpu().numpy()
         pu, bu = self.pu[:, :K], self.bu
@@ -601,7 +633,8 @@ class MFEngine(ItemSync, Predictor):
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
                       self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper),
                       self.mode, qlog, self._ptr(self.ycbuf) if self.ydefer else None,
-                      n_waves, flags, self.dtype, st)
+                      n_waves, flags, self._ptr(self._hx_status) if self.hx else None,
+                      self.dtype, st)
 
     def run_chunk(self, c: int, events=None):
         """Run chunk c: the epoch kernel, preceded in "log" mode by the <pu^2> reduction of the
@@ -630,6 +663,7 @@ class MFEngine(ItemSync, Predictor):
                                                   self.u_lo * self.ld * self.pu.element_size()),
                       self.u_hi - self.u_lo, self.K, self.ld, self._ptr(self.work), self.dtype,
                       st)
+            self._global_stat()  # (several ranks: every rank's <p^2>)
         if "start" in ev:
             ev["start"].record(self.stream)
         lg = self.logs[c] if self.is_log else None
@@ -707,6 +741,7 @@ class MFEngine(ItemSync, Predictor):
             self._sq_reduce(cur, st)
         else:
             launched = False
+        launched = self._global_stat() or launched  # (several ranks: every rank's <p^2>)
         fork_bound, self._fork_bound = self._fork_bound and not launched, False
         self._sq_pending = True
         if "start" in ev:
@@ -715,8 +750,6 @@ class MFEngine(ItemSync, Predictor):
         hv = lg["heavy"]
         sums_h = self.sums.data_ptr() + lg["n_pieces"] * self.ldq * self.sums.element_size()
         ls, ln, lw = lg["sched"], lg["sched"].numel(), self.n_waves
-        if "chain" in lg:
-            ls, ln, lw = lg["chain"], lg["chain"].numel(), lg["n_chains"]
         if hv is None:
             self._epoch_sq(ls, ln, lw, st)
             if "end" in ev:
@@ -751,7 +784,7 @@ class MFEngine(ItemSync, Predictor):
             # work is (nearly) done, so it may spread over every XCD)
             if jw is not None:  # (it ends once the light replay of this chunk has published)
                 _lib.call("mf_launch_join", self._ptr(jw), 2, self._join_epoch)
-            self._reduce_log(hv, sums_h, st, 0 if self.heavy_replay_all else self.heavy_xcd)
+            self._reduce_log(hv, sums_h, st)
             if jw is None and self._nev is None:
                 self._ev_wait(self.stream, "join")
             elif jw is None:
@@ -771,26 +804,54 @@ class MFEngine(ItemSync, Predictor):
     def _reduce_log(self, lg, sums_ptr, st, xmask=0):
         """Piece sums of one user group's log: mf_log_replay (checkpoint form) or mf_log_reduce.
         xmask: run on those XCDs only (bit x: XCD x; 0: all)."""
+        rec = self._recency_args(lg)
         if self.ckpt:
             _lib.call("mf_log_replay", ctypes.c_void_p(self._qlog_base),
                       ctypes.c_void_p(self._elog_base), self.ldq, self.K, ctypes.byref(self._csr),
                       self._ptr(self.qb), ctypes.byref(self._hyper), self._ptr(lg["perm"]),
                       self._ptr(lg["ck"]), self._ptr(lg["pb"]), lg["n_pieces"],
-                      ctypes.c_void_p(sums_ptr), self._ptr(lg["pitem"]),
+                      ctypes.c_void_p(sums_ptr), self._ptr(lg["pitem"]), rec,
                       (xmask << _lib.MF_EPOCH_XCD_SHIFT) |
                       (_lib.MF_EPOCH_ERR_IN_ROW if self.err_in_row else 0), self.dtype, st)
         else:
             _lib.call("mf_log_reduce", ctypes.c_void_p(self._qlog_base), self.ldq, self.K + 1,
                       self._ptr(lg["perm"]), self._ptr(lg["pb"]), lg["n_pieces"],
-                      ctypes.c_void_p(sums_ptr), self.dtype, st)
+                      ctypes.c_void_p(sums_ptr), self._ptr(lg["pitem"]),
+                      ctypes.byref(self._hyper), rec, self.dtype, st)
+
+    def _recency_args(self, lg):
+        """mf_recency_t of one user group's log in the current chunk (None: no recency)."""
+        if not self.recency:
+            return None
+        c = getattr(self, "_chunk", 0)
+        pos0 = self._pos0[c] if self._pos0 else None
+        rec = _lib.MfRecency(lg["rpos"].data_ptr(), pos0.data_ptr() if pos0 is not None else None,
+                             self._totals()[c].data_ptr(), self.work.data_ptr())
+        return ctypes.byref(rec)
+
+    def _global_stat(self):
+        """Several ranks: the chunk-start <p^2> partial in self.work summed over every rank before
+        the chunk's replay / reduce reads it (the recency weights) -- one 2-double all-reduce on
+        the main stream; True if it launched one."""
+        ctx = self._ctx
+        if ctx is None or ctx.world == 1 or not self.is_log:
+            return False
+        ctx.all_reduce_sum(self.work)
+        return True
 
     def _prepare(self, ctx):
         """Global per-item rating counts of every chunk (all ranks) for the count-aware rules;
         with SVD++ on several ranks, the per-item factors of the y_j affine merge (dist.py)."""
+        self._ctx = ctx
         self.totals = []
+        self._pos0 = []
         for t in self._totals_local:
             tt = self.torch.from_numpy(t).to(self.dev)
             if ctx is not None and ctx.world > 1:
+                if self.recency:  # this rank's ratings of an item follow the earlier ranks'
+                    every = ctx.all_gather_rows(tt[None].to(self.torch.int64),
+                                                [1] * ctx.world).cpu()
+                    self._pos0.append(every[:ctx.rank].sum(0).to(self.torch.int32).to(self.dev))
                 ctx.all_reduce_sum(tt)
             self.totals.append(tt)
         self._yaff = []
@@ -824,12 +885,18 @@ class MFEngine(ItemSync, Predictor):
             self._prepare(None)
         return self.merge_rule == "count"
 
+    def _log_rule(self):
+        """mf_log_apply's merge rule."""
+        if self.merge_rule != "sum" and self.totals is None:
+            self._prepare(None)
+        return {"count": _lib.MF_MERGE_COUNT, "recency": _lib.MF_MERGE_RECENCY,
+                "sum": _lib.MF_MERGE_SUM}[self.merge_rule]
+
     def _log_fold(self, delta_out, apply):
         """mf_log_apply of the current chunk (its pieces were reduced in run_chunk)."""
         c = getattr(self, "_chunk", 0)
         lg = self.logs[c]
         hv = lg["heavy"]
-        count = self._count_rule()
         sums2 = (ctypes.c_void_p(self.sums.data_ptr() + lg["n_pieces"] * self.ldq *
                                  self.sums.element_size()) if hv is not None else None)
         if apply:
@@ -838,7 +905,7 @@ class MFEngine(ItemSync, Predictor):
                   self._bias_col, self._ptr(self.sums), self._ptr(lg["ipp"]), sums2,
                   self._ptr(hv["ipp"]) if hv is not None else None,
                   self._ptr(self._totals()[c]), ctypes.byref(self._hyper),
-                  self._ptr(self.work), _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM,
+                  self._ptr(self.work), self._log_rule(),
                   None if delta_out is None else self._ptr(delta_out), int(apply),
                   *self._stat_args(apply), self.dtype, self._st())
 
@@ -882,35 +949,44 @@ class MFEngine(ItemSync, Predictor):
             self._log_fold(None, True)
 
     def sync_items(self, ctx):
+        """The chunk's item-side exchange: one rank folds locally; several ranks fill ONE packed
+        buffer (the log sums, or q's and y's snapshot deltas side by side), SUM-all-reduce it
+        once (one RCCL collective per chunk, nothing serialised behind another) and apply it.
+        self._sync_events (dict of "ar_begin" / "ar_end" torch events, set by bench.py's
+        instrumented epochs) brackets the collective on the engine's stream."""
         if ctx is None or ctx.world == 1:
             self._merge_local()
             return
-        bufs = self._delta_buffer()
+        flat, bufs = self._delta_buffer()
         self._delta_into(bufs)
-        for b in bufs:
-            ctx.all_reduce_sum(b)
+        ev = getattr(self, "_sync_events", None)
+        if ev:
+            ev["ar_begin"].record(self.stream)
+        ctx.all_reduce_sum(flat)
+        if ev:
+            ev["ar_end"].record(self.stream)
         self._apply(bufs)
 
     def _delta_buffer(self):
-        """[log sums + the <pu^2> partial {sum, count} in its last two elements (log mode)] +
-        [one delta per snapshot table]: log mode all-reduces ONE buffer per chunk."""
+        """(flat, views): one device buffer holding [log sums (log mode)] + [one delta per
+        snapshot table] -- the chunk's whole exchange is one all-reduce."""
         if self._delta is None:
-            z = lambda n: self.torch.zeros(n, dtype=self.tdt, device=self.dev)
-            bufs = []
-            if self.is_log:
-                bufs.append(z(self.n_items * self.ldq + 2))
-            for tab, snap, ld, _, _ in self._snap_tables():
-                bufs.append(z(self.n_items * ld))
-            self._delta = bufs
+            sizes = ([self.n_items * self.ldq] if self.is_log else []) + \
+                [self.n_items * ld for _, _, ld, _, _ in self._snap_tables()]
+            flat = self.torch.zeros(sum(sizes), dtype=self.tdt, device=self.dev)
+            views, o = [], 0
+            for n in sizes:
+                views.append(flat[o:o + n])
+                o += n
+            self._delta = (flat, views)
         return self._delta
 
     def _delta_into(self, bufs):
         c = getattr(self, "_chunk", 0)
         st = self._st()
         x = 0
-        if self.is_log:
+        if self.is_log:  # (self.work already holds every rank's <p^2>: _global_stat)
             self._log_fold(bufs[0], False)
-            bufs[0][-2:].copy_(self.work)  # (the statistic rides in the same all-reduce)
             x = 1
         for tab, snap, ld, bias_col, rule in self._snap_tables():
             if rule == "affine":
@@ -935,17 +1011,14 @@ class MFEngine(ItemSync, Predictor):
         c = getattr(self, "_chunk", 0)
         st = self._st()
         x = 0
-        if self.is_log:  # bufs[0]: the all-reduced sums, then the sum of squares of pu
-            count = self._count_rule()
-            self.work.copy_(bufs[0][-2:])
+        if self.is_log:  # bufs[0]: the all-reduced sums
             if not self._snap_tables():
                 self._bind_fork()
             _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K,
                       self._bias_col, self._ptr(bufs[0]), None, None, None,
                       self._ptr(self._totals()[c]),
-                      ctypes.byref(self._hyper), self._ptr(self.work),
-                      _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM, None, 1,
-                      *self._stat_args(True), self.dtype, st)
+                      ctypes.byref(self._hyper), self._ptr(self.work), self._log_rule(), None,
+                      1, *self._stat_args(True), self.dtype, st)
             x = 1
         for tab, snap, ld, _, rule in self._snap_tables():
             if rule == "affine":

@@ -144,7 +144,8 @@ class _MFBase(AlgoBase):
                        hyper=self._hyper(global_mean), biased=getattr(self, "biased", True),
                        dtype=self.dtype, mode=self._resolve_mode(),
                        n_chunks=self.chunks_per_epoch, deterministic=self.deterministic,
-                       user_order=user_order, n_waves=self.n_waves, world=world)
+                       user_order=user_order, n_waves=self.n_waves, world=world,
+                       **getattr(self, "_engine_options", {}))
         eng.set_factors(pu[lo:hi], qi, yj=yj)
         del pu
         verbose = self.verbose

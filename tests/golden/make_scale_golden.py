@@ -16,7 +16,6 @@ usage: python tests/golden/make_scale_golden.py {c4|c5shard} [--epochs 20]
 (each case merges its entry into scale_golden.json; c4 ~25 min, c5shard ~1 h on one core)
 """
 import argparse
-import hashlib
 import json
 import os
 import sys
@@ -36,13 +35,6 @@ import oracle as orc  # noqa: E402
 OUT = os.path.join(HERE, "scale_golden.json")
 CASES = {"c4": dict(shape="c4", users=0, algo="svd", K=128),
          "c5shard": dict(shape="c5", users=1_250_000, algo="svdpp", K=128)}
-
-
-def fingerprint(csr, test):
-    h = hashlib.sha256()
-    for a in (*csr, *test):
-        h.update(np.ascontiguousarray(a).tobytes())
-    return h.hexdigest()[:16]
 
 
 def main():
@@ -83,7 +75,7 @@ def main():
         "workload": desc, "algo": c["algo"], "n_factors": K, "shape": c["shape"],
         "users": c["users"] or None, "train_ratings": int(len(ratings)),
         "held_out": int(len(tr)), "n_items": int(n_items), "global_mean": gm,
-        "data_fingerprint": fingerprint(csr, (tu, ti, tr)),
+        "data_fingerprint": bench.data_fingerprint(csr, (tu, ti, tr)),
         "rmse_by_epoch": curve,
         "global_mean_rmse": orc.rmse(tr, np.full(len(tr), gm)),
         "oracle": ("oracle_svdpp_sgd_affine (mf.pyx:463-498)" if svdpp

@@ -40,14 +40,20 @@ def test_version_and_error_without_device(lib):
                           0, None, None, 0, 0, 0, None)
     assert rc == 1001 and b"null csr" in lib.mf_last_error()
     rc = lib.mf_log_replay(None, None, 16, 10, None, None, None, None, None, None, 3, None, None,
-                           0, 0, None)
+                           None, 0, 0, None)
     assert rc == 1001 and b"null argument" in lib.mf_last_error()
     assert lib.mf_ckpt_interval() in (2, 4, 8, 16)
     rc = lib.mf_log_apply(None, 10, 16, 10, 10, None, None, None, None, None, None, None, 1, None,
                           1, None, None, 0, 0, None)
     assert rc == 1001 and b"count-aware rule needs" in lib.mf_last_error()
-    rc = lib.mf_log_reduce(None, 16, 11, None, None, 5, None, 0, None)
+    rc = lib.mf_log_reduce(None, 16, 11, None, None, 5, None, None, None, None, 0, None)
     assert rc == 1001 and b"null argument" in lib.mf_last_error()
+    rec = _lib.MfRecency(0, 0, 0, 0)
+    rc = lib.mf_log_reduce(1, 16, 11, 1, 1, 5, 1, None, None, ctypes.byref(rec), 0, None)
+    assert rc == 1001 and b"recency weights need" in lib.mf_last_error()
+    rc = lib.mf_svdpp_epoch(ctypes.byref(csr), None, 1, None, None, 16, None, 16, None, 10, None,
+                            1, None, None, 0, 0, None, 0, None)
+    assert rc == 1001 and b"null csr" in lib.mf_last_error()
     rc = lib.mf_sumsq(None, 4, 8, 4, None, 0, None)
     assert rc == 1001
     rc = lib.mf_svd_epoch_sq(ctypes.byref(csr), None, 1, None, None, 16, None, 16, 10, 1, None,
@@ -60,7 +66,9 @@ def test_version_and_error_without_device(lib):
 def test_header_constants_match_python():
     text = open(_lib.HEADER_PATH).read()
     for name, val in (("MF_F32", 0), ("MF_F64", 1), ("MF_MODE_PLAIN", 0), ("MF_MODE_ATOMIC", 1),
-                      ("MF_MODE_LOG", 2), ("MF_MERGE_SUM", 0), ("MF_MERGE_COUNT", 1), ("MF_MERGE_MEAN", 2), ("MF_EPOCH_DUP_ITEMS", 1),
+                      ("MF_MODE_LOG", 2), ("MF_MERGE_SUM", 0), ("MF_MERGE_COUNT", 1), ("MF_MERGE_MEAN", 2),
+                      ("MF_MERGE_RECENCY", 3), ("MF_EPOCH_DUP_ITEMS", 1), ("MF_HX_HELPER_TIMEOUT", 1),
+                      ("MF_HX_CHAIN_FALLBACK", 2),
                       ("MF_MAX_FACTORS_F32", 512),
                       ("MF_MAX_FACTORS_F64", 256)):
         assert "#define %s" % name in text and str(val) in text.split("#define %s" % name)[1].split("\n")[0]

@@ -93,7 +93,10 @@ def test_svd_deterministic_fp32_matches_reference(torch, golden, u1):
 
 @pytest.mark.parametrize("name", ["svd_k20_e5", "svd_k5_e2_unbiased", "svd_k10_e3_hyper"])
 @pytest.mark.parametrize("chunks", [1, 3])
-def test_log_mode_fp64_matches_deltalog_oracle(torch, golden, u1, name, chunks):
+@pytest.mark.parametrize("merge", ["count", "recency"])
+def test_log_mode_fp64_matches_deltalog_oracle(torch, golden, u1, name, chunks, merge):
+    """The log schedule's fold -- count-aware weight or recency weights (replay-side) -- in fp64
+    against oracle_svd_sgd_deltalog (merge 2 / 3) on the same chunking, to 1e-9."""
     from surprise_amd import SVD
     from surprise_amd.dist import chunk_users
     meta, _ = golden
@@ -104,8 +107,10 @@ def test_log_mode_fp64_matches_deltalog_oracle(torch, golden, u1, name, chunks):
     for c, us in enumerate(chunk_users(np.arange(ts.n_users), row_ptr, chunks)):
         cou[us] = c
     P, f = run_oracle_log("SVD", case["params"], row_ptr, items, ratings, ts.n_items,
-                          ts.global_mean, cou, chunks)
-    algo = SVD(**case["params"], dtype="float64", chunks_per_epoch=chunks).fit(ts)
+                          ts.global_mean, cou, chunks, merge=2 if merge == "count" else 3)
+    algo = SVD(**case["params"], dtype="float64", chunks_per_epoch=chunks)
+    algo._engine_options = {"merge": merge}
+    algo.fit(ts)
     for k in ("pu", "qi", "bu", "bi"):
         np.testing.assert_allclose(getattr(algo, k), f[k], rtol=0, atol=1e-9, err_msg=k)
     ref = _oracle_test_rmse(P, f, "SVD", ts, list(test))[1]
@@ -172,6 +177,23 @@ def test_svdpp_parallel_rmse_within_1e3(torch, golden, u1, name, mode):
     case = meta["cases"][name]
     ts, test = u1
     algo = SVDpp(**case["params"], mode=mode).fit(ts)
+    assert abs(_rmse(algo.test(test)) - case["rmse"]) < RMSE_TOL
+
+
+@pytest.mark.parametrize("opt", [{"helpers": False}, {"ydefer": False}])
+def test_svdpp_atomic_alternatives_rmse_within_1e3(torch, golden, u1, opt):
+    """SVD++'s non-default atomic-mode paths (MFEngine helpers=False: the chain wave issues its
+    own q atomics; ydefer=False: y_j updated by float atomics at each user's end) within 1e-3
+    of the reference's held-out RMSE, like the default."""
+    from surprise_amd import SVDpp
+    meta, _ = golden
+    case = meta["cases"]["svdpp_k20_e20"]
+    ts, test = u1
+    algo = SVDpp(**case["params"], mode="atomic")
+    algo._engine_options = opt
+    algo.fit(ts)
+    eng = algo._engine
+    assert (eng.hx, eng.ydefer) == ((False, True) if "helpers" in opt else (False, False))
     assert abs(_rmse(algo.test(test)) - case["rmse"]) < RMSE_TOL
 
 
@@ -380,9 +402,10 @@ def test_checkpoint_log_matches_gradient_log(torch, u1, K, dtype, chunks):
 
 
 def test_heavy_user_split_matches_single_launch(torch, u1):
-    """The two-stream split (the heaviest users' epoch kernel + replay on a side stream,
-    SURPRISE_AMD_HEAVY; measured slower, off by default) computes the same schedule: per item
-    the two groups' piece sums are added in a fixed order (mf_log_apply's sums2)."""
+    """The two-stream split (the heaviest users' epoch kernel + replay on their own stream, the
+    default for small epochs on a full MI355X; here forced with heavy=0.25) computes the same
+    schedule as one launch: per item the two groups' piece sums are added in a fixed order
+    (mf_log_apply's sums2)."""
     from surprise_amd.engine import MFEngine
     ts, _ = u1
     row_ptr, items, ratings = ts.csr()
@@ -424,10 +447,10 @@ def test_native_fork_and_kernel_join_equal_torch_events(torch, request, monkeypa
     ii = np.arange(ts.n_users, dtype=np.int32) % ts.n_items
     out = []
     for native in ("1", "0"):
-        monkeypatch.setenv("SURPRISE_AMD_NATIVE_EVENTS", native)
-        monkeypatch.setenv("SURPRISE_AMD_JOIN_FLAG", native)
         eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype="float32",
-                       mode="log", n_chunks=chunks, heavy=heavy)
+                       mode="log", n_chunks=chunks, heavy=heavy,
+                       events="native" if native == "1" else "torch",
+                       join="kernel" if native == "1" else "event")
         assert eng.logs[0]["heavy"] is not None and (eng._nev is not None) == (native == "1")
         assert (eng._join_words is not None) == (native == "1")
         eng.set_factors(pu0, qi0)
@@ -446,7 +469,7 @@ def test_native_fork_and_kernel_join_equal_torch_events(torch, request, monkeypa
                                             (61, "float64", 0.25)])
 def test_errors_in_checkpoint_rows_equal_elog(torch, u1, monkeypatch, K, dtype, heavy):
     """MF_EPOCH_ERR_IN_ROW (each pair's errors stored in its checkpoint row's padding, read back
-    by the replay from the loaded row) against the errors in elog (SURPRISE_AMD_ERR_IN_ROW=0):
+    by the replay from the loaded row) against the errors in elog (err_in_row=False):
     the same values reach the same operations, so the fits are bit-identical (split and unsplit
     chunks)."""
     from surprise_amd.engine import MFEngine
@@ -458,9 +481,8 @@ def test_errors_in_checkpoint_rows_equal_elog(torch, u1, monkeypatch, K, dtype, 
     pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
     out = []
     for in_row in (True, False):
-        monkeypatch.setenv("SURPRISE_AMD_ERR_IN_ROW", "1" if in_row else "0")
         eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype=dtype,
-                       mode="log", heavy=heavy)
+                       mode="log", heavy=heavy, err_in_row=in_row)
         assert eng.ckpt and eng.err_in_row == in_row
         eng.set_factors(pu0, qi0)
         eng.run_epochs(3)

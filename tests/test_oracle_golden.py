@@ -253,14 +253,16 @@ def run_oracle_log(algo, params, row_ptr, items, ratings, n_items, global_mean, 
 
 
 @pytest.mark.parametrize("name", ["svd_k20_e5", "svd_k5_e2_unbiased", "svd_k10_e3_hyper"])
-def test_deltalog_one_user_per_chunk_is_the_reference(golden, u1, name):
-    """Pins the delta-log oracle to the reference: one user per chunk = SVD.sgd bit-for-bit."""
+@pytest.mark.parametrize("merge", [2, 3])
+def test_deltalog_one_user_per_chunk_is_the_reference(golden, u1, name, merge):
+    """Pins the delta-log oracle to the reference: one user per chunk = SVD.sgd bit-for-bit,
+    with the count-aware (2) and the recency-weighted (3) fold alike."""
     meta, _ = golden
     case = meta["cases"][name]
     ts, _ = u1
     row_ptr, items, ratings = ts.csr()
     P, f = run_oracle_log("SVD", case["params"], row_ptr, items, ratings, ts.n_items,
-                          ts.global_mean, np.arange(ts.n_users), ts.n_users)
+                          ts.global_mean, np.arange(ts.n_users), ts.n_users, merge=merge)
     assert _sha(f["pu"], f["qi"]) == case["sha_pu_qi"]
     assert _sha(f["bu"], f["bi"]) == case["sha_bu_bi"]
 
@@ -278,15 +280,16 @@ def test_deltalog_svdpp_one_user_per_chunk_is_the_affine_form(u1):
 
 
 @pytest.mark.parametrize("name", ["svd_k20_e5", "svd_k100_e20", "svd_k10_e3_hyper"])
-def test_deltalog_one_chunk_within_1e3_of_reference(golden, u1, name):
-    """The schedule itself (all users of the epoch against one snapshot, count-aware merge)
-    stays within the north-star tolerance of the sequential reference on u1."""
+@pytest.mark.parametrize("merge", [2, 3])
+def test_deltalog_one_chunk_within_1e3_of_reference(golden, u1, name, merge):
+    """The schedule itself (all users of the epoch against one snapshot, count-aware or
+    recency-weighted fold) stays within the north-star tolerance of the sequential reference."""
     meta, _ = golden
     case = meta["cases"][name]
     ts, test = u1
     row_ptr, items, ratings = ts.csr()
     P, f = run_oracle_log("SVD", case["params"], row_ptr, items, ratings, ts.n_items,
-                          ts.global_mean)
+                          ts.global_mean, merge=merge)
     assert abs(_oracle_test_rmse(P, f, "SVD", ts, list(test))[1] - case["rmse"]) < 1e-3
 
 
