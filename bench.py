@@ -224,13 +224,18 @@ def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
     if ctx is not None:
         ctx.barrier()
     elapsed = time.perf_counter() - t0
+    multi = ctx is not None and ctx.world > 1
     for step in range(PHASE_STEPS if instrument else 0):
         for c in range(eng.n_chunks):
             ev = {k: torch.cuda.Event(enable_timing=True)
-                  for k in ("begin", "start", "end", "end_h", "end_r", "done")}
+                  for k in ("begin", "start", "end", "end_h", "end_r", "done", "ar_begin",
+                            "ar_end")}
             ev["begin"].record(eng.stream)
             eng.run_chunk(c, events=ev)
+            if multi:  # (the collective of the chunk's exchange, bracketed on the stream)
+                eng._sync_events = ev
             eng.sync_items(ctx)
+            eng._sync_events = None
             ev["done"].record(eng.stream)
             recs.append(ev)
     torch.cuda.synchronize()
@@ -241,6 +246,11 @@ def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
         phases.update({"pre_ms": span("begin", "start") * n, "epoch_kernel_ms": span("start", "end") * n,
                   "replay_ms": span("end", "end_r") * n, "fold_sync_ms": span("end_r", "done") * n,
                   "step_gpu_ms": span("begin", "done") * n, "instrumented_steps": len(recs) // n})
+        if multi:  # the exchange: one SUM all-reduce per chunk (ms per chunk and per step)
+            ar = span("ar_begin", "ar_end")
+            phases.update({"allreduce_ms_per_chunk": ar, "allreduce_ms": ar * n,
+                           "allreduce_bytes_per_chunk": int(eng._delta_buffer()[0].numel()
+                                                            * eng._delta_buffer()[0].element_size())})
     return elapsed, phases
 
 

@@ -284,7 +284,7 @@ class MFEngine(ItemSync, Predictor):
 
     def __init__(self, csr, n_items, n_factors, *, algo="svd", hyper=None, biased=True,
                  dtype="float32", mode="log", n_chunks=1, deterministic=False,
-                 user_order=None, n_waves=0, device=None, ld=None, world=1, merge="count",
+                 user_order=None, n_waves=0, device=None, ld=None, world=1, merge=None,
                  ckpt=True, heavy=None, err_in_row=True, events="native", join="event",
                  helpers=True, ydefer=True):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
@@ -329,8 +329,14 @@ class MFEngine(ItemSync, Predictor):
         if self.deterministic:
             mode, n_chunks, n_waves = "plain", 1, 1
         self.mode = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
-        # the log fold's recency weights (MF_MERGE_RECENCY, log mode only)
-        self.recency = merge == "recency" and self.mode == _lib.MF_MODE_LOG
+        # item-side merge rule: the log fold weights each logged gradient by its recency
+        # (MF_MERGE_RECENCY); the snapshot-delta merges of the other modes (several
+        # ranks) by the count-aware rule
+        if merge is None:
+            merge = "recency" if self.mode == _lib.MF_MODE_LOG else "count"
+        if merge == "recency" and self.mode != _lib.MF_MODE_LOG:
+            raise ValueError("merge='recency' is the log schedule's fold (mode='log')")
+        self.recency = merge == "recency"
         self.n_chunks = max(1, int(n_chunks))
         if events not in ("native", "torch") or join not in ("event", "kernel"):
             raise ValueError("events must be 'native' or 'torch', join 'event' or 'kernel'")
@@ -442,9 +448,9 @@ class MFEngine(ItemSync, Predictor):
                 lg["pitem"] = to_dev(np.repeat(np.arange(self.n_items, dtype=np.int32),
                                                np.diff(ipp)))
                 if self.recency:
-                    lg["rpos"] = to_dev(kpos[perm] if kpos is not None else
-                                        np.arange(len(perm), dtype=np.int64) -
-                                        np.repeat(pb[ipp[:-1]], cnt)).astype(np.int32)
+                    rp = kpos[perm] if kpos is not None else \
+                        np.arange(len(perm), dtype=np.int64) - np.repeat(pb[ipp[:-1]], cnt)
+                    lg["rpos"] = to_dev(rp.astype(np.int32))
                 lgs.append(lg)
             main = lgs[0]
             main["heavy"] = lgs[1] if len(lgs) > 1 else None
@@ -482,6 +488,7 @@ class MFEngine(ItemSync, Predictor):
             # A_u = decay^{|I_u|} (the epoch kernel's per-user factor), fp64 on the host
             self.uA = to_dev(np.power(decay, np.diff(row_ptr).astype(np.float64))).to(self.tdt)
         self.totals = None  # set by _prepare(): summed over every rank
+        self._pos0 = []  # (recency, several ranks: per chunk, the item counts of earlier ranks)
         # {sum pu^2, count} of the chunk start, double-buffered: chunk t accumulates into slot
         # t % 2 and its fold clears slot (t + 1) % 2 for the next chunk (no separate fill)
         self._works = torch.zeros(2, 2, dtype=torch.float64, device=dev)
@@ -824,9 +831,10 @@ class MFEngine(ItemSync, Predictor):
         if not self.recency:
             return None
         c = getattr(self, "_chunk", 0)
+        totals = self._totals()[c]  # (prepares the per-item counts on first use)
         pos0 = self._pos0[c] if self._pos0 else None
         rec = _lib.MfRecency(lg["rpos"].data_ptr(), pos0.data_ptr() if pos0 is not None else None,
-                             self._totals()[c].data_ptr(), self.work.data_ptr())
+                             totals.data_ptr(), self.work.data_ptr())
         return ctypes.byref(rec)
 
     def _global_stat(self):

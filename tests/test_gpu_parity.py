@@ -126,7 +126,7 @@ def test_log_mode_long_runs_track_deltalog_oracle(torch, golden, u1, name):
     ts, test = u1
     row_ptr, items, ratings = ts.csr()
     P, f = run_oracle_log("SVD", case["params"], row_ptr, items, ratings, ts.n_items,
-                          ts.global_mean)
+                          ts.global_mean, merge=3)
     ref = _oracle_test_rmse(P, f, "SVD", ts, list(test))[1]
     got64 = _rmse(SVD(**case["params"], dtype="float64").fit(ts).test(test))
     got32 = _rmse(SVD(**case["params"]).fit(ts).test(test))

@@ -157,7 +157,7 @@ def test_svd_log_item_table_above_715mb(torch, dtype, K, n_items):
     got = eng.get_factors()
     hp = orc.hyper(**HYPER)
     pu, qc, bu, bc = orc.svd_sgd_deltalog(row_ptr, local, ratings, len(ids), K, 2, True, gm, hp,
-                                          pu0.copy(), qc0.copy())
+                                          pu0.copy(), qc0.copy(), merge=3)
     tol = 1e-9 if dtype == "float64" else 2e-5
     np.testing.assert_allclose(got["pu"], pu, rtol=0, atol=tol)
     np.testing.assert_allclose(got["qi"][ids], qc, rtol=0, atol=tol)

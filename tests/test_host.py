@@ -287,3 +287,49 @@ def test_piece_bounds_partition_every_range():
             assert ptr[i + 1] - ptr[i] == -(-n // rows)
             if n:
                 assert b[0] == offs[i] and b[-1] == offs[i + 1]
+
+
+# ------------------------------------------------------------------ log layouts (host side)
+
+def _random_csr(seed=0, n_users=200, n_items=50):
+    rng = np.random.RandomState(seed)
+    deg = rng.randint(1, 30, n_users)
+    row_ptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    items = np.concatenate([rng.choice(n_items, d, replace=False) for d in deg]).astype(np.int32)
+    return rng, row_ptr, items
+
+
+def test_packed_checkpoint_rows_are_one_per_pair_and_in_bounds():
+    """ckpt_positions / ck_row0 (the kernels' packed log): every pair of a user's ratings has its
+    own row, both ratings of a pair share it, and the rows fit in ck_row0[n_users]."""
+    from surprise_amd.engine import ck_row0, ckpt_positions, log_layout
+    _, row_ptr, items = _random_csr()
+    perm, _, _, _ = log_layout(row_ptr, items, np.arange(len(row_ptr) - 1), 50)
+    ck = ckpt_positions(row_ptr, perm)
+    row, odd = ck >> 1, ck & 1
+    u = np.searchsorted(row_ptr, perm, side="right") - 1
+    j = perm - row_ptr[u]
+    assert np.array_equal(odd, j & 1)
+    assert np.array_equal(row, ck_row0(row_ptr)[u] + j // 2)
+    assert row.max() < ck_row0(row_ptr)[-1]
+    pairs = {}
+    for r, uu, jj in zip(row, u, j // 2):
+        assert pairs.setdefault(int(r), (int(uu), int(jj))) == (int(uu), int(jj))
+
+
+def test_recency_positions_follow_user_order_within_items():
+    """The recency fold's positions: a rating's rank among the chunk's ratings of its item in
+    user order, the same from a chunk's single-group perm and from the general form."""
+    from surprise_amd.engine import item_positions, log_layout
+    rng, row_ptr, items = _random_csr(1)
+    users = rng.choice(len(row_ptr) - 1, 120, replace=False)
+    perm, pb, ipp, cnt = log_layout(row_ptr, items, users, 50)
+    rp = np.arange(len(perm)) - np.repeat(pb[ipp[:-1]], cnt)
+    ks, pos = item_positions(row_ptr, items, users, 50)
+    kpos = np.zeros(int(row_ptr[-1]), np.int32)
+    kpos[ks] = pos
+    assert np.array_equal(rp, kpos[perm])
+    for i in range(50):  # positions 0..N_i-1 in increasing CSR position
+        sel = items[perm] == i
+        assert np.array_equal(rp[sel], np.arange(sel.sum()))
+        assert np.all(np.diff(perm[sel]) > 0)
