@@ -69,7 +69,8 @@ def parse():
                    help="device arithmetic; default f64 (the reference's: mf.pyx:207-227) for "
                         "ml-1m, f32 for c4 / c5 (fp64 K=128 item rows exceed the 1 KiB "
                         "lookahead layout and the fp64 log would not fit C4 on one GPU)")
-    p.add_argument("--chunks", type=int, default=1)
+    p.add_argument("--chunks", type=int, default=0,
+                   help="epoch-chunks (0: the engine's default, engine.default_chunks)")
     p.add_argument("--merge", default=None, choices=["count", "recency"],
                    help="log schedule's item fold (default: the engine's)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -400,11 +401,14 @@ def main():
     mode = args.mode if args.mode != "auto" else ("atomic" if algo == "svdpp" else "log")
     n_users = len(row_ptr) - 1
 
+    from surprise_amd.engine import default_chunks
+
     def make_engine(a=algo, k=K, md=mode, dt=args.dtype):
         pu, qi, yj = init_tables(args.shape, rank, n_users, n_items, k, a == "svdpp",
                                  getattr(workload, "user_lo", 0))
         eng = MFEngine(csr, n_items, k, algo=a, hyper=hyper_for(a, gm), mode=md,
-                       dtype=TORCH_DTYPE[dt], n_chunks=args.chunks, world=world,
+                       dtype=TORCH_DTYPE[dt], world=world,
+                       n_chunks=args.chunks or default_chunks(a, md, n_users_global),
                        **({"merge": args.merge} if args.merge else {}))
         eng.set_factors(pu, qi, yj=yj)
         eng._prepare(ctx)  # global per-item counts (all ranks)

@@ -17,7 +17,8 @@ no CPU fallback.  Extra, keyword-only device options:
                      epoch-chunk -- race-free, bit-reproducible), "atomic" (shared rows,
                      float atomics), "plain" (shared rows, plain stores) or "auto" ("log" for
                      SVD, "atomic" for SVD++)
-  chunks_per_epoch   epoch-chunks (item merges / all-reduces per epoch)
+  chunks_per_epoch   epoch-chunks (item merges / all-reduces per epoch); "auto" (default): 1
+                     for SVD, one per 100,000 users for SVD++ (engine.default_chunks)
   deterministic      one wavefront, users in Trainset order: the reference's exact sequence
   n_waves            wavefronts per launch (0 = fill the GPU)
   distributed        opt-in: shard users over the torch.distributed ranks of the job (one
@@ -140,10 +141,14 @@ class _MFBase(AlgoBase):
             b = shard_users(csr[0], world)
             lo, hi = int(b[ctx.rank]), int(b[ctx.rank + 1])
             csr = local_csr(csr, lo, hi)
+        chunks = self.chunks_per_epoch
+        if chunks == "auto":
+            from .engine import default_chunks
+            chunks = default_chunks(self._algo, self._resolve_mode(), n_users)
         eng = MFEngine(csr, n_items, self.n_factors, algo=self._algo,
                        hyper=self._hyper(global_mean), biased=getattr(self, "biased", True),
                        dtype=self.dtype, mode=self._resolve_mode(),
-                       n_chunks=self.chunks_per_epoch, deterministic=self.deterministic,
+                       n_chunks=chunks, deterministic=self.deterministic,
                        user_order=user_order, n_waves=self.n_waves, world=world,
                        **getattr(self, "_engine_options", {}))
         eng.set_factors(pu[lo:hi], qi, yj=yj)
@@ -279,7 +284,7 @@ class SVD(_MFBase):
                  lr_all=.005, reg_all=.02, lr_bu=None, lr_bi=None, lr_pu=None, lr_qi=None,
                  reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, random_state=None,
                  verbose=False, *, dtype="float32", mode="auto",
-                 chunks_per_epoch=1, deterministic=False, n_waves=0, distributed=False):
+                 chunks_per_epoch="auto", deterministic=False, n_waves=0, distributed=False):
         self.n_factors = n_factors
         self.n_epochs = n_epochs
         self.biased = biased
@@ -335,7 +340,7 @@ class SVDpp(_MFBase):
                  reg_all=.02, lr_bu=None, lr_bi=None, lr_pu=None, lr_qi=None, lr_yj=None,
                  reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, reg_yj=None,
                  random_state=None, verbose=False, *, dtype="float32", mode="auto",
-                 chunks_per_epoch=1, deterministic=False, n_waves=0,
+                 chunks_per_epoch="auto", deterministic=False, n_waves=0,
                  distributed=False):
         self.n_factors = n_factors
         self.n_epochs = n_epochs
