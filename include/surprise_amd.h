@@ -76,7 +76,9 @@ typedef struct mf_csr {
  * reference's per-rating order); the item rows qb[i] = [q_i | b_i] are updated per `mode`.
  *   pu [n_users][ldu], bu [n_users], qb [n_items][ldq]
  *   biased    : 0 reproduces SVD(biased=False) (hp->global_mean must then be 0)
- *   mode      : MF_MODE_*
+ *   mode      : MF_MODE_*; MF_MODE_LOG with ldq * sizeof(dtype) <= 1 KiB (the lookahead body)
+ *               needs ldq >= n_factors + 2 and qb[i][n_factors + 1] = 1 for every item (the user
+ *               bias rides in that column of the user row; the column is never updated)
  *   qlog      : MF_MODE_LOG: device [nnz][ldq] gradient log, row k = err_k * [p_u | 1 | 0..] of
  *               rating k of the CSR (the user row before the rating's step; whole rows written,
  *               zero padding included); each user's segment must be < 2^30
@@ -105,8 +107,8 @@ typedef struct mf_csr {
  * atomics; sched entries < 0 are skipped (a schedule laid out per chain, strided by n_waves). */
 #define MF_EPOCH_SVDPP_HELPERS 2
 /* mf_svd_epoch / mf_svd_epoch_sq with the checkpoint log (elog): err_k is written into its pair's
- * checkpoint row, padding column E + (k - c) (E = n_factors + 1 rounded up to even for fp32,
- * n_factors + 1 for fp64; needs E + 2 <= ldq) instead of elog[k]; mf_log_replay with the same
+ * checkpoint row, padding column E + (k - c) (E = n_factors + 2 rounded up to even for fp32,
+ * n_factors + 2 for fp64; needs E + 2 <= ldq) instead of elog[k]; mf_log_replay with the same
  * flag reads it there (no per-rating gather of elog). */
 #define MF_EPOCH_ERR_IN_ROW 4
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,

@@ -862,6 +862,11 @@ __device__ __forceinline__ void wave_sum2_u(T x, T y, T &sx, T &sy) {
 // (columns 0..K; mf_log_apply turns the sums into the item steps).  Same arithmetic as the
 // reference recursion up to rounding (fp64: equal to the delta-log oracle to 1e-9,
 // tests/test_gpu_parity.py).
+// The user bias rides in the row too: column K+1 of the user row holds c_k = mu + bu_k and the
+// item table's column K+1 is the constant 1 (MF_MODE_LOG's layout, include/surprise_amd.h), with
+// ap = abu, lrp = lr_bu and a constant kb added to A in that column: c's recursion
+// c_{k+1} = abu c_k + kb + lr_bu err_k is the row's own, <q_k, p_k> includes c_k and Y_k includes
+// lr_bu, so err_k = r_k - X_k - err_{k-1} Y_k with no scalar bias recursion beside it.
 template <typename T, int G, bool CK, bool ER = false>
 __device__ __forceinline__ void epoch_body_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
@@ -884,8 +889,11 @@ __device__ __forceinline__ void epoch_body_la(
 
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), prow = (uint32_t)ldu * sizeof(T);
     const uint32_t q_oob = (uint32_t)n_items * qrow;
+    const T lr_bu = biased ? hp.lr_bu : T(0);
+    const T abu = T(1) - lr_bu * hp.reg_bu;
+    const T kb = hp.gm * (T(1) - abu);
     uint32_t cq[G], cu[G], cl[G];
-    vec one[G], lrp[G], ap[G];
+    vec one[G], lrp[G], ap[G], kvec[G], cvec[G];
 #pragma unroll
     for (int v = 0; v < G; ++v) {
         const int c0 = (lane + kWave * v) * W;
@@ -896,20 +904,21 @@ __device__ __forceinline__ void epoch_body_la(
 #pragma unroll
         for (int e = 0; e < W; ++e) {
             const int c = c0 + e;
-            const bool fac = c < K, bias = biased && c == K;
+            const bool fac = c < K, bias = biased && c == K, ub = c == K + 1;
             L::set(one[v], e, bias ? T(1) : T(0));
-            L::set(lrp[v], e, fac ? hp.lr_pu : T(0));
-            L::set(ap[v], e, fac ? T(1) - hp.lr_pu * hp.reg_pu : T(1));
+            L::set(cvec[v], e, ub ? T(1) : T(0));
+            L::set(lrp[v], e, fac ? hp.lr_pu : (ub ? lr_bu : T(0)));
+            L::set(ap[v], e, fac ? T(1) - hp.lr_pu * hp.reg_pu : (ub ? abu : T(1)));
+            L::set(kvec[v], e, ub ? kb : T(0));
         }
     }
+    // the lane and element of column K+1 (c = mu + bu)
+    const int cb_lane = ((K + 1) / W) % kWave, cb_grp = ((K + 1) / W) / kWave, cb_e = (K + 1) % W;
     // err_col > 0: lane d < kB of a bank's err vector goes to its pair's checkpoint row (the
     // bank's row d / 2), column err_col + (d & 1)
     const uint32_t ce = (ER && lane < kB)
                             ? (uint32_t)(((lane >> 1) * ldq + err_col + (lane & 1)) * sizeof(T))
                             : kLogOob;
-    const T lr_bu = biased ? hp.lr_bu : T(0);
-    const T abu = T(1) - lr_bu * hp.reg_bu;
-    const T kb = hp.gm * (T(1) - abu);
     const rsrc_t q_rs = make_rsrc(qb, q_oob);
     const int prio_len = (int)(row_ptr[sched[0] + 1] - row_ptr[sched[0]]);
 
@@ -929,10 +938,12 @@ __device__ __forceinline__ void epoch_body_la(
         const rsrc_t p_rs = make_rsrc(pu + (int64_t)u * ldu, (uint32_t)K * sizeof(T));
         const rsrc_t b_rs = make_rsrc(bu + u, sizeof(T));
 
+        // p_0 = [p_u | 1 | mu + bu]: the item bias's constant and the user bias in the row
+        const T bu0 = Buf<T>::template ld<0>(b_rs, 0);
         vec p0[G];
 #pragma unroll
-        for (int v = 0; v < G; ++v) p0[v] = L::template ld<0>(p_rs, cu[v]) + one[v];
-        const T bu0 = Buf<T>::template ld<0>(b_rs, 0);
+        for (int v = 0; v < G; ++v)
+            p0[v] = L::template ld<0>(p_rs, cu[v]) + one[v] + (hp.gm + bu0) * cvec[v];
 
 
         // Two banks of kB gathered rows alternate.  At the start of a bank: the ids of the bank
@@ -999,10 +1010,9 @@ __device__ __forceinline__ void epoch_body_la(
             __builtin_amdgcn_sched_barrier(0);
             fill(0, go0, gr0);
         }
-        // state entering rating k: err_p = err_{k-1}, c0_p = c0_{k-1}, A_p = A_{k-1}, D_p = D_{k-1},
-        // X = X_k, Yb = Y_k + lr_bu (k = 0: err_{-1} = 0, c0_{-1} = c_0, A_{-1} = p_0, D_{-1} = 0,
-        // X_0 = <q_0, p_0>)
-        T err_p = T(0), c0_p = hp.gm + bu0, X, Yb = T(0);
+        // state entering rating k: err_p = err_{k-1}, A_p = A_{k-1}, D_p = D_{k-1}, X = X_k,
+        // Y = Y_k (k = 0: err_{-1} = 0, A_{-1} = p_0, D_{-1} = 0, X_0 = <q_0, p_0>)
+        T err_p = T(0), X, Y = T(0);
         vec A_p[G], D_p[G];
         {
             vec part = L::splat(T(0));
@@ -1025,13 +1035,14 @@ __device__ __forceinline__ void epoch_body_la(
             // steps' memory waits in order
 #pragma unroll
             for (int v = 0; v < G; ++v) asm volatile("" : "+v"(qn[v])::"memory");
-            const T err = (br[bk][d] - c0_p) - X - err_p * Yb;  // mf.pyx:250
-            const T c0 = abu * (lr_bu * err_p + c0_p) + kb;     // mf.pyx:253, one rating late
+            // (X + err_p Y = <q_k, p_k> + c_k: the bias columns ride in the dot)
+            const T err = (br[bk][d] - X) - err_p * Y;  // mf.pyx:250
             vec pk[G], A[G], D[G], px = L::splat(T(0)), py = L::splat(T(0));
 #pragma unroll
             for (int v = 0; v < G; ++v) {
-                pk[v] = A_p[v] + err_p * D_p[v];  // p_k (mf.pyx:258-262, one rating late)
-                A[v] = ap[v] * pk[v];
+                // p_k, c_k (mf.pyx:253-262, one rating late)
+                pk[v] = A_p[v] + err_p * D_p[v];
+                A[v] = ap[v] * pk[v] + kvec[v];
                 D[v] = lrp[v] * bank[bk][d][v];
                 px += qn[v] * A[v];
                 py += qn[v] * D[v];
@@ -1045,9 +1056,8 @@ __device__ __forceinline__ void epoch_body_la(
             wave_sum2_u(L::hsum(px), L::hsum(py), Xn, Yn);  // X_{k+1}, Y_{k+1}
             if (FULL) {
                 err_p = err;
-                c0_p = c0;
                 X = Xn;
-                Yb = Yn + lr_bu;
+                Y = Yn;
 #pragma unroll
                 for (int v = 0; v < G; ++v) {
                     A_p[v] = A[v];
@@ -1055,9 +1065,8 @@ __device__ __forceinline__ void epoch_body_la(
                 }
             } else {
                 err_p = valid ? err : err_p;
-                c0_p = valid ? c0 : c0_p;
                 X = valid ? Xn : X;
-                Yb = valid ? Yn + lr_bu : Yb;
+                Y = valid ? Yn : Y;
 #pragma unroll
                 for (int v = 0; v < G; ++v) {
                     A_p[v] = valid ? A[v] : A_p[v];
@@ -1110,12 +1119,14 @@ __device__ __forceinline__ void epoch_body_la(
         } else {
             tail_bank(B0{});
         }
-        // after rating n-1: p_n = A_{n-1} + err_{n-1} D_{n-1}, c_n = lr_bu err_{n-1} + c0_{n-1}
+        // after rating n-1: p_n = A_{n-1} + err_{n-1} D_{n-1} (column K+1: c_n = mu + bu)
         double sq = 0;  // psq: sum of p_n^2 over the factor columns (the log fold's <p^2>)
+        T cn = T(0);
 #pragma unroll
         for (int v = 0; v < G; ++v) {
             const vec pn = A_p[v] + err_p * D_p[v];
             L::template st<0>(p_rs, cu[v], pn);
+            if (v == cb_grp) cn = readlane(L::get(pn, cb_e), cb_lane);
 #pragma unroll
             for (int e = 0; e < W; ++e) {
                 const double x = (double)L::get(pn, e);
@@ -1126,7 +1137,7 @@ __device__ __forceinline__ void epoch_body_la(
             sq = wave_sum(sq);
             if (lane == 0) psq[u] = sq;
         }
-        const T bu_u = lr_bu * err_p + c0_p - hp.gm;
+        const T bu_u = cn - hp.gm;
         Buf<T>::template st<0>(b_rs, lane == 0 ? 0u : (uint32_t)sizeof(T), bu_u);
         __builtin_amdgcn_s_setprio(0);
     };
@@ -1637,6 +1648,9 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
 {
     if ((psq || err_col) && (PP || M != kLog || !elog))
         return set_err(MF_E_UNSUPPORTED, "user_sq / errors in rows: the SVD checkpoint log only");
+    // the lookahead body (SVD, MF_MODE_LOG, rows <= 1 KiB) carries the user bias in column K + 1
+    if (!PP && M == kLog && MF_LA && (int64_t)ldq * sizeof(T) <= 512 * kLaMaxG && ldq < K + 2)
+        return set_err(MF_E_ARG, "MF_MODE_LOG: ldq >= n_factors + 2 (the user-bias column)");
     // elog: SVD: the checkpoint log (the lookahead body: kLog, up to two lane groups);
     //       SVD++: the deferred y buffer (kAtomic)
     if (elog && !PP && (M != kLog || !MF_LA || (int64_t)ldq * sizeof(T) > 512 * kLaMaxG))
@@ -2049,9 +2063,11 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
 // load per piece, and the replay gathers nothing but the checkpoint rows (no item rows, no item
 // ids).  Summed per piece in perm order exactly like log_reduce_kernel; equal to the gradient
 // log's sums up to a rounding of the undone step (fp64: the delta-log oracle to 1e-9).
-// One wave per piece (<= 64 ratings): lane x holds rating x's checkpoint offset, parity and
-// err (vector gathers once per piece); per rating v_readlane broadcasts, the row gather and 3
-// packed FMAs.  Two groups of MF_REPLAY_U rows are in flight per wave.
+// One wave per piece (<= 64 ratings): lane x holds rating x's checkpoint offset, parity, err
+// and weight (vector gathers once per piece).  Odd and even ratings are summed apart, so a
+// rating costs two v_readlane broadcasts, the row gather and 2 (packed) FMAs per element; the
+// undone step enters once per piece: sum_even w err_k p_k = iap o (sum_even w err p_{c+1} -
+// D sum_even w err^2).  Two groups of MF_REPLAY_U rows are in flight per wave.
 template <typename T, int G, bool REC>
 __device__ __forceinline__ void log_replay_body(
     const T *__restrict__ ckpt, const T *__restrict__ elog, int ldq, int K,
@@ -2095,20 +2111,33 @@ __device__ __forceinline__ void log_replay_body(
         // lane x: rating x, its pair's (packed) checkpoint row and parity (ck_pos = 2 row + odd)
         const int k_l = perm[xl], ck_l = ck_pos[xl];
         const int c_l = ck_l >> 1, odd_l = ck_l & 1;  // odd 1: k = c + 1 (the row as stored)
-        // err_k: gathered from elog, or (err_col > 0) read from the row below
-        const T ek_l = lane < cnt && err_col <= 0 ? elog[k_l] : T(0);  // lanes >= cnt: weight 0
+        // err_k per lane: from elog, or (err_col > 0) column err_col + odd of its checkpoint row
+        // (one gather per lane: the line is the row load's own); lanes >= cnt: 0, weight 0
+        const T ek_l = lane >= cnt ? T(0)
+                       : err_col > 0 ? ckpt[(int64_t)c_l * ldq + err_col + odd_l] : elog[k_l];
         // the piece's item row (snapshot) -> D = lrp o q_i
         // (piece_item: the item id without the perm -> items hop on the piece's critical path)
         const int item = piece_item ? piece_item[pc] : items[readlane(k_l, 0)];
         const uint32_t qoff = (uint32_t)item * qrow;
-        T wf_l = T(1), wb_l = T(1);  // (REC: lane x's recency weights)
-        if constexpr (REC) recency_weights(rc, l_q, l_b, item, xl, wf_l, wb_l);
+        // gradient weight per lane: err_k, times (REC) its recency weight wf for the factor
+        // columns; the bias column (p_k's column K is 1, so its gradient is err_k) gets
+        // sum err_k (wb - wf) added once per piece.
+        T ef_l = ek_l, dw_l = T(0);
+        if constexpr (REC) {
+            T wf_l, wb_l;
+            recency_weights(rc, l_q, l_b, item, xl, wf_l, wb_l);
+            ef_l = ek_l * wf_l;
+            dw_l = wb_l - wf_l;
+        }
+        // g_k = p_k for odd k, iap o (p_{c+1} - err_k D) for even: split by parity so a rating
+        // costs one FMA per element --  acc = sum_odd ef p + iap o (sum_even ef p - D sum_even ef ek)
+        const T eo_l = odd_l ? ef_l : T(0), ee_l = odd_l ? T(0) : ef_l;
         vec D[G];
 #pragma unroll
         for (int v = 0; v < G; ++v) D[v] = lrp[v] * L::template lds<0>(q_rs, cq[v], qoff);
-        vec acc[G];
+        vec ao[G], ae[G];
 #pragma unroll
-        for (int v = 0; v < G; ++v) acc[v] = L::splat(T(0));
+        for (int v = 0; v < G; ++v) ao[v] = ae[v] = L::splat(T(0));
         auto load_grp = [&](const int x0, vec (&p)[kU][G]) {
 #pragma unroll
             for (int y = 0; y < kU; ++y) {  // (x past cnt: lane cnt-1's rating, weight 0)
@@ -2122,32 +2151,11 @@ __device__ __forceinline__ void log_replay_body(
 #pragma unroll
             for (int y = 0; y < kU; ++y) {
                 const int x = x0 + y < kWave ? x0 + y : kWave - 1;
-                const int odd = readlane(odd_l, x);
-                T ek;
-                if (err_col > 0) {  // column err_col + odd of the checkpoint row
-                    const int c = err_col + odd, l = (c / W) % kWave, vg = (c / W) / kWave;
-                    T e = T(0);
+                const T wo = readlane(eo_l, x), we = readlane(ee_l, x);
 #pragma unroll
-                    for (int v = 0; v < G; ++v)
-                        if (v == vg) e = readlane(L::get(p[y][v], c % W), l);
-                    ek = x0 + y < cnt ? e : T(0);
-                } else {
-                    ek = readlane(ek_l, x);
-                }
-                if constexpr (REC) {  // (the weights scale the gradient, not the undone step)
-                    const T wf = readlane(wf_l, x), wb = readlane(wb_l, x);
-                    const T ef = ek * wf, eb = ek * wb;
-#pragma unroll
-                    for (int v = 0; v < G; ++v) {
-                        const vec pc_ = iap[v] * (p[y][v] - ek * D[v]);
-                        acc[v] += (L::splat(ef) + (eb - ef) * bsel[v]) * (odd ? p[y][v] : pc_);
-                    }
-                } else {
-#pragma unroll
-                    for (int v = 0; v < G; ++v) {
-                        const vec pc_ = iap[v] * (p[y][v] - ek * D[v]);  // p_c from p_{c+1}
-                        acc[v] += ek * (odd ? p[y][v] : pc_);           // g_k = err_k p_k, in order
-                    }
+                for (int v = 0; v < G; ++v) {
+                    ao[v] += wo * p[y][v];
+                    ae[v] += we * p[y][v];
                 }
             }
         };
@@ -2159,6 +2167,15 @@ __device__ __forceinline__ void log_replay_body(
             if (x0 + kU >= cnt) break;
             load_grp(x0 + 2 * kU, pA);
             comp_grp(x0 + kU, pB);
+        }
+        const T se = wave_sum_u(ee_l * ek_l);
+        T sb = T(0);
+        if constexpr (REC) sb = wave_sum_u(ek_l * dw_l);
+        vec acc[G];
+#pragma unroll
+        for (int v = 0; v < G; ++v) {
+            acc[v] = ao[v] + iap[v] * (ae[v] - se * D[v]);
+            if constexpr (REC) acc[v] += sb * bsel[v];
         }
 #pragma unroll
         for (int v = 0; v < G; ++v) {
@@ -3363,10 +3380,11 @@ int check_epoch(const mf_csr_t *c, const int32_t *sched, const void *pu, const v
 }
 
 // First of the two padding columns that hold a checkpoint row's errors (MF_EPOCH_ERR_IN_ROW):
-// past the bias column, 8-byte aligned for fp32 (one lane's pair); 0 if the row has no room.
+// past the item-bias column K and the user-bias column K + 1, 8-byte aligned for fp32 (one
+// lane's pair); 0 if the row has no room.
 int err_column(int K, int ldq, int dtype)
 {
-    const int c = dtype == MF_F32 ? ((K + 2) & ~1) : K + 1;
+    const int c = dtype == MF_F32 ? ((K + 3) & ~1) : K + 2;
     return c + 2 <= ldq ? c : 0;
 }
 

@@ -75,9 +75,10 @@ ITEM_ROW_ALIGN = 64  # bytes
 
 
 def default_ldq(n_factors: int, dtype: int) -> int:
-    """Item row length: n_factors + the item bias column, padded to a 64-byte multiple."""
+    """Item row length: n_factors + the item-bias column + the constant column of the user bias
+    (the SVD log's lookahead body), padded to a 64-byte multiple."""
     per = ITEM_ROW_ALIGN // (4 if dtype == _lib.MF_F32 else 8)
-    return -(-(n_factors + 1) // per) * per
+    return -(-(n_factors + 2) // per) * per
 
 
 def stable_argsort(keys):
@@ -413,7 +414,7 @@ class MFEngine(ItemSync, Predictor):
         self.heavy_xcd = 1 if heavy > 0 and _lib.xcd_layout_ok() else 0
         # checkpoint log with MF_EPOCH_ERR_IN_ROW where the row has room: each pair's two errors
         # ride in its checkpoint row's padding (the replay gathers no elog entries)
-        e0 = ((self.K + 2) & ~1) if self.dtype == _lib.MF_F32 else self.K + 1
+        e0 = ((self.K + 3) & ~1) if self.dtype == _lib.MF_F32 else self.K + 2
         # (read-only after construction: elog is sized for it)
         self._err_in_row = self.ckpt and e0 + 2 <= self.ldq and bool(err_in_row)
         C = _lib.load().mf_ckpt_interval() if self.ckpt else 0
@@ -600,6 +601,8 @@ class MFEngine(ItemSync, Predictor):
         put(self.qb, qi)
         self.qb[:, K].copy_(t.from_numpy(np.zeros(self.n_items) if bi is None else
                                          np.asarray(bi, np.float64)).to(self.dev, self.tdt))
+        if self.algo == "svd" and self.is_log:  # (the lookahead body's user-bias column)
+            self.qb[:, K + 1] = 1
         if self.yj is not None:
             put(self.yj, yj)
         if self.qb_s is not None:

@@ -370,10 +370,10 @@ def test_zero_epochs_and_single_rating_users(torch):
 
 @pytest.mark.parametrize("K,dtype,chunks", [(20, "float64", 1), (20, "float64", 3),
                                             (100, "float64", 2), (100, "float32", 1),
-                                            (127, "float32", 2)])
+                                            (126, "float32", 2)])
 def test_checkpoint_log_matches_gradient_log(torch, u1, K, dtype, chunks):
     """The checkpoint log (one user row per pair of ratings, errors in the rows' padding -- or in
-    elog where the row has no room, K=127 fp32 --, mf_log_replay rebuilding the gradients by
+    elog where the row has no room, K=126 fp32 --, mf_log_replay rebuilding the gradients by
     undoing one step, <pu^2> from user_sq) against the gradient log (a whole gradient row per
     rating, mf_log_reduce, mf_sumsq): the same epochs from the same state.  Same arithmetic up
     to the summation of the statistic and one rounding per rating: fp64 within 1e-10, fp32
@@ -391,7 +391,7 @@ def test_checkpoint_log_matches_gradient_log(torch, u1, K, dtype, chunks):
         eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype=dtype,
                        mode="log", n_chunks=chunks, ckpt=ck)
         assert eng.ckpt == ck
-        assert eng.err_in_row == (ck and K != 127)
+        assert eng.err_in_row == (ck and K != 126)
         eng.set_factors(pu0, qi0)
         eng.run_epochs(4)
         out.append(eng.get_factors())
@@ -466,7 +466,7 @@ def test_native_fork_and_kernel_join_equal_torch_events(torch, request, monkeypa
 
 
 @pytest.mark.parametrize("K,dtype,heavy", [(100, "float32", 0.25), (20, "float64", 0.0),
-                                            (61, "float64", 0.25)])
+                                            (60, "float64", 0.25)])
 def test_errors_in_checkpoint_rows_equal_elog(torch, u1, monkeypatch, K, dtype, heavy):
     """MF_EPOCH_ERR_IN_ROW (each pair's errors stored in its checkpoint row's padding, read back
     by the replay from the loaded row) against the errors in elog (err_in_row=False):
