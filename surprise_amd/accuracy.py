@@ -1,5 +1,4 @@
-"""Accuracy metrics, mirroring surprise/accuracy.py:22-143 (rmse, mae, fcp)."""
-from collections import defaultdict
+"""Accuracy metrics, mirroring surprise/accuracy.py:22-143 (rmse, mae; fcp is not on the SVD path and is not mirrored)."""
 
 import numpy as np
 
@@ -24,30 +23,3 @@ def mae(predictions, verbose=True):
         print("MAE:  {0:1.4f}".format(mae_))
     return mae_
 
-
-def fcp(predictions, verbose=True):
-    """Fraction of concordant pairs (accuracy.py:91-143)."""
-    if not predictions:
-        raise ValueError("Prediction list is empty.")
-    predictions_u = defaultdict(list)
-    nc_u = defaultdict(int)
-    nd_u = defaultdict(int)
-    for u0, _, r0, est, _ in predictions:
-        predictions_u[u0].append((r0, est))
-    for u0, preds in predictions_u.items():
-        for r0i, esti in preds:
-            for r0j, estj in preds:
-                if esti > estj and r0i > r0j:
-                    nc_u[u0] += 1
-                if esti >= estj and r0i < r0j:
-                    nd_u[u0] += 1
-    nc = np.mean(list(nc_u.values())) if nc_u else 0
-    nd = np.mean(list(nd_u.values())) if nd_u else 0
-    try:
-        fcp_ = nc / (nc + nd)
-    except ZeroDivisionError:
-        raise ValueError("cannot compute fcp on this list of prediction. " +
-                         "Does every user have at least two predictions?")
-    if verbose:
-        print("FCP:  {0:1.4f}".format(fcp_))
-    return fcp_

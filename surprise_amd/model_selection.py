@@ -1,8 +1,8 @@
 """Cross-validation harness around the hot path, mirroring
-surprise/model_selection/split.py (get_cv :44-55, KFold :58-122, ShuffleSplit
-:422-541, train_test_split :543-576, PredefinedKFold :654-685) and
-surprise/model_selection/validation.py (cross_validate :29-142, fit_and_score
-:683-769, print_summary :772-811).
+surprise/model_selection/split.py (get_cv :44-55, KFold :58-122, PredefinedKFold
+:654-685) and surprise/model_selection/validation.py (cross_validate :29-142,
+fit_and_score :683-769).  ShuffleSplit / train_test_split / print_summary are not
+on the SVD path (out of scope) and are not mirrored.
 
 Index logic is the reference's, so a fold built here holds the same ratings in
 the same order as the reference's fold for the same seed; array-native
@@ -11,7 +11,6 @@ datasets (``RatingColumns``) are indexed without Python tuples.
 import numbers
 import time
 from itertools import chain
-from math import ceil, floor
 
 import numpy as np
 
@@ -71,70 +70,6 @@ class KFold:
         return self.n_splits
 
 
-class ShuffleSplit:
-    """split.py:422-541."""
-
-    def __init__(self, n_splits=5, test_size=.2, train_size=None, random_state=None,
-                 shuffle=True):
-        if n_splits <= 0:
-            raise ValueError("n_splits = {0} should be strictly greater than 0.".format(n_splits))
-        if test_size is not None and test_size <= 0:
-            raise ValueError("test_size={0} should be strictly greater than 0".format(test_size))
-        if train_size is not None and train_size <= 0:
-            raise ValueError("train_size={0} should be strictly greater than "
-                             "0".format(train_size))
-        self.n_splits = n_splits
-        self.test_size = test_size
-        self.train_size = train_size
-        self.random_state = random_state
-        self.shuffle = shuffle
-
-    def validate_train_test_sizes(self, test_size, train_size, n_ratings):
-        if test_size is not None and test_size >= n_ratings:
-            raise ValueError("test_size={0} should be less than the number of ratings "
-                             "{1}".format(test_size, n_ratings))
-        if train_size is not None and train_size >= n_ratings:
-            raise ValueError("train_size={0} should be less than the number of ratings "
-                             "{1}".format(train_size, n_ratings))
-        if np.asarray(test_size).dtype.kind == "f":
-            test_size = ceil(test_size * n_ratings)
-        if train_size is None:
-            train_size = n_ratings - test_size
-        elif np.asarray(train_size).dtype.kind == "f":
-            train_size = floor(train_size * n_ratings)
-        if test_size is None:
-            test_size = n_ratings - train_size
-        if train_size + test_size > n_ratings:
-            raise ValueError("The sum of train_size and test_size ({0}) should be smaller than "
-                             "the number of ratings {1}.".format(train_size + test_size,
-                                                                 n_ratings))
-        return int(train_size), int(test_size)
-
-    def split(self, data):
-        # the reference unpacks (train, test) into (test_size, train_size) and then slices
-        # with the swapped names, which cancels out (split.py:517-532)
-        train_size, test_size = self.validate_train_test_sizes(
-            self.test_size, self.train_size, len(data.raw_ratings))
-        rng = get_rng(self.random_state)
-        for _ in range(self.n_splits):
-            if self.shuffle:
-                permutation = rng.permutation(len(data.raw_ratings))
-            else:
-                permutation = np.arange(len(data.raw_ratings))
-            raw_trainset = _subset(data.raw_ratings, permutation[:train_size])
-            raw_testset = _subset(data.raw_ratings, permutation[train_size:train_size + test_size])
-            yield data.construct_trainset(raw_trainset), data.construct_testset(raw_testset)
-
-    def get_n_folds(self):
-        return self.n_splits
-
-
-def train_test_split(data, test_size=.2, train_size=None, random_state=None, shuffle=True):
-    ss = ShuffleSplit(n_splits=1, test_size=test_size, train_size=train_size,
-                      random_state=random_state, shuffle=shuffle)
-    return next(ss.split(data))
-
-
 class PredefinedKFold:
     """split.py:654-685."""
 
@@ -192,37 +127,9 @@ def cross_validate(algo, data, measures=["rmse", "mae"], cv=None, return_train_m
     ret["fit_time"] = fit_times
     ret["test_time"] = test_times
     ret["num_tested"] = [num_tested for _ in fit_times]
-    if verbose:
-        print_summary(algo, measures, test_measures, train_measures, fit_times, test_times,
-                      cv.n_splits)
+    if verbose:  # (the reference's print_summary table is not on the hot path)
+        for m, vals in test_measures.items():
+            print("{} (testset): mean {:1.4f} std {:1.4f}".format(m.upper(), np.mean(vals),
+                                                                  np.std(vals)))
     return ret
 
-
-def print_summary(algo, measures, test_measures, train_measures, fit_times, test_times,
-                  n_splits):
-    print("Evaluating {0} of algorithm {1} on {2} split(s).".format(
-        ", ".join((m.upper() for m in measures)), algo.__class__.__name__, n_splits))
-    print()
-    row_format = "{:<18}" + "{:<8}" * (n_splits + 2)
-    s = row_format.format("", *["Fold {0}".format(i + 1) for i in range(n_splits)] +
-                          ["Mean"] + ["Std"])
-    s += "\n"
-    s += "\n".join(row_format.format(
-        key.upper() + " (testset)", *["{:1.4f}".format(v) for v in vals] +
-        ["{:1.4f}".format(np.mean(vals))] + ["{:1.4f}".format(np.std(vals))])
-        for (key, vals) in test_measures.items())
-    if train_measures:
-        s += "\n"
-        s += "\n".join(row_format.format(
-            key.upper() + " (trainset)", *["{:1.4f}".format(v) for v in vals] +
-            ["{:1.4f}".format(np.mean(vals))] + ["{:1.4f}".format(np.std(vals))])
-            for (key, vals) in train_measures.items())
-    s += "\n"
-    s += row_format.format("Fit time", *["{:.2f}".format(t) for t in fit_times] +
-                           ["{:.2f}".format(np.mean(fit_times))] +
-                           ["{:.2f}".format(np.std(fit_times))])
-    s += "\n"
-    s += row_format.format("Test time", *["{:.2f}".format(t) for t in test_times] +
-                           ["{:.2f}".format(np.mean(test_times))] +
-                           ["{:.2f}".format(np.std(test_times))])
-    print(s)

@@ -9,8 +9,7 @@ import pytest
 from conftest import GOLDEN
 from surprise_amd import (SVD, SVDpp, AlgoBase, Dataset, Prediction, PredictionImpossible,
                           Reader, Trainset, accuracy, synthetic)
-from surprise_amd.model_selection import (KFold, PredefinedKFold, ShuffleSplit, get_cv,
-                                          train_test_split)
+from surprise_amd.model_selection import KFold, PredefinedKFold, get_cv
 from surprise_amd.utils import get_rng
 
 
@@ -89,15 +88,6 @@ def test_kfold_partitions_and_determinism():
     assert isinstance(get_cv(None), KFold) and get_cv(3).n_splits == 3
 
 
-def test_shuffle_split_sizes():
-    u, i, r = synthetic.shape("tiny")
-    data = Dataset.load_from_arrays(u, i, r)
-    tr, te = train_test_split(data, test_size=.25, random_state=0)
-    assert len(te) == 300 and tr.n_ratings == 900
-    tr, te = next(ShuffleSplit(1, test_size=100, train_size=500, random_state=0).split(data))
-    assert len(te) == 100 and tr.n_ratings == 500
-
-
 def test_load_from_df_structured_array():
     import pandas as pd
     df = pd.DataFrame({"u": [1, 2, 2, 3], "i": [10, 10, 20, 30], "r": [4, 3, 5, 1]})
@@ -134,14 +124,6 @@ def test_accuracy_known_answers():
     assert accuracy.mae(preds, verbose=False) == abs(0 - 2) / 2
     preds = [Prediction(0, 0, 2, 1, None), Prediction(0, 0, 3, 4, None)]
     assert accuracy.mae(preds, verbose=False) == (abs(2 - 1) + abs(3 - 4)) / 2
-    u0, u1, u2 = 0, 1, 2
-    preds = [Prediction(u0, 0, 1, 1, None), Prediction(u0, 0, 2, 2, None),
-             Prediction(u0, 0, 3, 3, None), Prediction(u1, 0, 1, 3, None),
-             Prediction(u1, 0, 2, 2, None), Prediction(u1, 0, 3, 1, None)]
-    assert accuracy.fcp(preds, verbose=False) == .5
-    preds.append(Prediction(u2, 0, 1, 2, None))
-    with pytest.raises(ValueError):
-        accuracy.fcp(preds[6:], verbose=False)
     with pytest.raises(ValueError):
         accuracy.rmse([], verbose=False)
 
