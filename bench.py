@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--shape", default="ml-1m", choices=sorted(SHAPE_DEFAULTS))
+    p.add_argument("--hx-chains", type=int, default=0,
+                   help="SVD++ helper-wave launch: user chains per CU (0: the engine default)")
     p.add_argument("--algo", default=None, choices=["svd", "svdpp"])
     p.add_argument("--factors", type=int, default=None)
     p.add_argument("--mode", default="auto")
@@ -409,7 +411,8 @@ def main():
         eng = MFEngine(csr, n_items, k, algo=a, hyper=hyper_for(a, gm), mode=md,
                        dtype=TORCH_DTYPE[dt], world=world,
                        n_chunks=args.chunks or default_chunks(a, md, n_users_global),
-                       **({"merge": args.merge} if args.merge else {}))
+                       **({"merge": args.merge} if args.merge else {}),
+                       **({"hx_chains_per_cu": args.hx_chains} if args.hx_chains else {}))
         eng.set_factors(pu, qi, yj=yj)
         eng._prepare(ctx)  # global per-item counts (all ranks)
         return eng

@@ -1163,15 +1163,17 @@ __device__ __forceinline__ void epoch_body_la(
 #ifndef MF_PP_HX_BANK
 #define MF_PP_HX_BANK 8  // ratings per bank of gathered item rows in the helper-wave chain
 #endif
-#ifndef MF_PP_HX_R
-#define MF_PP_HX_R (4 * MF_PP_HX_BANK)  // ring slots
+#ifndef MF_PP_HX_BANK_G2
+#define MF_PP_HX_BANK_G2 4  // ... with two lane groups (fp32 K > 126): 2 workgroups fit a CU
 #endif
+template <int G>
+constexpr int hx_bank() { return G == 1 ? MF_PP_HX_BANK : MF_PP_HX_BANK_G2; }
 constexpr int kHxHelpers = 3;
 constexpr int kSpinMax = 1 << 22;  // bounded spins (s_sleep 2 each, ~0.2 s): never hang the GPU
 
 template <typename T, int G>
 struct PPRing {
-    static constexpr int R = MF_PP_HX_R;
+    static constexpr int R = 4 * hx_bank<G>();  // ring slots
     typename Lane8<T>::vec data[R][G][kWave];
     uint32_t off[R];
     int head, done;
@@ -1276,7 +1278,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
     using vec = typename L::vec;
     constexpr int W = L::W;
     // (the chain of a helper-wave launch is alone on its SIMD: registers for deeper banks)
-    constexpr int kB = HX ? MF_PP_HX_BANK : (G == 1 ? MF_LA_BANK : MF_LA_BANK_G2);
+    constexpr int kB = HX ? hx_bank<G>() : (G == 1 ? MF_LA_BANK : MF_LA_BANK_G2);
     constexpr int U = Lane1<T, G>::U;
     const int lane = threadIdx.x & (kWave - 1);
     int64_t wave, grid_waves;

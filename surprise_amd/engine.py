@@ -304,7 +304,7 @@ class MFEngine(ItemSync, Predictor):
                  dtype="float32", mode="log", n_chunks=1, deterministic=False,
                  user_order=None, n_waves=0, device=None, ld=None, world=1, merge=None,
                  ckpt=True, heavy=None, err_in_row=True, events="native", join="event",
-                 helpers=True, ydefer=True):
+                 helpers=True, ydefer=True, hx_chains_per_cu=None):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -323,7 +323,8 @@ class MFEngine(ItemSync, Predictor):
           helpers     SVD++ atomic mode: one user chain per workgroup whose q atomics three
                       helper waves issue (MF_EPOCH_SVDPP_HELPERS)
           ydefer      SVD++ atomic mode: the users' y updates folded per item after the chunk
-                      (mf_svdpp_y_fold) instead of float atomics at each user's end"""
+                      (mf_svdpp_y_fold) instead of float atomics at each user's end
+          hx_chains_per_cu  the helper-wave launch's user chains per CU (HX_CHAINS_PER_CU)"""
         torch = _lib.require_gpu()
         self.torch = torch
         self.algo = algo
@@ -490,7 +491,8 @@ class MFEngine(ItemSync, Predictor):
         self._hx_status = torch.zeros(1, dtype=torch.int32, device=dev) if self.hx else None
         if self.hx:
             props = torch.cuda.get_device_properties(self.dev)
-            self.hx_chains = HX_CHAINS_PER_CU * props.multi_processor_count
+            cpc = HX_CHAINS_PER_CU if hx_chains_per_cu is None else int(hx_chains_per_cu)
+            self.hx_chains = max(1, cpc) * props.multi_processor_count
             for us in self.sched:
                 self.hx_sched.append(to_dev(chain_schedule(us.cpu().numpy(), row_ptr,
                                                            self.hx_chains)))

@@ -10,7 +10,6 @@ datasets (``RatingColumns``) are indexed without Python tuples.
 """
 import numbers
 import time
-from itertools import chain
 
 import numpy as np
 
