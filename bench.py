@@ -62,6 +62,9 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--shape", default="ml-1m", choices=sorted(SHAPE_DEFAULTS))
+    p.add_argument("--hot-rows", type=int, default=-1,
+                   help="SVD++ helper-wave launch: q rows with a delta replica (-1: the engine's "
+                        "policy, engine.hot_items)")
     p.add_argument("--hx-chains", type=int, default=0,
                    help="SVD++ helper-wave launch: user chains per CU (0: the engine default)")
     p.add_argument("--algo", default=None, choices=["svd", "svdpp"])
@@ -412,7 +415,8 @@ def main():
                        dtype=TORCH_DTYPE[dt], world=world,
                        n_chunks=args.chunks or default_chunks(a, md, n_users_global),
                        **({"merge": args.merge} if args.merge else {}),
-                       **({"hx_chains_per_cu": args.hx_chains} if args.hx_chains else {}))
+                       **({"hx_chains_per_cu": args.hx_chains} if args.hx_chains else {}),
+                       **({"hot_rows": args.hot_rows} if args.hot_rows >= 0 else {}))
         eng.set_factors(pu, qi, yj=yj)
         eng._prepare(ctx)  # global per-item counts (all ranks)
         return eng

@@ -111,6 +111,13 @@ typedef struct mf_csr {
  * n_factors + 2 for fp64; needs E + 2 <= ldq) instead of elog[k]; mf_log_replay with the same
  * flag reads it there (no per-rating gather of elog). */
 #define MF_EPOCH_ERR_IN_ROW 4
+/* mf_svd_epoch / mf_svd_epoch_sq with the checkpoint log (elog, errors in elog): the checkpoint
+ * rows hold the n_factors factor columns only, at a stride of n_factors (fp32: rounded up to
+ * even) elements instead of ldq -- rows of whole cache lines when n_factors * size is a multiple
+ * of 128 B (K=128 fp32: 512 B vs 576); the log then needs ck_row0 rows of that stride.
+ * mf_log_replay with the same flag reads them so (the bias column's gradient, err_k * 1, is
+ * summed from the errors). */
+#define MF_EPOCH_CKPT_NARROW 16
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
                  const mf_hyper_t *hp, int32_t mode, void *qlog, void *elog, int32_t n_waves,
@@ -129,10 +136,22 @@ int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
  */
 #define MF_HX_HELPER_TIMEOUT 1
 #define MF_HX_CHAIN_FALLBACK 2
+/* hot (nullable, MF_EPOCH_SVDPP_HELPERS only): per item, nonzero = the row has a delta replica at
+ * row n_items + i of qb (qb then holds 2 * n_items rows, the replica rows zero at the call and
+ * 3 * n_items * ldq * size < 2^32).  The float atomics on one row are performed one after the
+ * other at the memory side, so the most-rated items' rows bound the launch; the chains of odd
+ * workgroups add a hot item's deltas to its replica, the others to the row, and every read of a
+ * hot row adds the replica -- the value one row would hold.  mf_svdpp_hot_fold afterwards. */
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
                    const mf_hyper_t *hp, int32_t mode, void *qlog, void *ycbuf, int32_t n_waves,
-                   int32_t flags, int32_t *status, int32_t dtype, void *stream);
+                   int32_t flags, int32_t *status, const uint8_t *hot, int32_t dtype,
+                   void *stream);
+
+/* After mf_svdpp_epoch with hot rows: row i += row n_items + i and the replica row zeroed, for
+ * i in hot_items[0 .. n_hot). */
+int mf_svdpp_hot_fold(void *qb, int32_t ldq, int32_t n_items, const int32_t *hot_items,
+                      int32_t n_hot, int32_t dtype, void *stream);
 
 /*
  * SVD++ deferred y update (MF_MODE_ATOMIC with ycbuf != NULL in mf_svdpp_epoch): the epoch kernel

@@ -22,6 +22,12 @@ MF_EPOCH_DUP_ITEMS = 1
 MF_EPOCH_XCD_SHIFT = 8  # flags bits 8..15: XCD mask (include/surprise_amd.h)
 MF_EPOCH_SVDPP_HELPERS = 2
 MF_EPOCH_ERR_IN_ROW = 4  # checkpoint log: errors in the checkpoint rows' padding
+MF_EPOCH_CKPT_NARROW = 16  # checkpoint log: rows of the factor columns only (errors in elog)
+
+
+def ckpt_narrow_ld(K: int, dtype: int) -> int:
+    """The MF_EPOCH_CKPT_NARROW checkpoint rows' stride (elements): K, fp32 rounded up to even."""
+    return (K + 1) & ~1 if dtype == MF_F32 else K
 MAX_FACTORS = {MF_F32: 512, MF_F64: 256}
 
 
@@ -53,7 +59,9 @@ SIGNATURES = {
     "mf_svd_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32, _i32,
                      ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_svdpp_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp, _i32,
-                       ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _vp, _i32, _vp],
+                       ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _vp, _vp, _i32,
+                       _vp],
+    "mf_svdpp_hot_fold": [_vp, _i32, _i32, _vp, _i32, _i32, _vp],
     "mf_svdpp_y_fold": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32,
                         _vp],
     "mf_svd_epoch_sq": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32,

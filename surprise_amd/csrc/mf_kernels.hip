@@ -40,7 +40,8 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    bool hx, double *psq, int err_col, int32_t *status, void *stream);
+                    bool hx, double *psq, int err_col, int ck_ld, int32_t *status,
+                    const uint8_t *hot, void *stream);
 }  // namespace mf_ext
 
 namespace {
@@ -873,7 +874,7 @@ __device__ __forceinline__ void epoch_body_la(
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *qlog, T *elog, int K,
     int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, double *psq,
-    int err_col)
+    int err_col, int ck_ld)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -889,6 +890,9 @@ __device__ __forceinline__ void epoch_body_la(
 
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), prow = (uint32_t)ldu * sizeof(T);
     const uint32_t q_oob = (uint32_t)n_items * qrow;
+    // CK: the checkpoint rows' stride, ldq or (MF_EPOCH_CKPT_NARROW) K: the factor columns only
+    const uint32_t lrow = CK ? (uint32_t)ck_ld * sizeof(T) : qrow;
+    const int l_cols = ER ? err_col : (CK && ck_ld < ldq ? K : ldq);  // columns a log row stores
     const T lr_bu = biased ? hp.lr_bu : T(0);
     const T abu = T(1) - lr_bu * hp.reg_bu;
     const T kb = hp.gm * (T(1) - abu);
@@ -900,7 +904,7 @@ __device__ __forceinline__ void epoch_body_la(
         const uint32_t b = (uint32_t)c0 * sizeof(T);
         cq[v] = c0 < ldq ? b : q_oob;
         cu[v] = c0 < ldu ? b : prow;  // >= the pu record (K elements): dropped
-        cl[v] = c0 < (ER ? err_col : ldq) ? b : kLogOob;  // (ER: the err columns' own store)
+        cl[v] = c0 < l_cols ? b : kLogOob;  // (ER: the err columns' own store)
 #pragma unroll
         for (int e = 0; e < W; ++e) {
             const int c = c0 + e;
@@ -930,7 +934,7 @@ __device__ __forceinline__ void epoch_body_la(
         else if (n * 4 > prio_len) __builtin_amdgcn_s_setprio(2);
         else if (n * 8 > prio_len) __builtin_amdgcn_s_setprio(1);
         // CK: the user's checkpoint rows, one per pair, packed (ck_row0); else row k per rating
-        const rsrc_t l_rs = CK ? make_rsrc(qlog + ck_row0(s, u) * ldq, (uint32_t)((n + 1) / 2) * qrow)
+        const rsrc_t l_rs = CK ? make_rsrc(qlog + ck_row0(s, u) * ck_ld, (uint32_t)((n + 1) / 2) * lrow)
                                : make_rsrc(qlog + s * ldq, (uint32_t)n * qrow);
         const rsrc_t e_rs = make_rsrc(CK && !ER ? elog + s : qlog, (uint32_t)n * sizeof(T));
         const int32_t *__restrict__ it = items + s;
@@ -984,12 +988,12 @@ __device__ __forceinline__ void epoch_body_la(
                 for (int x = 0; x < kLg; ++x)
 #pragma unroll
                     for (int v = 0; v < G; ++v)
-                        L::template sts<MF_LOG_AUX>(l_rs, cl[v], (uint32_t)(j0p / kCkpt + x) * qrow,
+                        L::template sts<MF_LOG_AUX>(l_rs, cl[v], (uint32_t)(j0p / kCkpt + x) * lrow,
                                                     lg[x][v]);
                 // err_k: into its pair's row (columns err_col, err_col + 1; the row stores above
                 // leave those columns alone) or to elog[k]; one store per bank either way
                 if constexpr (ER)
-                    Buf<T>::template st<0>(l_rs, ce + (uint32_t)(j0p / kCkpt) * qrow, ev);
+                    Buf<T>::template st<0>(l_rs, ce + (uint32_t)(j0p / kCkpt) * lrow, ev);
                 else
                     Buf<T>::template st<0>(e_rs, lane < kB ? (uint32_t)(j0p + lane) * sizeof(T) : kLogOob, ev);
                 return;
@@ -1199,14 +1203,15 @@ __device__ __forceinline__ void set_status(int32_t *status, int32_t bit) {
 }
 
 // helper wave h of a chain: issue the atomics of the slots t = h (mod kHxHelpers)
+// (n_rows: the rows the slots' offsets may address -- 2 n_items with hot-row replicas)
 template <typename T, int G>
-__device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_items,
+__device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_rows,
                                int32_t *status)
 {
     constexpr int R = PPRing<T, G>::R;
     constexpr int U = Lane1<T, G>::U;
     const int lane = threadIdx.x & (kWave - 1);
-    const uint32_t qrow = (uint32_t)ldq * sizeof(T), q_oob = (uint32_t)n_items * qrow;
+    const uint32_t qrow = (uint32_t)ldq * sizeof(T), q_oob = (uint32_t)n_rows * qrow;
     const rsrc_t q_rs = make_rsrc(qb, q_oob);
     uint32_t cq1[U];
 #pragma unroll
@@ -1266,13 +1271,20 @@ __device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_
 // bank's row gathers (a row's vmcnt wait then never covers an atomic younger than a whole bank:
 // an atomic stays counted for thousands of cycles under load).  The y update is deferred:
 // c_u = (m_n - dc^n m_0) / sqrt|I_u| goes to ycbuf (mf_svdpp_y_fold applies it after the chunk).
-template <typename T, int G, bool HX>
+//
+// Hot-row replicas (HOT, the helper-wave launch): the float atomics on one row are performed one
+// after the other at the memory side, so the most-rated items' rows bound the launch (C3: the
+// top item's 4525 ratings of an epoch, ~0.12 us each).  An item with hot[i] != 0 has a delta
+// replica at row n_items + i of qb: the chains of odd workgroups add its deltas there, the
+// others to the row itself, and every read of the row adds the replica (the value one row would
+// hold: no staleness added); mf_svdpp_hot_fold folds the replicas back after the chunk.
+template <typename T, int G, bool HX, bool HOT = false>
 __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *ycbuf, int K,
     Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, PPRing<T, G> *ring,
-    int32_t *status)
+    int32_t *status, const uint8_t *__restrict__ hot = nullptr)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -1292,7 +1304,10 @@ __device__ __forceinline__ void epoch_body_pp_la(
     if (wave >= n_waves) return;
 
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), yrow = (uint32_t)ldu * sizeof(T);
-    const uint32_t q_oob = (uint32_t)n_items * qrow, y_oob = (uint32_t)n_items * yrow;
+    // (HOT: the table's range covers the replicas, rows n_items .. 2 n_items - 1)
+    const uint32_t rep_shift = (uint32_t)n_items * qrow;
+    const uint32_t q_oob = (HOT ? 2u : 1u) * rep_shift, y_oob = (uint32_t)n_items * yrow;
+    const bool to_rep = HOT && (blockIdx.x & 1);  // this chain's hot deltas: to the replicas
     int pushed = 0;  // HX: ratings pushed to the ring
     uint32_t cq[G], cu[G], cq1[U], cy1[U];
     vec one[G], lrp[G], ap[G], lry[G], lrpy[G], lrq[G], nrq[G];
@@ -1378,20 +1393,27 @@ __device__ __forceinline__ void epoch_body_pp_la(
             to_lane8<G>(acc1, m0);
         }
 
-        auto grp_load = [&](int j0, uint32_t &go, T &gr) {
+        auto grp_load = [&](int j0, uint32_t &go, T &gr, int &gh) {
             int j = j0 + (lane & (kB - 1));
             j = j < n ? j : n - 1;
-            go = (uint32_t)it[j] * qrow;
+            const int i = it[j];
+            go = (uint32_t)i * qrow;
             gr = rt[j];
+            if constexpr (HOT) gh = hot[i];
         };
         vec bank[2][kB][G];
+        vec rep[HOT ? 2 : 1][HOT ? kB : 1][G];  // HOT: the replica rows of a bank's entries
         T br[2][kB];
         uint32_t bo[2][kB];
+        uint32_t hm[2] = {0u, 0u};  // HOT: bit d = entry d of the bank is a hot item
         vec dl[kB][G];      // the q deltas of the current bank (issued one bank late)
         uint32_t dlo[kB];   // their row offsets (masked ratings: past the table)
         uint32_t go_n1, go_n2;
         T gr_n1, gr_n2;
-        auto fill = [&](const int bk, const uint32_t go, const T gr) {
+        int gh_n1 = 0, gh_n2 = 0;
+        auto fill = [&](const int bk, const uint32_t go, const T gr, const int gh) {
+            if constexpr (HOT)
+                hm[bk] = (uint32_t)__builtin_amdgcn_ballot_w64(gh != 0) & ((1u << kB) - 1u);
 #pragma unroll
             for (int d = 0; d < kB; ++d) {
                 const uint32_t off = readlane((int)go, d);
@@ -1399,6 +1421,13 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 br[bk][d] = readlane(gr, d);
 #pragma unroll
                 for (int v = 0; v < G; ++v) bank[bk][d][v] = L::template lds<kSc1>(q_rs, cq[v], off);
+                if constexpr (HOT) {  // (a uniform branch: most entries are not hot)
+                    if ((hm[bk] >> d) & 1u) {
+#pragma unroll
+                        for (int v = 0; v < G; ++v)
+                            rep[bk][d][v] = L::template lds<kSc1>(q_rs, cq[v], off + rep_shift);
+                    }
+                }
             }
         };
         auto atomics = [&]() {  // the previous bank's q deltas as float atomics, from this wave
@@ -1448,12 +1477,20 @@ __device__ __forceinline__ void epoch_body_pp_la(
         {
             uint32_t go0;
             T gr0;
-            grp_load(0, go0, gr0);
-            grp_load(kB, go_n1, gr_n1);
+            int gh0 = 0;
+            grp_load(0, go0, gr0, gh0);
+            grp_load(kB, go_n1, gr_n1, gh_n1);
             asm volatile("" ::"v"(go0), "v"(gr0), "v"(go_n1), "v"(gr_n1));
             __builtin_amdgcn_sched_barrier(0);
-            fill(0, go0, gr0);
+            fill(0, go0, gr0, gh0);
         }
+        // a bank entry's item row as the model sees it (HOT: + its replica)
+        auto qrow_of = [&](const int bk, const int d, const int v) -> vec {
+            if constexpr (HOT) {
+                if ((hm[bk] >> d) & 1u) return bank[bk][d][v] + rep[bk][d][v];
+            }
+            return bank[bk][d][v];
+        };
         // state entering rating k: err_p = err_{k-1}, c0_p = c0_{k-1}, Pp = ap o p_{k-1},
         // Mp = dc o m_{k-1}, Dpp = lrp o q_{k-1}, Dmp = lry o q_{k-1}, X = X_k, Yb = Y_k + lr_bu
         // (k = 0: err_{-1} = 0, c0_{-1} = c_0, Pp = p_0, Mp = m_0, X_0 = <q_0, p_0 + m_0>)
@@ -1467,7 +1504,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 Mp[v] = m0[v];
                 Dpp[v] = L::splat(T(0));
                 Dmp[v] = L::splat(T(0));
-                part += bank[0][0][v] * (p0[v] + m0[v]);
+                part += qrow_of(0, 0, v) * (p0[v] + m0[v]);
             }
             X = wave_sum_u(L::hsum(part));
         }
@@ -1476,15 +1513,20 @@ __device__ __forceinline__ void epoch_body_pp_la(
             constexpr int bk = decltype(bank_c)::value;
             const int k = j0 + d;
             const bool valid = FULL || k < n;
-            vec (&qn)[G] = d + 1 < kB ? bank[bk][d + 1] : bank[bk ^ 1][0];
+            const int bn = d + 1 < kB ? bk : bk ^ 1, dn = d + 1 < kB ? d + 1 : 0;
+            vec qn[G];
 #pragma unroll
-            for (int v = 0; v < G; ++v) asm volatile("" : "+v"(qn[v])::"memory");
+            for (int v = 0; v < G; ++v) {
+                asm volatile("" : "+v"(bank[bn][dn][v])::"memory");
+                if constexpr (HOT) asm volatile("" : "+v"(rep[bn][dn][v])::"memory");
+                qn[v] = qrow_of(bn, dn, v);
+            }
             const T err = (br[bk][d] - c0_p) - X - err_p * Yb;  // mf.pyx:483
             const T c0 = abu * (lr_bu * err_p + c0_p) + kb;     // mf.pyx:486, one rating late
             vec P[G], M[G], Dp[G], Dm[G], px = L::splat(T(0)), py = L::splat(T(0));
 #pragma unroll
             for (int v = 0; v < G; ++v) {
-                const vec q = bank[bk][d][v];
+                const vec q = qrow_of(bk, d, v);
                 const vec pk = Pp[v] + err_p * Dpp[v];  // p_k, m_k (one rating late)
                 const vec mk = Mp[v] + err_p * Dmp[v];
                 const vec sk = pk + mk;                 // puf + u_impl (mf.pyx:491-493)
@@ -1496,7 +1538,8 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 py += qn[v] * (lrpy[v] * q);
                 dl[d][v] = err * (lrq[v] * sk) + nrq[v] * q;  // mf.pyx:489, :492
             }
-            dlo[d] = valid ? bo[bk][d] : bo[bk][d] + q_oob;
+            const bool hot_d = HOT && to_rep && ((hm[bk] >> d) & 1u);
+            dlo[d] = valid ? (hot_d ? bo[bk][d] + rep_shift : bo[bk][d]) : bo[bk][d] + q_oob;
             T Xn, Yn;
             wave_sum2_u(L::hsum(px), L::hsum(py), Xn, Yn);  // X_{k+1}, Y_{k+1}
             err_p = valid ? err : err_p;
@@ -1514,13 +1557,14 @@ __device__ __forceinline__ void epoch_body_pp_la(
         int j0 = 0;
         auto full_bank = [&](auto bank_c, auto first_c) {
             constexpr int bk = decltype(bank_c)::value;
-            grp_load(j0 + 2 * kB, go_n2, gr_n2);
+            grp_load(j0 + 2 * kB, go_n2, gr_n2, gh_n2);
             asm volatile("" ::: "memory");  // issue order: ids, rows, then the atomics
-            fill(bk ^ 1, go_n1, gr_n1);
+            fill(bk ^ 1, go_n1, gr_n1, gh_n1);
             asm volatile("" ::: "memory");
             if (!decltype(first_c)::value) flush();
             go_n1 = go_n2;
             gr_n1 = gr_n2;
+            gh_n1 = gh_n2;
 #pragma unroll
             for (int d = 0; d < kB; ++d) step(std::true_type{}, bank_c, j0, d);
             j0 += kB;
@@ -1583,7 +1627,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
         const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,       \
         T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *qlog, T *elog,\
         int K, int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, double *psq,   \
-        int err_col
+        int err_col, int ck_ld
 #define MF_EPOCH_ARGS \
     row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, elog, K, biased, hp,    \
         n_items, n_waves_req, xmask
@@ -1601,7 +1645,8 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
     }
     if constexpr (MODE == kLog && !PP && G <= kLaMaxG && MF_LA) {  // (the gradient log)
         epoch_body_la<T, G, false>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
-                                   qlog, elog, K, biased, hp, n_items, n_waves_req, xmask, psq, 0);
+                                   qlog, elog, K, biased, hp, n_items, n_waves_req, xmask, psq, 0,
+                                   ldq);
     } else {
         epoch_body<T, G, MODE, PP, DUPS, kPF>(MF_EPOCH_ARGS);
     }
@@ -1614,12 +1659,13 @@ __global__ __launch_bounds__(kBlock) void mf_ckpt_epoch_kernel(MF_EPOCH_PARAMS)
 {
     epoch_body_la<T, G, true, ER>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
                                   qlog, elog, K, biased, hp, n_items, n_waves_req, xmask, psq,
-                                  err_col);
+                                  err_col, ck_ld);
 }
 
 // SVD++ with helper waves (MF_SVDPP_HELPERS): workgroup = chain wave 0 + kHxHelpers atomic waves
-template <typename T, int G>
-__global__ __launch_bounds__(kBlock) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS, int32_t *status)
+template <typename T, int G, bool HOT>
+__global__ __launch_bounds__(kBlock) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS, int32_t *status,
+                                                             const uint8_t *hot)
 {
     __shared__ PPRing<T, G> ring;
     const int w = threadIdx.x / kWave;
@@ -1630,11 +1676,12 @@ __global__ __launch_bounds__(kBlock) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS, in
     }
     __syncthreads();
     if (w == 0) {
-        epoch_body_pp_la<T, G, true>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
-                                     yj, elog, K, hp, n_items, n_waves_req, 0, &ring, status);
+        epoch_body_pp_la<T, G, true, HOT>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu,
+                                          qb, ldq, yj, elog, K, hp, n_items, n_waves_req, 0,
+                                          &ring, status, hot);
         if (blockIdx.x >= n_waves_req) lds_store(&ring.done, 1);  // (no chain in this workgroup)
     } else {
-        pp_ring_helper<T, G>(&ring, w - 1, qb, ldq, n_items, status);
+        pp_ring_helper<T, G>(&ring, w - 1, qb, ldq, (HOT ? 2 : 1) * n_items, status);
     }
 }
 
@@ -1646,7 +1693,8 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    bool hx, double *psq, int err_col, int32_t *status, void *stream)
+                    bool hx, double *psq, int err_col, int ck_ld, int32_t *status,
+                    const uint8_t *hot, void *stream)
 {
     if ((psq || err_col) && (PP || M != kLog || !elog))
         return set_err(MF_E_UNSUPPORTED, "user_sq / errors in rows: the SVD checkpoint log only");
@@ -1663,15 +1711,18 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
         return set_err(MF_E_UNSUPPORTED, "deferred y: MF_MODE_ATOMIC only");
     if (hx && !(PP && M == kAtomic && elog && !dups))
         return set_err(MF_E_UNSUPPORTED, "helper waves: SVD++, MF_MODE_ATOMIC, deferred y, no repeated items");
+    if (hot && !hx) return set_err(MF_E_ARG, "hot-row replicas: the helper-wave launch only");
     return dispatch_g<T>(ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         if constexpr (PP && M == kAtomic && V <= kLaMaxG) {
             if (hx) {  // one workgroup per chain: wave 0 trains, waves 1-3 issue the q atomics
-                hipLaunchKernelGGL((mf_svdpp_hx_kernel<T, V>), dim3(waves), dim3(kBlock), 0,
+                auto kern = hot ? mf_svdpp_hx_kernel<T, V, true> : mf_svdpp_hx_kernel<T, V, false>;
+                hipLaunchKernelGGL(kern, dim3(waves), dim3(kBlock), 0,
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
                                    (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
-                                   cast_hyper<T>(hp), csr->n_items, waves, 0, nullptr, 0, status);
+                                   cast_hyper<T>(hp), csr->n_items, waves, 0, nullptr, 0, ldq,
+                                   status, hot);
                 return check_launch("mf_svdpp_hx_kernel");
             }
         } else {
@@ -1685,7 +1736,8 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
                                    (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
-                                   cast_hyper<T>(hp), csr->n_items, waves, xmask, psq, err_col);
+                                   cast_hyper<T>(hp), csr->n_items, waves, xmask, psq, err_col,
+                                   ck_ld);
                 return check_launch("mf_ckpt_epoch_kernel");
             }
         }
@@ -1696,14 +1748,15 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                            (hipStream_t)stream,
                            csr->row_ptr, csr->items, (const T *)csr->ratings, sched, n_sched,
                            (T *)pu, (T *)bu, ldu, (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K,
-                           biased, cast_hyper<T>(hp), csr->n_items, waves, xmask, psq, err_col);
+                           biased, cast_hyper<T>(hp), csr->n_items, waves, xmask, psq, err_col,
+                           ldq);
         return check_launch(PP ? "mf_epoch_kernel<svdpp>" : "mf_epoch_kernel<svd>");
     });
 }
 template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
     void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, bool, double *,
-    int, int32_t *, void *);
+    int, int, int32_t *, const uint8_t *, void *);
 }  // namespace mf_ext
 #else  // the main translation unit
 
@@ -1727,6 +1780,22 @@ JoinArgs take_join() {
 
 namespace {
 
+
+// ---------------------------------------------------------------- hot-row replicas (SVD++)
+// row i += replica row n_items + i, replica = 0, for the listed items (mf_svdpp_hot_fold)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void hot_fold_kernel(T *qb, int ldq, int n_items,
+                                                          const int32_t *__restrict__ hot_items,
+                                                          int64_t total)
+{
+    for (int64_t x = blockIdx.x * (int64_t)kBlock + threadIdx.x; x < total;
+         x += (int64_t)gridDim.x * kBlock) {
+        const int64_t i = hot_items[x / ldq], c = x % ldq;
+        T *rep = qb + (n_items + i) * ldq + c;
+        qb[i * ldq + c] += *rep;
+        *rep = T(0);
+    }
+}
 
 // ---------------------------------------------------------------- item-table merge (epoch-chunk)
 //
@@ -2077,7 +2146,7 @@ __device__ __forceinline__ void log_replay_body(
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
     const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int err_col,
     const int32_t *__restrict__ piece_item, const int64_t wave, const int64_t n_waves,
-    const bool wt, const Recency &rc)
+    const bool wt, const Recency &rc, const int ldc)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -2093,7 +2162,7 @@ __device__ __forceinline__ void log_replay_body(
     for (int v = 0; v < G; ++v) {
         const int c0 = (lane + kWave * v) * W;
         cq[v] = c0 < ldq ? (uint32_t)c0 * sizeof(T) : q_oob;
-        cc[v] = c0 < ldq ? c0 : 0;  // (lanes past the row re-read column 0: no branch)
+        cc[v] = c0 < ldc ? c0 : 0;  // (lanes past the row re-read column 0: no branch)
 #pragma unroll
         for (int e = 0; e < W; ++e) {
             const bool fac = c0 + e < K;
@@ -2103,10 +2172,11 @@ __device__ __forceinline__ void log_replay_body(
     }
     double l_q = 0, l_b = 0;
     vec bsel[G];
-    if constexpr (REC) {
-        recency_logs(rc, l_q, l_b);
-        bias_selector<T, G>(K, bsel);
-    }
+    bias_selector<T, G>(K, bsel);
+    if constexpr (REC) recency_logs(rc, l_q, l_b);
+    // narrow rows (MF_EPOCH_CKPT_NARROW): the K factor columns only; the bias column's gradient
+    // err_k * 1 is summed from the per-lane errors
+    const bool narrow = ldc < ldq;
     for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
         const int beg = piece_beg[pc], cnt = piece_beg[pc + 1] - beg;  // 1 <= cnt <= 64
         const int xl = beg + (lane < cnt ? lane : cnt - 1);
@@ -2116,7 +2186,7 @@ __device__ __forceinline__ void log_replay_body(
         // err_k per lane: from elog, or (err_col > 0) column err_col + odd of its checkpoint row
         // (one gather per lane: the line is the row load's own); lanes >= cnt: 0, weight 0
         const T ek_l = lane >= cnt ? T(0)
-                       : err_col > 0 ? ckpt[(int64_t)c_l * ldq + err_col + odd_l] : elog[k_l];
+                       : err_col > 0 ? ckpt[(int64_t)c_l * ldc + err_col + odd_l] : elog[k_l];
         // the piece's item row (snapshot) -> D = lrp o q_i
         // (piece_item: the item id without the perm -> items hop on the piece's critical path)
         const int item = piece_item ? piece_item[pc] : items[readlane(k_l, 0)];
@@ -2144,7 +2214,7 @@ __device__ __forceinline__ void log_replay_body(
 #pragma unroll
             for (int y = 0; y < kU; ++y) {  // (x past cnt: lane cnt-1's rating, weight 0)
                 const int x = x0 + y < kWave ? x0 + y : kWave - 1;
-                const T *row = ckpt + (int64_t)readlane(c_l, x) * ldq;
+                const T *row = ckpt + (int64_t)readlane(c_l, x) * ldc;
 #pragma unroll
                 for (int v = 0; v < G; ++v) p[y][v] = *(const vec *)(row + cc[v]);
             }
@@ -2173,11 +2243,13 @@ __device__ __forceinline__ void log_replay_body(
         const T se = wave_sum_u(ee_l * ek_l);
         T sb = T(0);
         if constexpr (REC) sb = wave_sum_u(ek_l * dw_l);
+        if (narrow) sb += wave_sum_u(ef_l);  // (the bias column read nothing: all of it here)
         vec acc[G];
 #pragma unroll
         for (int v = 0; v < G; ++v) {
             acc[v] = ao[v] + iap[v] * (ae[v] - se * D[v]);
-            if constexpr (REC) acc[v] += sb * bsel[v];
+            if (narrow) acc[v] -= acc[v] * bsel[v];
+            acc[v] += sb * bsel[v];
         }
 #pragma unroll
         for (int v = 0; v < G; ++v) {
@@ -2252,13 +2324,13 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
     const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int xmask,
     int err_col, const int32_t *__restrict__ piece_item, uint32_t *join, int join_role,
-    uint32_t join_epoch, Recency rc)
+    uint32_t join_epoch, Recency rc, int ldc)
 {
     int64_t wave, n_waves;
     if (wave_slot(xmask, wave, n_waves))
         log_replay_body<T, G, REC>(ckpt, elog, ldq, K, items, qb, n_items, lr_pu, inv_ap, perm,
                                    ck_pos, piece_beg, n_pieces, sums, err_col, piece_item, wave,
-                                   n_waves, join && join_role == 1, rc);
+                                   n_waves, join && join_role == 1, rc, ldc);
     if (join) join_arrive(join, join_role, join_epoch);
 }
 
@@ -3390,6 +3462,9 @@ int err_column(int K, int ldq, int dtype)
     return c + 2 <= ldq ? c : 0;
 }
 
+// MF_EPOCH_CKPT_NARROW: the checkpoint rows' stride, K rounded up to 8 bytes (whole lane pairs)
+int ckpt_narrow_ld(int K, int dtype) { return dtype == MF_F32 ? (K + 1) & ~1 : K; }
+
 // the kernels' recency inputs (rec NULL: off)
 int make_recency(const mf_recency_t *rec, const mf_hyper_t *hp, Recency &rc)
 {
@@ -3406,7 +3481,8 @@ template <bool PP>
 int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                  int32_t biased, const mf_hyper_t *hp, int32_t mode, int32_t n_waves, int32_t flags,
-                 int32_t dtype, void *stream, double *psq = nullptr, int32_t *status = nullptr)
+                 int32_t dtype, void *stream, double *psq = nullptr, int32_t *status = nullptr,
+                 const uint8_t *hot = nullptr)
 {
     const bool dups = flags & MF_EPOCH_DUP_ITEMS;
     const bool hx = flags & MF_EPOCH_SVDPP_HELPERS;
@@ -3420,7 +3496,17 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         err_col = err_column(K, ldq, dtype);
         if (err_col <= 0) return set_err(MF_E_UNSUPPORTED, "MF_EPOCH_ERR_IN_ROW: no spare columns");
     }
+    int ck_ld = ldq;  // the checkpoint rows' stride
+    if (flags & MF_EPOCH_CKPT_NARROW) {
+        if (PP || mode != MF_MODE_LOG || !elog || err_col || K < 1)
+            return set_err(MF_E_ARG, "MF_EPOCH_CKPT_NARROW: the SVD checkpoint log, errors in elog");
+        ck_ld = ckpt_narrow_ld(K, dtype);
+    }
     if (PP && !yj) return set_err(MF_E_ARG, "null yj");
+    // hot-row replicas: the range covers 2 n_items rows and the masked offsets (row + range) must
+    // stay below 2^32
+    if (hot && 3.0 * csr->n_items * ldq * (dtype == MF_F32 ? 4.0 : 8.0) >= 4294967296.0)
+        return set_err(MF_E_UNSUPPORTED, "hot-row replicas: item table >= 1.33 GiB");
     if (n_sched <= 0) return 0;
     // default: one wave per user up to MF_EPOCH_WPC waves per CU (then strided): a wave that
     // finishes its user exits and the dispatcher starts the next one -- measured 5 us faster at
@@ -3432,7 +3518,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         constexpr int M = decltype(mode_c)::value;
         return mf_ext::launch_epoch_tm<T, M, PP>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj,
                                                   qlog, elog, K, biased, hp, waves, dups, xmask,
-                                                  hx, psq, err_col, status, stream);
+                                                  hx, psq, err_col, ck_ld, status, hot, stream);
     };
     auto by_mode = [&](auto tag_t) -> int {
         switch (mode) {
@@ -3476,7 +3562,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 920; }
+int mf_version(void) { return 930; }
 
 #ifndef MF_SOURCE_HASH
 #define MF_SOURCE_HASH "unknown"
@@ -3559,11 +3645,28 @@ int mf_svd_epoch_sq(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                    int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
                    const mf_hyper_t *hp, int32_t mode, void *qlog, void *ycbuf, int32_t n_waves,
-                   int32_t flags, int32_t *status, int32_t dtype, void *stream)
+                   int32_t flags, int32_t *status, const uint8_t *hot, int32_t dtype, void *stream)
 {
     return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, ycbuf,
                               n_factors, 1, hp, mode, n_waves, flags, dtype, stream, nullptr,
-                              status);
+                              status, hot);
+}
+
+int mf_svdpp_hot_fold(void *qb, int32_t ldq, int32_t n_items, const int32_t *hot_items,
+                      int32_t n_hot, int32_t dtype, void *stream)
+{
+    if (n_hot < 0 || n_items < 0 || ldq <= 0) return set_err(MF_E_ARG, "bad argument");
+    if (n_hot == 0) return 0;
+    if (!qb || !hot_items) return set_err(MF_E_ARG, "null pointer");
+    const int64_t total = (int64_t)n_hot * ldq;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == MF_F32)
+        hipLaunchKernelGGL(hot_fold_kernel<float>, dim3(elementwise_grid(total)), dim3(kBlock), 0,
+                           st, (float *)qb, ldq, n_items, hot_items, total);
+    else
+        hipLaunchKernelGGL(hot_fold_kernel<double>, dim3(elementwise_grid(total)), dim3(kBlock), 0,
+                           st, (double *)qb, ldq, n_items, hot_items, total);
+    return check_launch("hot_fold_kernel");
 }
 
 int mf_sumsq(const void *x, int64_t n_rows, int32_t n_cols, int32_t ld, double *out, int32_t dtype,
@@ -3666,6 +3769,9 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
     const int err_col = (flags & MF_EPOCH_ERR_IN_ROW) ? err_column(n_factors, ldq, dtype) : 0;
     if ((flags & MF_EPOCH_ERR_IN_ROW) && err_col <= 0)
         return set_err(MF_E_UNSUPPORTED, "MF_EPOCH_ERR_IN_ROW: no spare columns");
+    if ((flags & MF_EPOCH_CKPT_NARROW) && (err_col || n_factors < 1))
+        return set_err(MF_E_ARG, "MF_EPOCH_CKPT_NARROW: errors in elog, n_factors >= 1");
+    const int ldc = (flags & MF_EPOCH_CKPT_NARROW) ? ckpt_narrow_ld(n_factors, dtype) : ldq;
     const int64_t rb = (int64_t)ldq * (dtype == MF_F64 ? 8 : 4);
     if (rb > 512 * kLaMaxG) return set_err(MF_E_UNSUPPORTED, "checkpoint log: ldq * size <= 1 KiB only");
     Recency rc;
@@ -3686,7 +3792,7 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
                                    (const T *)qb, csr->n_items, (T)hp->lr_pu,
                                    (T)(1.0 / (1.0 - hp->lr_pu * hp->reg_pu)), perm,
                                    ck_pos, piece_beg, n_pieces, (T *)sums, xmask, err_col,
-                                   piece_item, join.words, join.role, join.epoch, rc);
+                                   piece_item, join.words, join.role, join.epoch, rc, ldc);
                 return check_launch("log_replay_kernel");
             }
         });

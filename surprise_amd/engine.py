@@ -185,6 +185,32 @@ def chain_schedule(users, row_ptr, n_chains, user_cost=16):
     return out.ravel()
 
 
+HOT_MIN_RATINGS = 1000  # hot_items(): rows with fewer ratings never bound the launch
+HOT_TRIGGER = 0.005     # ... replicas only if the top item holds >= this share of the ratings,
+HOT_SHARE = 0.0015      # ... then for every item holding >= this share
+HOT_MAX = 64
+
+
+def hot_items(items, n_items, n=None):
+    """Items whose q rows get a delta replica in the SVD++ helper-wave launch (sorted ids).
+    n = None: if the most-rated item holds >= HOT_TRIGGER of the ratings (and >=
+    HOT_MIN_RATINGS of them), every item holding >= HOT_SHARE (at most HOT_MAX, most-rated
+    first), else none; otherwise the n most-rated items.  Measured (tools/exp_hot_rows.sh): at
+    C3 (top item 0.57% of the ratings) 0 / 8 / 32 replicas give 0.608 / 0.575 / 0.567 ms per
+    epoch; on the C5 shard (top item 0.46%) replicas of its top items change nothing and the
+    replica reads cost 14% (99.9 -> 114 ms), so none there."""
+    cnt = np.bincount(np.asarray(items, np.int64), minlength=n_items)[:n_items]
+    order = np.argsort(-cnt, kind="stable")
+    if n is None:
+        tot = max(int(cnt.sum()), 1)
+        top = int(cnt.max()) if len(cnt) else 0
+        if top < max(HOT_MIN_RATINGS, HOT_TRIGGER * tot):
+            return order[:0]
+        n = min(HOT_MAX, int((cnt >= HOT_SHARE * tot).sum()))
+    n = max(0, min(int(n), int((cnt > 0).sum())))
+    return np.sort(order[:n])
+
+
 def ck_row0(row_ptr):
     """First packed checkpoint row of every user, (row_ptr[u] + u + 1) // 2 (the kernels'
     ck_row0): pair m of user u is row ck_row0[u] + m; the log holds ck_row0[n_users] rows."""
@@ -303,8 +329,9 @@ class MFEngine(ItemSync, Predictor):
     def __init__(self, csr, n_items, n_factors, *, algo="svd", hyper=None, biased=True,
                  dtype="float32", mode="log", n_chunks=1, deterministic=False,
                  user_order=None, n_waves=0, device=None, ld=None, world=1, merge=None,
-                 ckpt=True, heavy=None, err_in_row=True, events="native", join="event",
-                 helpers=True, ydefer=True, hx_chains_per_cu=None):
+                 ckpt=True, heavy=None, err_in_row=True, narrow=None, events="native",
+                 join="event",
+                 helpers=True, ydefer=True, hx_chains_per_cu=None, hot_rows=None):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -316,6 +343,9 @@ class MFEngine(ItemSync, Predictor):
                       stream (>= 1: that many users; < 1: those with >= heavy * the top degree;
                       0: no split; None: 128 on a full MI355X for small epochs)
           err_in_row  checkpoint log: each pair's errors in its row's padding (else elog)
+          narrow      checkpoint log: rows of the K factor columns only, errors in elog
+                      (MF_EPOCH_CKPT_NARROW); None = where that makes rows of whole 128-byte
+                      lines (K * size % 128 == 0, e.g. fp32 K=128: 512 vs 576 B per row)
           events      "native": the split's fork / join as HIP events bound to the kernels that
                       complete them (mf_launch_event); "torch": torch.cuda.Event record / wait
           join        "event": the main stream waits for the side stream's event; "kernel": the
@@ -324,7 +354,10 @@ class MFEngine(ItemSync, Predictor):
                       helper waves issue (MF_EPOCH_SVDPP_HELPERS)
           ydefer      SVD++ atomic mode: the users' y updates folded per item after the chunk
                       (mf_svdpp_y_fold) instead of float atomics at each user's end
-          hx_chains_per_cu  the helper-wave launch's user chains per CU (HX_CHAINS_PER_CU)"""
+          hx_chains_per_cu  the helper-wave launch's user chains per CU (HX_CHAINS_PER_CU)
+          hot_rows    the helper-wave launch: items whose q row gets a delta replica
+                      (mf_svdpp_epoch's hot rows): None = auto (hot_items()), 0 = none, n = the
+                      n most-rated items"""
         torch = _lib.require_gpu()
         self.torch = torch
         self.algo = algo
@@ -416,8 +449,17 @@ class MFEngine(ItemSync, Predictor):
         # checkpoint log with MF_EPOCH_ERR_IN_ROW where the row has room: each pair's two errors
         # ride in its checkpoint row's padding (the replay gathers no elog entries)
         e0 = ((self.K + 3) & ~1) if self.dtype == _lib.MF_F32 else self.K + 2
+        # ... unless narrow rows (the factor columns only, errors in elog) are whole cache lines
+        # where the padded rows are not: the replay reads each row twice (C4: 757 -> ~520 B per
+        # read), so a 4-byte error gather per rating costs less than the rows' extra line
+        lc = _lib.ckpt_narrow_ld(self.K, self.dtype)
+        if narrow is None:
+            narrow = lc * esz % 128 == 0 and lc < self.ldq
+        self.narrow = self.ckpt and bool(narrow) and lc < self.ldq
+        self.ldc = lc if self.narrow else self.ldq  # the checkpoint rows' stride
         # (read-only after construction: elog is sized for it)
-        self._err_in_row = self.ckpt and e0 + 2 <= self.ldq and bool(err_in_row)
+        self._err_in_row = (self.ckpt and not self.narrow and e0 + 2 <= self.ldq
+                            and bool(err_in_row))
         C = _lib.load().mf_ckpt_interval() if self.ckpt else 0
         _pu = []
         pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
@@ -496,6 +538,17 @@ class MFEngine(ItemSync, Predictor):
             for us in self.sched:
                 self.hx_sched.append(to_dev(chain_schedule(us.cpu().numpy(), row_ptr,
                                                            self.hx_chains)))
+        # ... and delta replicas of the most-rated items' rows (their serialised float atomics
+        # bound the launch otherwise)
+        hot = hot_items(items, self.n_items, hot_rows) if self.hx else np.zeros(0, np.int64)
+        if len(hot) and 3 * self.n_items * self.ldq * esz >= (1 << 32):
+            hot = hot[:0]  # (the replica rows must stay inside 32-bit buffer offsets)
+        self.hot_list = to_dev(hot.astype(np.int32)) if len(hot) else None
+        self.hot_flag = None
+        if len(hot):
+            flag = np.zeros(self.n_items, np.uint8)
+            flag[hot] = 1
+            self.hot_flag = to_dev(flag)
         self.ycsc = []
         if self.ydefer:
             for us in self.sched:
@@ -526,7 +579,10 @@ class MFEngine(ItemSync, Predictor):
         U, I, ld, ldq = self.n_users, self.n_items, self.ld, self.ldq
         z = lambda *shape: torch.zeros(*shape, dtype=self.tdt, device=dev)
         self.pu, self.bu = z(U, ld), z(U)
-        self.qb = z(I, ldq)
+        # (hot rows: the replica rows n_items .. 2 n_items - 1 of the same allocation, zero
+        # between chunks; self.qb is the model's table, rows 0 .. n_items - 1)
+        self._qb_alloc = z(2 * I if self.hot_list is not None else I, ldq)
+        self.qb = self._qb_alloc[:I]
         self.yj = z(I, ld) if algo == "svdpp" else None
         self.ycbuf = z(U, ld) if self.ydefer else None
         if self.ydefer:
@@ -545,7 +601,7 @@ class MFEngine(ItemSync, Predictor):
                 rows = int(ck_row0(row_ptr)[-1])
                 if rows >= (1 << 30):
                     raise _lib.SurpriseAMDError("checkpoint log too large for 32-bit positions")
-                self.qlog = z(max(rows, 1), ldq)
+                self.qlog = z(max(rows, 1), self.ldc)
                 self._qlog_base = self.qlog.data_ptr()
             else:  # the gradient log: the kernels index it by absolute CSR position k
                 self.qlog = z(max(k_hi - k_lo, 1), ldq)
@@ -663,7 +719,8 @@ class MFEngine(ItemSync, Predictor):
                       self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper),
                       self.mode, qlog, self._ptr(self.ycbuf) if self.ydefer else None,
                       n_waves, flags, self._ptr(self._hx_status) if self.hx else None,
-                      self.dtype, st)
+                      self._ptr(self.hot_flag) if self.hot_flag is not None and
+                      flags & _lib.MF_EPOCH_SVDPP_HELPERS else None, self.dtype, st)
 
     def run_chunk(self, c: int, events=None):
         """Run chunk c: the epoch kernel, preceded in "log" mode by the <pu^2> reduction of the
@@ -714,6 +771,9 @@ class MFEngine(ItemSync, Predictor):
         if self.hx:
             hs = self.hx_sched[c]
             self._epoch(hs, hs.numel(), self.hx_chains, _lib.MF_EPOCH_SVDPP_HELPERS, st)
+            if self.hot_list is not None:
+                _lib.call("mf_svdpp_hot_fold", self._ptr(self.qb), self.ldq, self.n_items,
+                          self._ptr(self.hot_list), self.hot_list.numel(), self.dtype, st)
         else:
             self._epoch(s, s.numel(), self.n_waves, 0, st, lx)
         if "end" in ev:
@@ -740,6 +800,7 @@ class MFEngine(ItemSync, Predictor):
                   self._ptr(self.user_sq), n_waves,
                   (_lib.MF_EPOCH_DUP_ITEMS if self.dup_items else 0) |
                   (_lib.MF_EPOCH_ERR_IN_ROW if self.err_in_row else 0) |
+                  (_lib.MF_EPOCH_CKPT_NARROW if self.narrow else 0) |
                   (xmask << _lib.MF_EPOCH_XCD_SHIFT), self.dtype, st)
 
     def _sq_reduce(self, out, st):
@@ -841,7 +902,8 @@ class MFEngine(ItemSync, Predictor):
                       self._ptr(lg["ck"]), self._ptr(lg["pb"]), lg["n_pieces"],
                       ctypes.c_void_p(sums_ptr), self._ptr(lg["pitem"]), rec,
                       (xmask << _lib.MF_EPOCH_XCD_SHIFT) |
-                      (_lib.MF_EPOCH_ERR_IN_ROW if self.err_in_row else 0), self.dtype, st)
+                      (_lib.MF_EPOCH_ERR_IN_ROW if self.err_in_row else 0) |
+                      (_lib.MF_EPOCH_CKPT_NARROW if self.narrow else 0), self.dtype, st)
         else:
             _lib.call("mf_log_reduce", ctypes.c_void_p(self._qlog_base), self.ldq, self.K + 1,
                       self._ptr(lg["perm"]), self._ptr(lg["pb"]), lg["n_pieces"],

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_without_device(lib):
-    assert lib.mf_version() == 920
+    assert lib.mf_version() == 930
     rc = lib.mf_item_affine(None, None, 10, 16, None, None, None, 0, 0, None)
     assert rc == 1001 and b"bad argument" in lib.mf_last_error()
     # argument validation happens before any device call
@@ -52,7 +52,7 @@ def test_version_and_error_without_device(lib):
     rc = lib.mf_log_reduce(1, 16, 11, 1, 1, 5, 1, None, None, ctypes.byref(rec), 0, None)
     assert rc == 1001 and b"recency weights need" in lib.mf_last_error()
     rc = lib.mf_svdpp_epoch(ctypes.byref(csr), None, 1, None, None, 16, None, 16, None, 10, None,
-                            1, None, None, 0, 0, None, 0, None)
+                            1, None, None, 0, 0, None, None, 0, None)
     assert rc == 1001 and b"null csr" in lib.mf_last_error()
     rc = lib.mf_sumsq(None, 4, 8, 4, None, 0, None)
     assert rc == 1001

@@ -197,6 +197,25 @@ def test_svdpp_atomic_alternatives_rmse_within_1e3(torch, golden, u1, opt):
     assert abs(_rmse(algo.test(test)) - case["rmse"]) < RMSE_TOL
 
 
+@pytest.mark.parametrize("dtype", ["float32", "float64"])
+def test_svdpp_hot_row_replicas_rmse_within_1e3(torch, golden, u1, dtype):
+    """Delta replicas of the 32 most-rated items' q rows (MFEngine hot_rows: half the chains'
+    atomics on a hot row go to its replica, every read sums both, mf_svdpp_hot_fold after each
+    chunk) hold the reference's RMSE like the default, and leave the replica rows zero."""
+    from surprise_amd import SVDpp
+    meta, _ = golden
+    case = meta["cases"]["svdpp_k20_e20"]
+    ts, test = u1
+    algo = SVDpp(**case["params"], mode="atomic", dtype=dtype)
+    algo._engine_options = {"hot_rows": 32}
+    algo.fit(ts)
+    eng = algo._engine
+    assert eng.hx and eng.hot_list is not None and eng.hot_list.numel() == 32
+    assert eng._qb_alloc.shape[0] == 2 * eng.n_items
+    assert float(eng._qb_alloc[eng.n_items:].abs().max()) == 0.0
+    assert abs(_rmse(algo.test(test)) - case["rmse"]) < RMSE_TOL
+
+
 def test_batched_test_equals_per_call_estimate(torch, u1):
     """The HIP predict kernel (batched test()) agrees with the reference-style estimate()."""
     from surprise_amd import SVD, SVDpp
@@ -489,6 +508,37 @@ def test_errors_in_checkpoint_rows_equal_elog(torch, u1, monkeypatch, K, dtype, 
         out.append(eng.get_factors())
     for k in ("pu", "qi", "bu", "bi"):
         np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
+
+
+@pytest.mark.parametrize("K,dtype,heavy,auto", [(128, "float32", 0.0, True),
+                                                 (64, "float32", 0.25, True),
+                                                 (48, "float64", 0.0, True),
+                                                 (21, "float32", 0.25, False),
+                                                 (20, "float64", 0.0, False)])
+def test_narrow_checkpoint_rows_match_padded_rows(torch, u1, K, dtype, heavy, auto):
+    """MF_EPOCH_CKPT_NARROW (checkpoint rows of the K factor columns only, errors in elog, the
+    bias column's gradient summed from the errors) against the padded rows: the same gradients,
+    the bias column summed in another order (fp64 within 1e-12, fp32 within 1e-5); auto: the
+    engine picks narrow rows by itself (rows of whole 128-byte lines)."""
+    from surprise_amd.engine import MFEngine
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
+                 reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    rng = np.random.RandomState(4)
+    pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
+    out = []
+    for narrow in (None if auto else True, False):
+        eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype=dtype,
+                       mode="log", heavy=heavy, narrow=narrow)
+        assert eng.ckpt and eng.narrow == (narrow is not False)
+        assert eng.qlog.shape[1] == (eng.ldc if eng.narrow else eng.ldq)
+        eng.set_factors(pu0, qi0)
+        eng.run_epochs(3)
+        out.append(eng.get_factors())
+    tol = 1e-12 if dtype == "float64" else 1e-5
+    for k in ("pu", "qi", "bu", "bi"):
+        np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=tol, err_msg=k)
 
 
 def test_user_sq_statistic_equals_sumsq(torch, u1):

@@ -315,3 +315,19 @@ def test_recency_positions_follow_user_order_within_items():
         sel = items[perm] == i
         assert np.array_equal(rp[sel], np.arange(sel.sum()))
         assert np.all(np.diff(perm[sel]) > 0)
+
+
+def test_hot_items_policy():
+    """engine.hot_items: the items whose SVD++ q rows get a delta replica."""
+    from surprise_amd.engine import hot_items, HOT_MAX
+    items = np.concatenate([np.full(2000, 7), np.full(700, 3), np.full(300, 5),
+                            np.arange(10000).repeat(30)])               # 303,000 ratings
+    np.testing.assert_array_equal(hot_items(items, 10000), [3, 7])    # top 0.67%: >= 0.15%
+    np.testing.assert_array_equal(hot_items(items, 10000, 3), [3, 5, 7])  # the 3 most rated
+    assert len(hot_items(items, 10000, 0)) == 0
+    assert len(hot_items(np.arange(50).repeat(20), 50)) == 0          # top item < 1000 ratings
+    flat = np.concatenate([np.full(1600, 0), np.arange(1, 1000).repeat(300)])  # top 0.53%
+    assert len(hot_items(flat, 1000)) == 1
+    assert len(hot_items(np.arange(300).repeat(1000)[::-1], 300)) == 0  # top 0.33%: none
+    many = np.concatenate([np.full(3000, 1), np.arange(2, 200).repeat(1000)])
+    assert len(hot_items(many, 200)) == HOT_MAX
