@@ -65,6 +65,9 @@ def parse():
     p.add_argument("--hot-rows", type=int, default=-1,
                    help="SVD++ helper-wave launch: q rows with a delta replica (-1: the engine's "
                         "policy, engine.hot_items)")
+    p.add_argument("--replay-rows", type=int, default=0,
+                   help="SVD checkpoint log: ratings per replay piece (0: the engine's policy, "
+                        "engine.replay_piece_rows)")
     p.add_argument("--hx-chains", type=int, default=0,
                    help="SVD++ helper-wave launch: user chains per CU (0: the engine default)")
     p.add_argument("--algo", default=None, choices=["svd", "svdpp"])
@@ -416,7 +419,8 @@ def main():
                        n_chunks=args.chunks or default_chunks(a, md, n_users_global),
                        **({"merge": args.merge} if args.merge else {}),
                        **({"hx_chains_per_cu": args.hx_chains} if args.hx_chains else {}),
-                       **({"hot_rows": args.hot_rows} if args.hot_rows >= 0 else {}))
+                       **({"hot_rows": args.hot_rows} if args.hot_rows >= 0 else {}),
+                       **({"replay_rows": args.replay_rows} if args.replay_rows else {}))
         eng.set_factors(pu, qi, yj=yj)
         eng._prepare(ctx)  # global per-item counts (all ranks)
         return eng

@@ -213,7 +213,9 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
  * q from the snapshot table qb; every rating of a piece has the same item) -- call it before
  * mf_log_apply.  piece_item (nullable): the item of each piece (else read through perm and the
  * CSR items).  Requires ldq * sizeof(dtype) <= 1 KiB.  flags: bits 8..15 an XCD mask as in
- * mf_svd_epoch (MF_EPOCH_XCD_SHIFT), 0 = every XCD; MF_EPOCH_ERR_IN_ROW: errors in the rows.
+ * mf_svd_epoch (MF_EPOCH_XCD_SHIFT), 0 = every XCD; MF_EPOCH_ERR_IN_ROW: errors in the rows;
+ * MF_EPOCH_CKPT_NARROW: narrow checkpoint rows.  Unlike mf_log_reduce, a piece may hold any
+ * number >= 1 of ratings (of one item): longer pieces mean fewer sums rows for mf_log_apply.
  * rec (nullable): each gradient err_k * p_k weighted by its recency weight (mf_recency_t).
  */
 int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_factors,

@@ -2134,8 +2134,10 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
 // load per piece, and the replay gathers nothing but the checkpoint rows (no item rows, no item
 // ids).  Summed per piece in perm order exactly like log_reduce_kernel; equal to the gradient
 // log's sums up to a rounding of the undone step (fp64: the delta-log oracle to 1e-9).
-// One wave per piece (<= 64 ratings): lane x holds rating x's checkpoint offset, parity, err
-// and weight (vector gathers once per piece).  Odd and even ratings are summed apart, so a
+// One wave per piece (any number of ratings of one item, 64 at a time: lane x holds rating x's
+// checkpoint offset, parity, err and weight, vector gathers once per 64).  Pieces longer than 64
+// shorten mf_log_apply's per-item chain of piece rows (C4's top item: ~1M ratings = 16k pieces
+// of 64).  Odd and even ratings are summed apart, so a
 // rating costs two v_readlane broadcasts, the row gather and 2 (packed) FMAs per element; the
 // undone step enters once per piece: sum_even w err_k p_k = iap o (sum_even w err p_{c+1} -
 // D sum_even w err^2).  Two groups of MF_REPLAY_U rows are in flight per wave.
@@ -2178,72 +2180,79 @@ __device__ __forceinline__ void log_replay_body(
     // err_k * 1 is summed from the per-lane errors
     const bool narrow = ldc < ldq;
     for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
-        const int beg = piece_beg[pc], cnt = piece_beg[pc + 1] - beg;  // 1 <= cnt <= 64
-        const int xl = beg + (lane < cnt ? lane : cnt - 1);
-        // lane x: rating x, its pair's (packed) checkpoint row and parity (ck_pos = 2 row + odd)
-        const int k_l = perm[xl], ck_l = ck_pos[xl];
-        const int c_l = ck_l >> 1, odd_l = ck_l & 1;  // odd 1: k = c + 1 (the row as stored)
-        // err_k per lane: from elog, or (err_col > 0) column err_col + odd of its checkpoint row
-        // (one gather per lane: the line is the row load's own); lanes >= cnt: 0, weight 0
-        const T ek_l = lane >= cnt ? T(0)
-                       : err_col > 0 ? ckpt[(int64_t)c_l * ldc + err_col + odd_l] : elog[k_l];
+        // a piece: >= 1 ratings of ONE item, taken 64 at a time (lane x: rating x of the
+        // sub-piece); the undone step's and the bias column's scalar sums accumulate per lane
+        const int pbeg = piece_beg[pc], pend = piece_beg[pc + 1];
         // the piece's item row (snapshot) -> D = lrp o q_i
         // (piece_item: the item id without the perm -> items hop on the piece's critical path)
-        const int item = piece_item ? piece_item[pc] : items[readlane(k_l, 0)];
+        const int item = piece_item ? piece_item[pc] : items[perm[pbeg]];
         const uint32_t qoff = (uint32_t)item * qrow;
-        // gradient weight per lane: err_k, times (REC) its recency weight wf for the factor
-        // columns; the bias column (p_k's column K is 1, so its gradient is err_k) gets
-        // sum err_k (wb - wf) added once per piece.
-        T ef_l = ek_l, dw_l = T(0);
-        if constexpr (REC) {
-            T wf_l, wb_l;
-            recency_weights(rc, l_q, l_b, item, xl, wf_l, wb_l);
-            ef_l = ek_l * wf_l;
-            dw_l = wb_l - wf_l;
-        }
-        // g_k = p_k for odd k, iap o (p_{c+1} - err_k D) for even: split by parity so a rating
-        // costs one FMA per element --  acc = sum_odd ef p + iap o (sum_even ef p - D sum_even ef ek)
-        const T eo_l = odd_l ? ef_l : T(0), ee_l = odd_l ? T(0) : ef_l;
         vec D[G];
 #pragma unroll
         for (int v = 0; v < G; ++v) D[v] = lrp[v] * L::template lds<0>(q_rs, cq[v], qoff);
         vec ao[G], ae[G];
 #pragma unroll
         for (int v = 0; v < G; ++v) ao[v] = ae[v] = L::splat(T(0));
-        auto load_grp = [&](const int x0, vec (&p)[kU][G]) {
-#pragma unroll
-            for (int y = 0; y < kU; ++y) {  // (x past cnt: lane cnt-1's rating, weight 0)
-                const int x = x0 + y < kWave ? x0 + y : kWave - 1;
-                const T *row = ckpt + (int64_t)readlane(c_l, x) * ldc;
-#pragma unroll
-                for (int v = 0; v < G; ++v) p[y][v] = *(const vec *)(row + cc[v]);
+        T se_l = T(0), sb_l = T(0);  // per lane: sum_even w err^2, the bias column's extra
+        for (int beg = pbeg; beg < pend; beg += kWave) {
+            const int cnt = pend - beg < kWave ? pend - beg : kWave;  // 1 <= cnt <= 64
+            const int xl = beg + (lane < cnt ? lane : cnt - 1);
+            // lane x: rating x, its pair's (packed) checkpoint row and parity (2 row + odd)
+            const int k_l = perm[xl], ck_l = ck_pos[xl];
+            const int c_l = ck_l >> 1, odd_l = ck_l & 1;  // odd 1: k = c + 1 (the row as stored)
+            // err_k per lane: from elog, or (err_col > 0) column err_col + odd of its checkpoint
+            // row (one gather per lane: the line is the row load's own); lanes >= cnt: 0
+            const T ek_l = lane >= cnt ? T(0)
+                           : err_col > 0 ? ckpt[(int64_t)c_l * ldc + err_col + odd_l] : elog[k_l];
+            // gradient weight per lane: err_k, times (REC) its recency weight wf for the factor
+            // columns; the bias column (p_k's column K is 1, so its gradient is err_k) gets
+            // sum err_k (wb - wf) added once per piece.
+            T ef_l = ek_l;
+            if constexpr (REC) {
+                T wf_l, wb_l;
+                recency_weights(rc, l_q, l_b, item, xl, wf_l, wb_l);
+                ef_l = ek_l * wf_l;
+                sb_l += ek_l * (wb_l - wf_l);
             }
-        };
-        auto comp_grp = [&](const int x0, vec (&p)[kU][G]) {
+            if (narrow) sb_l += ef_l;  // (the bias column read nothing: all of it here)
+            // g_k = p_k for odd k, iap o (p_{c+1} - err_k D) for even: split by parity so a
+            // rating costs one FMA per element --
+            // acc = sum_odd ef p + iap o (sum_even ef p - D sum_even ef ek)
+            const T eo_l = odd_l ? ef_l : T(0), ee_l = odd_l ? T(0) : ef_l;
+            se_l += ee_l * ek_l;
+            auto load_grp = [&](const int x0, vec (&p)[kU][G]) {
 #pragma unroll
-            for (int y = 0; y < kU; ++y) {
-                const int x = x0 + y < kWave ? x0 + y : kWave - 1;
-                const T wo = readlane(eo_l, x), we = readlane(ee_l, x);
+                for (int y = 0; y < kU; ++y) {  // (x past cnt: lane cnt-1's rating, weight 0)
+                    const int x = x0 + y < kWave ? x0 + y : kWave - 1;
+                    const T *row = ckpt + (int64_t)readlane(c_l, x) * ldc;
 #pragma unroll
-                for (int v = 0; v < G; ++v) {
-                    ao[v] += wo * p[y][v];
-                    ae[v] += we * p[y][v];
+                    for (int v = 0; v < G; ++v) p[y][v] = *(const vec *)(row + cc[v]);
                 }
+            };
+            auto comp_grp = [&](const int x0, vec (&p)[kU][G]) {
+#pragma unroll
+                for (int y = 0; y < kU; ++y) {
+                    const int x = x0 + y < kWave ? x0 + y : kWave - 1;
+                    const T wo = readlane(eo_l, x), we = readlane(ee_l, x);
+#pragma unroll
+                    for (int v = 0; v < G; ++v) {
+                        ao[v] += wo * p[y][v];
+                        ae[v] += we * p[y][v];
+                    }
+                }
+            };
+            vec pA[kU][G], pB[kU][G];
+            load_grp(0, pA);
+            for (int x0 = 0; x0 < cnt; x0 += 2 * kU) {
+                load_grp(x0 + kU, pB);
+                comp_grp(x0, pA);
+                if (x0 + kU >= cnt) break;
+                load_grp(x0 + 2 * kU, pA);
+                comp_grp(x0 + kU, pB);
             }
-        };
-        vec pA[kU][G], pB[kU][G];
-        load_grp(0, pA);
-        for (int x0 = 0; x0 < cnt; x0 += 2 * kU) {
-            load_grp(x0 + kU, pB);
-            comp_grp(x0, pA);
-            if (x0 + kU >= cnt) break;
-            load_grp(x0 + 2 * kU, pA);
-            comp_grp(x0 + kU, pB);
         }
-        const T se = wave_sum_u(ee_l * ek_l);
-        T sb = T(0);
-        if constexpr (REC) sb = wave_sum_u(ek_l * dw_l);
-        if (narrow) sb += wave_sum_u(ef_l);  // (the bias column read nothing: all of it here)
+        const T se = wave_sum_u(se_l);
+        const T sb = REC || narrow ? wave_sum_u(sb_l) : T(0);
         vec acc[G];
 #pragma unroll
         for (int v = 0; v < G; ++v) {

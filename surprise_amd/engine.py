@@ -133,6 +133,23 @@ def item_positions(row_ptr, items, users, n_items):
     return ks, pos
 
 
+REPLAY_PIECES_PER_WAVE = 8  # replay_piece_rows(): pieces per replay wave kept at least
+
+
+REPLAY_MAX_ROWS = 256  # measured at C4 (ms/epoch): 64 35.0, 256 33.3, 1024 35.0
+
+
+def replay_piece_rows(row_ptr, users, waves=4096):
+    """Ratings per piece of the checkpoint replay (a multiple of 64, up to REPLAY_MAX_ROWS): long
+    pieces cut mf_log_apply's chain of piece rows on a popular item (C4: the top item's ~1M
+    ratings were 16k pieces of 64, summed by one wave: fold 1.47 -> 0.46 ms), as long as every
+    replay wave (~waves) still gets REPLAY_PIECES_PER_WAVE pieces of 64-rating sub-pieces."""
+    deg = np.diff(np.asarray(row_ptr, np.int64))
+    nnz = int(deg[np.asarray(users, np.int64)].sum()) if len(users) else 0
+    m = nnz // (PIECE_ROWS * waves * REPLAY_PIECES_PER_WAVE)
+    return PIECE_ROWS * int(max(1, min(REPLAY_MAX_ROWS // PIECE_ROWS, m)))
+
+
 def piece_bounds(offs, counts, piece_rows=PIECE_ROWS):
     """Item i's rows [offs[i], offs[i] + counts[i]) cut into pieces of <= piece_rows:
     (item_piece_ptr int32[n_items+1], piece_beg int64[n_pieces+1], the last = offs[-1])."""
@@ -331,7 +348,8 @@ class MFEngine(ItemSync, Predictor):
                  user_order=None, n_waves=0, device=None, ld=None, world=1, merge=None,
                  ckpt=True, heavy=None, err_in_row=True, narrow=None, events="native",
                  join="event",
-                 helpers=True, ydefer=True, hx_chains_per_cu=None, hot_rows=None):
+                 helpers=True, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
+                 replay_rows=None):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -355,6 +373,7 @@ class MFEngine(ItemSync, Predictor):
           ydefer      SVD++ atomic mode: the users' y updates folded per item after the chunk
                       (mf_svdpp_y_fold) instead of float atomics at each user's end
           hx_chains_per_cu  the helper-wave launch's user chains per CU (HX_CHAINS_PER_CU)
+          replay_rows checkpoint log: ratings per replay piece (None: replay_piece_rows())
           hot_rows    the helper-wave launch: items whose q row gets a delta replica
                       (mf_svdpp_epoch's hot rows): None = auto (hot_items()), 0 = none, n = the
                       n most-rated items"""
@@ -500,7 +519,11 @@ class MFEngine(ItemSync, Predictor):
                 kpos[ks] = pos
             lgs = []
             for us in parts:
-                perm, pb, ipp, cnt = log_layout(row_ptr, items, us, self.n_items)
+                rows = PIECE_ROWS
+                if self.ckpt:
+                    rows = replay_piece_rows(row_ptr, us) if replay_rows is None else \
+                        max(1, int(replay_rows))
+                perm, pb, ipp, cnt = log_layout(row_ptr, items, us, self.n_items, rows)
                 lg = dict(sched=to_dev(us), perm=to_dev(perm), pb=to_dev(pb), ipp=to_dev(ipp),
                           n_pieces=len(pb) - 1, cnt=cnt)
                 if self.ckpt:

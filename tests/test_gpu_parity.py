@@ -541,6 +541,40 @@ def test_narrow_checkpoint_rows_match_padded_rows(torch, u1, K, dtype, heavy, au
         np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=tol, err_msg=k)
 
 
+@pytest.mark.parametrize("rows,dtype,narrow,heavy", [(256, "float64", False, 0.0),
+                                                     (1024, "float32", True, 0.0),
+                                                     (128, "float32", False, 0.25)])
+def test_long_replay_pieces_match_64_rating_pieces(torch, ml1m, monkeypatch, rows, dtype, narrow,
+                                                    heavy):
+    """mf_log_replay over pieces longer than 64 ratings (taken 64 at a time; engine
+    replay_piece_rows, long at C4's size) against the default 64-rating pieces on the ML-1M
+    shape: the same gradients summed in another grouping (fp64 within 1e-11, fp32 within
+    1e-5)."""
+    import surprise_amd.engine as E
+    ts, _ = ml1m
+    row_ptr, items, ratings = ts.csr()
+    K = 32
+    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
+                 reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    rng = np.random.RandomState(5)
+    pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
+    out = []
+    for r in (rows, 64):
+        monkeypatch.setattr(E, "replay_piece_rows", lambda row_ptr, users, r=r: r)
+        eng = E.MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype=dtype,
+                         mode="log", heavy=heavy, narrow=narrow, n_chunks=2)
+        assert eng.ckpt and eng.narrow == narrow
+        groups = [g for lg in eng.logs for g in (lg, lg["heavy"]) if g is not None]
+        longest = max(int(np.diff(g["pb"].cpu().numpy()).max()) for g in groups)
+        assert (longest > 64) == (r > 64)
+        eng.set_factors(pu0, qi0)
+        eng.run_epochs(2)
+        out.append(eng.get_factors())
+    tol = 1e-11 if dtype == "float64" else 1e-5
+    for k in ("pu", "qi", "bu", "bi"):
+        np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=tol, err_msg=k)
+
+
 def test_user_sq_statistic_equals_sumsq(torch, u1):
     """<pu^2> for the next chunk, summed from the epoch kernel's per-user |p_u|^2 inside
     mf_log_apply, equals mf_sumsq over the updated pu (fp64, up to summation order)."""

@@ -331,3 +331,11 @@ def test_hot_items_policy():
     assert len(hot_items(np.arange(300).repeat(1000)[::-1], 300)) == 0  # top 0.33%: none
     many = np.concatenate([np.full(3000, 1), np.arange(2, 200).repeat(1000)])
     assert len(hot_items(many, 200)) == HOT_MAX
+
+
+def test_replay_piece_rows_policy():
+    """engine.replay_piece_rows: 64 at ML-1M size, REPLAY_MAX_ROWS at C4's."""
+    from surprise_amd.engine import replay_piece_rows, REPLAY_MAX_ROWS
+    assert replay_piece_rows(np.array([0, 800_000]), np.array([0])) == 64
+    assert replay_piece_rows(np.array([0, 99_000_000]), np.array([0])) == REPLAY_MAX_ROWS
+    assert replay_piece_rows(np.array([0, 10]), np.array([], np.int64)) == 64
