@@ -238,7 +238,7 @@ def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
         for c in range(eng.n_chunks):
             ev = {k: torch.cuda.Event(enable_timing=True)
                   for k in ("begin", "start", "end", "end_h", "end_r", "done", "ar_begin",
-                            "ar_end")}
+                            "ar_end", "l_start", "l_end")}
             ev["begin"].record(eng.stream)
             eng.run_chunk(c, events=ev)
             if multi:  # (the collective of the chunk's exchange, bracketed on the stream)
@@ -246,6 +246,7 @@ def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
             eng.sync_items(ctx)
             eng._sync_events = None
             ev["done"].record(eng.stream)
+            ev["chunk"] = c
             recs.append(ev)
     torch.cuda.synchronize()
     phases = {"host_enqueue_ms": t_enq / max(steps, 1) * 1e3}
@@ -255,6 +256,20 @@ def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
         phases.update({"pre_ms": span("begin", "start") * n, "epoch_kernel_ms": span("start", "end") * n,
                   "replay_ms": span("end", "end_r") * n, "fold_sync_ms": span("end_r", "done") * n,
                   "step_gpu_ms": span("begin", "done") * n, "instrumented_steps": len(recs) // n})
+        # the epoch kernel's launches (the dominant kernel): each one's span on its own stream
+        # and the ratings it trains -- roofline_of's per-launch figures
+        launches = []
+        for e in recs:
+            n_r = eng.epoch_launch_ratings(e["chunk"])
+            spans = [e["start"].elapsed_time(e["end"])]
+            if len(n_r) > 1:
+                spans.append(e["l_start"].elapsed_time(e["l_end"]))
+            launches += list(zip(spans, n_r))
+        phases["epoch_launches"] = {"per_step": len(launches) / max(len(recs) // n, 1),
+                                    "avg_us": float(np.mean([t for t, _ in launches])) * 1e3,
+                                    "avg_ratings": float(np.mean([r for _, r in launches])),
+                                    "ms_and_ratings": [[round(t, 4), r] for t, r in
+                                                       launches[:2 * n]]}
         if multi:  # the exchange: one SUM all-reduce per chunk (ms per chunk and per step)
             ar = span("ar_begin", "ar_end")
             phases.update({"allreduce_ms_per_chunk": ar, "allreduce_ms": ar * n,
@@ -368,13 +383,33 @@ def cpu_baselines(csr, n_items, K, n_train):
 
 
 # ---------------------------------------------------------------------------- main
-def roofline_of(algo, K, dtype, n_train, ms_step, shape):
-    """SURVEY 8(d) algorithmic bytes of a step / the step time, against the HBM peak."""
+def roofline_of(algo, K, dtype, n_train, ms_step, shape, phases=None):
+    """The dominant kernel's roofline: SURVEY 8(d) algorithmic bytes per launch (the ratings the
+    epoch-kernel launch trains x B per update) / its average launch duration (HIP events on the
+    stream it runs on, the instrumented epochs after the timed region), against the HBM peak;
+    beside it the whole step's (algorithmic bytes of a step / the step time).  traffic = the
+    measured HBM-side bytes per launch of that kernel (PMC, profiles/traffic_*)."""
     B = algorithmic_bytes_per_update(algo, K, ELEM_BYTES[dtype])
-    achieved = B * n_train / (ms_step * 1e-3) / 1e9
+    step_achieved = B * n_train / (ms_step * 1e-3) / 1e9
     traffic, tinfo = traffic_for(algo, K, shape, dtype)
+    el = (phases or {}).get("epoch_launches")
+    kname = "mf_svdpp_hx_kernel" if algo == "svdpp" else "mf_ckpt_epoch_kernel"
+    if el:
+        achieved = B * el["avg_ratings"] / (el["avg_us"] * 1e-6) / 1e9
+        per_launch = None
+        if tinfo and kname in (tinfo.get("per_kernel") or {}):
+            pk = tinfo["per_kernel"][kname]
+            per_launch = pk["bytes_per_step"] / max(pk["dispatches_per_step"], 1e-9)
+        dom = {"kernel": kname, "launches_per_step": el["per_step"],
+               "avg_launch_us": el["avg_us"], "algorithmic_bytes_per_launch": B * el["avg_ratings"],
+               "traffic_per_launch": per_launch}
+    else:
+        achieved, dom = step_achieved, None
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": (dom or {}).get("traffic_per_launch") if dom else traffic,
+            "dominant_kernel": dom, "step_achieved": step_achieved,
+            "step_frac": step_achieved / HBM_PEAK_GBS, "step_traffic": traffic,
             "algorithmic_bytes_per_update": B, "updates_per_step": n_train,
             "algorithmic_bytes_per_step": B * n_train,
             "traffic_breakdown": tinfo.get("per_kernel") if tinfo else None,
@@ -464,18 +499,21 @@ def main():
         "per_gpu_value": value / world,
         "device_bytes_per_rank_max": dev_bytes,
     }
-    rl = roofline_of(algo, K, args.dtype, n_train, ms_step, args.shape)
+    rl = roofline_of(algo, K, args.dtype, n_train, ms_step, args.shape, phases)
     rl.update({
-        "kernel": "one epoch step (%s): %s" % (
-            mode, "mf_ckpt_epoch_kernel (heavy + light users) + log_replay_kernel (both groups) "
-                  "+ log_apply_kernel" if mode == "log"
-            else "mf_epoch_kernel + y fold (+ merge)"),
+        "kernel": "dominant: the epoch kernel's launches (%s); step (%s): %s" % (
+            (rl["dominant_kernel"] or {}).get("kernel"), mode,
+            "mf_ckpt_epoch_kernel (heavy + light users) + log_replay_kernel (both groups) "
+            "+ log_apply_kernel" if mode == "log" else "mf_svdpp_hx_kernel + y fold (+ merge)"),
         "phases_gpu_ms": phases,
-        "note": "achieved = algorithmic bytes of a step (SURVEY 8(d): a gather + scatter of the "
-                "user and item rows per rating, s = %d bytes per element) / the measured step "
-                "time. ML-1M's tables are L2/MALL-resident: the HBM-side bytes (`traffic`: every "
-                "kernel's 2 x FETCH_SIZE + WRITE_SIZE per step, PMC) are mostly the checkpoint "
-                "log written and re-read, and the step is bound by the heaviest user's "
+        "note": "achieved = algorithmic bytes per launch of the dominant kernel (SURVEY 8(d): a "
+                "gather + scatter of the user and item rows per rating, s = %d bytes per "
+                "element, x the ratings the launch trains) / its average launch duration (HIP "
+                "events on its own stream); step_achieved = the same over the whole step. "
+                "traffic = that kernel's measured HBM-side bytes per launch (2 x FETCH_SIZE + "
+                "WRITE_SIZE, PMC), step_traffic = every kernel's per step. Where the tables are "
+                "L2/MALL-resident (ML-1M: 3 MB item table) the algorithmic bytes exceed what HBM "
+                "moves and frac can pass 1: the launch is bound by the heaviest user's "
                 "sequential chain (1805 ratings), not by HBM" % ELEM_BYTES[args.dtype]})
     result["roofline"] = rl
 
@@ -501,7 +539,7 @@ def main():
         del e32
         ms2 = el2 / args.steps * 1e3
         leg = {"dtype": other, "value": n_train * args.steps / el2, "ms_per_step": ms2,
-               "roofline": roofline_of(algo, K, other, n_train, ms2, args.shape)}
+               "roofline": roofline_of(algo, K, other, n_train, ms2, args.shape, ph)}
         leg["roofline"]["phases_gpu_ms"] = ph
         if not args.no_rmse:
             leg["rmse"] = rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world,
@@ -517,7 +555,7 @@ def main():
             n2 = max(10, args.steps // 2)
             e2, ph2 = run_steps(pp, None, n2, 2, torch)
             del pp
-            rl2 = roofline_of("svdpp", 100, dt, n_train, e2 / n2 * 1e3, args.shape)
+            rl2 = roofline_of("svdpp", 100, dt, n_train, e2 / n2 * 1e3, args.shape, ph2)
             rl2["phases_gpu_ms"] = ph2
             pp_legs[dt] = {"value": n_train * n2 / e2, "unit": "rating-updates/s", "steps": n2,
                            "ms_per_step": e2 / n2 * 1e3, "roofline": rl2}

@@ -643,6 +643,13 @@ class MFEngine(ItemSync, Predictor):
         if not self.biased:
             self._hyper.global_mean = 0.0
 
+    def epoch_launch_ratings(self, c):
+        """Ratings each epoch-kernel launch of chunk c trains, in launch order (checkpoint log,
+        split chunk: the heavy users' launch, then the light users'; else one launch)."""
+        if self.ckpt and self.logs[c]["heavy"] is not None:
+            return [int(self.logs[c]["heavy"]["perm"].numel()), int(self.logs[c]["perm"].numel())]
+        return [int(self._totals_local[c].sum())]
+
     @property
     def err_in_row(self):
         """Checkpoint log with each pair's errors in its row's padding (MF_EPOCH_ERR_IN_ROW)."""
@@ -753,7 +760,9 @@ class MFEngine(ItemSync, Predictor):
         runs its heavy users' epoch + replay on the side stream beside the rest, joined before
         returning.  events: optional dict of torch.cuda.Event: "start" (main stream, before the
         epoch kernels), "end" (after the main epoch kernel), "end_h" (after the heavy one),
-        "end_r" (after the log replay / reduce / y fold that follow the epoch kernel)."""
+        "end_r" (after the log replay / reduce / y fold that follow the epoch kernel);
+        checkpoint log, split chunk: "l_start" / "l_end" around the light users' epoch kernel
+        on the side stream."""
         torch = self.torch
         s = self.sched[c]
         st = self._st()
@@ -883,7 +892,11 @@ class MFEngine(ItemSync, Predictor):
             self._epoch_sq(hv["sched"], n_h, n_h, st, self.heavy_xcd)
             if "end" in ev:
                 ev["end"].record(self.stream)
+            if "l_start" in ev:  # (the light epoch kernel's own span, on its stream)
+                ev["l_start"].record(side)
             self._epoch_sq(ls, ln, lw, sh, lx)
+            if "l_end" in ev:
+                ev["l_end"].record(side)
             jw = self._join_words
             if jw is not None:
                 self._join_epoch = (self._join_epoch + 1) & 0xFFFFFFFF

@@ -149,5 +149,7 @@ def test_bench_two_ranks_spawned(torch):
     assert len(lines) == 1, p.stdout[-2000:]
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["scaling"] == "weak"
-    assert r["value"] > 0 and r["roofline"]["frac"] <= 1.0
+    assert r["value"] > 0 and r["roofline"]["frac"] > 0
+    assert r["roofline"]["dominant_kernel"]["kernel"] == "mf_ckpt_epoch_kernel"
+    assert r["roofline"]["phases_gpu_ms"]["allreduce_ms_per_chunk"] > 0
     assert r["rmse"]["gpu"] < r["rmse"]["global_mean_baseline"]
