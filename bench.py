@@ -685,20 +685,26 @@ def predict_leg(csr, test, n_items, gm, torch):
     out = {"held_out": len(testset), "reference_us_per_prediction": 6.6,
            "reference_note": "SVD: AlgoBase.predict per rating (SURVEY 3.2, measured in the "
                              "build container); SVD++ re-sums y_j over I_u per call"}
+    from surprise_amd.dataset import RatingColumns
+    columns = RatingColumns(np.asarray(tu), np.asarray(ti), np.asarray(tr, np.float64))
     for name, klass, k in (("svd", SVD, 100), ("svdpp", SVDpp, 100)):
         algo = klass(n_factors=k, n_epochs=20, random_state=0).fit(ts)
         leg = {"dtype": algo.dtype}
-        for fn in ("test", "test_metrics"):
-            getattr(algo, fn)(testset[:1000])  # warm (device tables, implicit term)
+        # test(): a list of Predictions (the reference's return type); test_metrics(): (rmse,
+        # mae) from the device; *_columns: the same on a column-native testset (RatingColumns:
+        # no Python object per rating on the way in)
+        for key, fn, data in (("test", "test", testset), ("test_metrics", "test_metrics", testset),
+                              ("test_metrics_columns", "test_metrics", columns)):
+            getattr(algo, fn)(data[:1000])  # warm (device tables, implicit term)
             t0 = time.perf_counter()
             reps = 3
             for _ in range(reps):
-                r = getattr(algo, fn)(testset)
+                r = getattr(algo, fn)(data)
             dt = (time.perf_counter() - t0) / reps
-            leg[fn] = {"seconds": dt, "predictions_per_s": len(testset) / dt,
-                       "us_per_prediction": dt / len(testset) * 1e6}
+            leg[key] = {"seconds": dt, "predictions_per_s": len(testset) / dt,
+                        "us_per_prediction": dt / len(testset) * 1e6}
             if fn == "test_metrics":
-                leg[fn]["rmse"] = r[0]
+                leg[key]["rmse"] = r[0]
         leg["speedup_vs_reference_test"] = 6.6 / leg["test"]["us_per_prediction"]
         out[name] = leg
         del algo

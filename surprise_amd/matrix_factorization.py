@@ -29,6 +29,8 @@ The fork's per-fit side effects in SVD.fit (:158-169: a print and an unused
 """
 from __future__ import annotations
 
+import operator
+
 import numpy as np
 
 from . import _lib
@@ -192,14 +194,22 @@ class _MFBase(AlgoBase):
         return self._engine
 
     def _columns(self, testset):
-        """(raw uids, raw iids, r_ui_trans) columns of a testset (list of triples or array)."""
+        """(raw uids, raw iids, r_ui_trans) columns of a testset: a list of triples (ids as
+        lists), or column-native -- a RatingColumns or a structured array with uid / iid /
+        rating fields (ids as arrays, no Python objects per rating)."""
+        from .dataset import RatingColumns
+        if isinstance(testset, RatingColumns):
+            return testset.uid, testset.iid, np.asarray(testset.rating, np.float64)
+        if isinstance(testset, np.ndarray) and testset.dtype.names:
+            return (testset["uid"], testset["iid"], np.asarray(testset["rating"], np.float64))
         if isinstance(testset, np.ndarray):
             testset = testset.tolist()
         rows = testset if isinstance(testset, list) else list(testset)
         if not rows:
             return [], [], np.zeros(0)
-        ru, ri, r = zip(*rows)
-        return list(ru), list(ri), np.asarray(r, np.float64)
+        g = operator.itemgetter
+        return (list(map(g(0), rows)), list(map(g(1), rows)),
+                np.fromiter(map(g(2), rows), np.float64, len(rows)))
 
     def _inner_columns(self, ruids, riids):
         """Vectorised raw -> inner id mapping (-1 = unknown, the 'UKN__' case of
@@ -226,6 +236,8 @@ class _MFBase(AlgoBase):
         est = np.fmax(lo, np.fmin(hi, est))  # algo_base.py:166-169 (NaN -> upper bound)
         reason = "User and item are unkown."
         ok, bad = {"was_impossible": False}, {"was_impossible": True, "reason": reason}
+        if isinstance(ruids, np.ndarray):  # (column-native testset: Python scalars, as listed)
+            ruids, riids = ruids.tolist(), riids.tolist()
         return [Prediction(a, b, c, e, dict(bad) if x else dict(ok))
                 for a, b, c, e, x in zip(ruids, riids, (r - ts.offset).tolist(), est.tolist(),
                                          impossible.tolist())]
@@ -268,7 +280,7 @@ def _map_ids(raw, mapping):
         return np.array([mapping[x] if x in mapping else -1 for x in raw], np.int32)
     import pandas as pd
     m = pd.Series(mapping, dtype="int64") if len(mapping) else pd.Series([], dtype="int64")
-    idx = m.index.get_indexer(pd.Index(list(raw)))
+    idx = m.index.get_indexer(pd.Index(raw if isinstance(raw, np.ndarray) else list(raw)))
     out = np.full(len(idx), -1, np.int32)
     hit = idx >= 0
     out[hit] = m.to_numpy()[idx[hit]]

@@ -665,3 +665,9 @@ def test_test_metrics_equal_reference_pipeline(torch, u1):
         fast = algo.test(test)
         assert [p.details for p in fast] == [p.details for p in slow]
         np.testing.assert_allclose([p.est for p in fast], [p.est for p in slow], atol=1e-12)
+        # the column-native testset (RatingColumns: id arrays, no tuple per rating): the same
+        from surprise_amd.dataset import RatingColumns
+        ru, ri, rr = zip(*test)
+        cols = RatingColumns(np.array(ru, dtype=object), np.array(ri, dtype=object), rr)
+        assert algo.test_metrics(cols) == (rmse, mae)
+        assert [p.est for p in algo.test(cols)] == [p.est for p in fast]

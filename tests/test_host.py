@@ -339,3 +339,19 @@ def test_replay_piece_rows_policy():
     assert replay_piece_rows(np.array([0, 800_000]), np.array([0])) == 64
     assert replay_piece_rows(np.array([0, 99_000_000]), np.array([0])) == REPLAY_MAX_ROWS
     assert replay_piece_rows(np.array([0, 10]), np.array([], np.int64)) == 64
+
+
+def test_testset_columns_list_and_column_native():
+    """_MFBase._columns: a list of triples and the column-native forms give the same columns."""
+    from surprise_amd import SVD
+    from surprise_amd.dataset import RatingColumns
+    rows = [(1, 10, 4.0), (2, 20, 3.5), (7, 10, 1.0)]
+    a = SVD()
+    ru, ri, r = a._columns(rows)
+    assert ru == [1, 2, 7] and ri == [10, 20, 10] and r.tolist() == [4.0, 3.5, 1.0]
+    cu, ci, cr = a._columns(RatingColumns([1, 2, 7], [10, 20, 10], [4.0, 3.5, 1.0]))
+    assert cu.tolist() == ru and ci.tolist() == ri and cr.tolist() == r.tolist()
+    st = np.array(rows, dtype=[("uid", "i8"), ("iid", "i8"), ("rating", "f8")])
+    su, si, sr = a._columns(st)
+    assert su.tolist() == ru and si.tolist() == ri and sr.tolist() == r.tolist()
+    assert a._columns([])[2].shape == (0,)
