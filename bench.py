@@ -1,8 +1,9 @@
 """Benchmark: rating-updates/sec of the SVD / SVD++ SGD hot path on MI355X.
 
-Default (N=1): BASELINE configs[1] -- SVD n_factors=100, fp32 on the device, synthetic planted
-ML-1M shape (6040 users x 3706 items x 1,000,209 ratings, surprise_amd.synthetic), KFold(5,
-random_state=0) fold 0 -> 800,167 training ratings.  One "step" = one epoch over them.
+Default (N=1): BASELINE configs[1] -- SVD n_factors=100 on the synthetic planted ML-1M shape
+(6040 users x 3706 items x 1,000,209 ratings, surprise_amd.synthetic), KFold(5, random_state=0)
+fold 0 -> 800,167 training ratings; one "step" = one epoch over them.  The headline computes in
+fp64 (the reference's arithmetic, mf.pyx:207-227); an fp32 leg rides beside it (`f32_leg`).
 
 --gpus N (one process per GPU; spawned here when WORLD_SIZE is unset, or launched by
 torch.distributed.run): every rank holds ONLY its own user rows on its device.
@@ -10,20 +11,32 @@ torch.distributed.run): every rank holds ONLY its own user rows on its device.
                            is the single-GPU dataset above; every population is ML-1M-shaped and
                            rates the same 3706 items, synthetic.population) -- per-GPU work fixed
   --shape c4 | c5          strong scaling: BASELINE configs[3] / [4] (2M x 200k x 100M, SVD
-                           K=128 / 10M x 1M x 1B, SVD++ K=128; 1% held out), sharded by user
-                           range; each rank generates only its own rows (synthetic.sharded_rows)
+                           K=128 / 10M x 1M x 1B, SVD++ K=128; 1% held out, fp32), sharded by
+                           user range; each rank generates only its own rows
 Item-side updates are SUM-all-reduced once per epoch-chunk (RCCL; `--backend gloo` only to
-rehearse several ranks on one GPU).
+rehearse several ranks on one GPU).  The BASELINE scaling configs:
+  C4 on 4 GPUs:  python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+                   --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 4 --shape c4
+                 ~25M ratings and 500k users per rank, ~7.5 GB of device memory per rank; one
+                 115 MB all-reduce per epoch (the per-item log sums, 200k x 144 fp32)
+  C5 on 8 GPUs:  python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+                   --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8 --shape c5
+                 1.25M users / ~123M ratings per rank (the C5 shard: 5.2 GB measured on one
+                 GPU, ~7.4 GB with the merge's snapshots and exchange buffer); 16 epoch-chunks,
+                 each ONE 1.09 GB all-reduce (q deltas 1M x 144 + y maps 1M x 128, fp32)
 
 Prints ONE JSON line on rank 0 with the contract fields plus:
-  roofline      algorithmic bytes of a step (SURVEY 8(d) per-update figure x updates per GPU) /
-                the measured step time (<= 1 by construction), the per-kernel GPU time of a step
-                from HIP events on the engine's stream, and `traffic`: HBM bytes per step summed
-                over every kernel (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_*.json)
-  cpu_baseline  the fp64 C restatement of the reference loop (oracle/): all host cores (one
-                pinned process per core) and one pinned core, host model and core count
-  rmse          held-out RMSE of a full 20-epoch fit vs the fp64 sequential oracle (N=1, SVD)
-  svdpp_c3      BASELINE configs[2]: SVD++ K=100 epochs timed on the same fold (N=1 default)
+  roofline      the dominant kernel's (the epoch kernel's launches): SURVEY 8(d) algorithmic
+                bytes per launch / its average launch duration (HIP events on the stream it runs
+                on), `traffic` its measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE,
+                profiles/traffic_*.json); the whole step's figures beside it (step_*), and the
+                per-phase GPU time of a step (phases_gpu_ms; N>1: the all-reduce per chunk)
+  cpu_baseline  the fp64 C restatement of the reference loop (oracle/): 16 pinned processes (the
+                box's CPU share) and one pinned core; the node's all-core figure is derived
+  rmse          held-out RMSE of a full 20-epoch fit vs the fp64 sequential oracle (N=1; c4 / c5
+                against the committed oracle values, tests/golden/scale_golden.json)
+  svdpp_c3      BASELINE configs[2]: SVD++ K=100 epochs on the same fold (fp64 + fp32 legs)
+  predict       test() / test_metrics() predictions/s of fitted SVD / SVD++
 """
 import argparse
 import json
