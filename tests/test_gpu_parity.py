@@ -180,11 +180,13 @@ def test_svdpp_parallel_rmse_within_1e3(torch, golden, u1, name, mode):
     assert abs(_rmse(algo.test(test)) - case["rmse"]) < RMSE_TOL
 
 
-@pytest.mark.parametrize("opt", [{"helpers": False}, {"ydefer": False}])
+@pytest.mark.parametrize("opt", [{"helpers": False}, {"ydefer": False},
+                                 {"hx_chains_per_cu": 1}])
 def test_svdpp_atomic_alternatives_rmse_within_1e3(torch, golden, u1, opt):
     """SVD++'s non-default atomic-mode paths (MFEngine helpers=False: the chain wave issues its
-    own q atomics; ydefer=False: y_j updated by float atomics at each user's end) within 1e-3
-    of the reference's held-out RMSE, like the default."""
+    own q atomics; ydefer=False: y_j updated by float atomics at each user's end;
+    hx_chains_per_cu=1: one helper-wave chain per CU) within 1e-3 of the reference's held-out
+    RMSE, like the default."""
     from surprise_amd import SVDpp
     meta, _ = golden
     case = meta["cases"]["svdpp_k20_e20"]
@@ -193,7 +195,8 @@ def test_svdpp_atomic_alternatives_rmse_within_1e3(torch, golden, u1, opt):
     algo._engine_options = opt
     algo.fit(ts)
     eng = algo._engine
-    assert (eng.hx, eng.ydefer) == ((False, True) if "helpers" in opt else (False, False))
+    want = {"helpers": (False, True), "ydefer": (False, False), "hx_chains_per_cu": (True, True)}
+    assert (eng.hx, eng.ydefer) == want[next(iter(opt))]
     assert abs(_rmse(algo.test(test)) - case["rmse"]) < RMSE_TOL
 
 
