@@ -473,8 +473,8 @@ class MFEngine(ItemSync, Predictor):
         # read), so a 4-byte error gather per rating costs less than the rows' extra line
         lc = _lib.ckpt_narrow_ld(self.K, self.dtype)
         if narrow is None:
-            narrow = lc * esz % 128 == 0 and lc < self.ldq
-        self.narrow = self.ckpt and bool(narrow) and lc < self.ldq
+            narrow = lc * esz % 128 == 0
+        self.narrow = self.ckpt and bool(narrow) and 0 < lc < self.ldq
         self.ldc = lc if self.narrow else self.ldq  # the checkpoint rows' stride
         # (read-only after construction: elog is sized for it)
         self._err_in_row = (self.ckpt and not self.narrow and e0 + 2 <= self.ldq
