@@ -672,5 +672,5 @@ def test_test_metrics_equal_reference_pipeline(torch, u1):
         from surprise_amd.dataset import RatingColumns
         ru, ri, rr = zip(*test)
         cols = RatingColumns(np.array(ru, dtype=object), np.array(ri, dtype=object), rr)
-        assert algo.test_metrics(cols) == (rmse, mae)
+        np.testing.assert_allclose(algo.test_metrics(cols), (rmse, mae), rtol=0, atol=1e-12)
         assert [p.est for p in algo.test(cols)] == [p.est for p in fast]
