@@ -597,6 +597,9 @@ class MFEngine(ItemSync, Predictor):
         self.user_sq = (torch.zeros(max(self.n_users, 1), dtype=torch.float64, device=dev)
                         if self.ckpt else None)
         self._sq_valid = self._sq_pending = False
+        # several ranks, checkpoint log: the next chunk's <p^2> rode in this chunk's exchange
+        # buffer (already every rank's sum: no collective of its own at the chunk start)
+        self._stat_global = False
 
         # ---- factor tables
         U, I, ld, ldq = self.n_users, self.n_items, self.ld, self.ldq
@@ -859,8 +862,10 @@ class MFEngine(ItemSync, Predictor):
                       self._ptr(self.user_sq), self.dtype, st)
             self._sq_reduce(cur, st)
             self._sq_valid = True
+            self._stat_global = False  # (a local partial again: _global_stat sums it)
         elif self._sq_pending:  # (the previous chunk was not folded by mf_log_apply)
             self._sq_reduce(cur, st)
+            self._stat_global = False
         else:
             launched = False
         launched = self._global_stat() or launched  # (several ranks: every rank's <p^2>)
@@ -964,6 +969,9 @@ class MFEngine(ItemSync, Predictor):
         ctx = self._ctx
         if ctx is None or ctx.world == 1 or not self.is_log:
             return False
+        if self._stat_global:  # (summed by the previous chunk's exchange)
+            self._stat_global = False
+            return False
         ctx.all_reduce_sum(self.work)
         return True
 
@@ -1020,8 +1028,9 @@ class MFEngine(ItemSync, Predictor):
         return {"count": _lib.MF_MERGE_COUNT, "recency": _lib.MF_MERGE_RECENCY,
                 "sum": _lib.MF_MERGE_SUM}[self.merge_rule]
 
-    def _log_fold(self, delta_out, apply):
-        """mf_log_apply of the current chunk (its pieces were reduced in run_chunk)."""
+    def _log_fold(self, delta_out, apply, stat=None):
+        """mf_log_apply of the current chunk (its pieces were reduced in run_chunk); stat: also
+        sum the next chunk's <p^2> (default: when it applies)."""
         c = getattr(self, "_chunk", 0)
         lg = self.logs[c]
         hv = lg["heavy"]
@@ -1035,7 +1044,7 @@ class MFEngine(ItemSync, Predictor):
                   self._ptr(self._totals()[c]), ctypes.byref(self._hyper),
                   self._ptr(self.work), self._log_rule(),
                   None if delta_out is None else self._ptr(delta_out), int(apply),
-                  *self._stat_args(apply), self.dtype, self._st())
+                  *self._stat_args(apply if stat is None else stat), self.dtype, self._st())
 
     def _bind_fork(self):
         """The next mf_log_apply completes the "fork" event the side stream waits for (the item
@@ -1087,20 +1096,33 @@ class MFEngine(ItemSync, Predictor):
             return
         flat, bufs = self._delta_buffer()
         self._delta_into(bufs)
+        ride = self._stat_rides()
+        if ride:  # the next chunk's <p^2> partial (summed by _delta_into) rides in the buffer
+            flat[-2:].copy_(self._works[self._wt % 2])
         ev = getattr(self, "_sync_events", None)
         if ev:
             ev["ar_begin"].record(self.stream)
         ctx.all_reduce_sum(flat)
         if ev:
             ev["ar_end"].record(self.stream)
+        if ride:
+            self._works[self._wt % 2].copy_(flat[-2:])
+            self._stat_global = True
         self._apply(bufs)
+
+    def _stat_rides(self):
+        """Several ranks, checkpoint log: the next chunk's <p^2> is summed from user_sq by this
+        chunk's first mf_log_apply (apply = 0, before the all-reduce) and rides in the exchange
+        buffer's last two elements -- one collective per chunk instead of two."""
+        return self.ckpt and self.world > 1
 
     def _delta_buffer(self):
         """(flat, views): one device buffer holding [log sums (log mode)] + [one delta per
         snapshot table] -- the chunk's whole exchange is one all-reduce."""
         if self._delta is None:
             sizes = ([self.n_items * self.ldq] if self.is_log else []) + \
-                [self.n_items * ld for _, _, ld, _, _ in self._snap_tables()]
+                [self.n_items * ld for _, _, ld, _, _ in self._snap_tables()] + \
+                ([2] if self._stat_rides() else [])
             flat = self.torch.zeros(sum(sizes), dtype=self.tdt, device=self.dev)
             views, o = [], 0
             for n in sizes:
@@ -1114,7 +1136,7 @@ class MFEngine(ItemSync, Predictor):
         st = self._st()
         x = 0
         if self.is_log:  # (self.work already holds every rank's <p^2>: _global_stat)
-            self._log_fold(bufs[0], False)
+            self._log_fold(bufs[0], False, stat=self._stat_rides())
             x = 1
         for tab, snap, ld, bias_col, rule in self._snap_tables():
             if rule == "affine":
@@ -1146,7 +1168,7 @@ class MFEngine(ItemSync, Predictor):
                       self._bias_col, self._ptr(bufs[0]), None, None, None,
                       self._ptr(self._totals()[c]),
                       ctypes.byref(self._hyper), self._ptr(self.work), self._log_rule(), None,
-                      1, *self._stat_args(True), self.dtype, st)
+                      1, *self._stat_args(not self._stat_rides()), self.dtype, st)
             x = 1
         for tab, snap, ld, _, rule in self._snap_tables():
             if rule == "affine":
