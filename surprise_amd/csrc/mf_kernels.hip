@@ -3146,7 +3146,7 @@ __global__ __launch_bounds__(kBlock) void als_user_kernel(
 // early users' c_u must decay with the later users' factors.)  Affine maps compose associatively,
 // (A2, c2) o (A1, c1) = (A2 A1, A2 c1 + c2), so the composition is a two-level tree over the log's
 // pieces (<= 64 ratings of one item): y_piece_kernel composes each piece (one wave, one FMA per
-// user, rows 8 users ahead), y_apply_kernel applies an item's pieces in order.
+// user, two groups of 8 users' rows in flight), y_apply_kernel applies an item's pieces in order.
 #ifndef MF_YFOLD_U
 #define MF_YFOLD_U 8
 #endif
@@ -3166,12 +3166,12 @@ __global__ __launch_bounds__(kBlock) void y_piece_kernel(
         T cacc[V], Aacc = T(1);
 #pragma unroll
         for (int v = 0; v < V; ++v) cacc[v] = T(0);
-        constexpr int kU = MF_YFOLD_U;  // users' rows in flight
-        for (int x = 0; x < e - b; x += kU) {
-            T g[kU][V], A[kU];
+        constexpr int kU = MF_YFOLD_U;  // users' rows per group, two groups in flight
+        const int n = e - b;
+        auto load = [&](const int x, T (&g)[kU][V], T (&A)[kU]) {
 #pragma unroll
             for (int a = 0; a < kU; ++a) {
-                const bool ok = x + a < e - b;
+                const bool ok = x + a < n;
                 const int64_t u = readlane(my_u, ok ? x + a : 0);
                 A[a] = ok ? uA[u] : T(1);  // (past the piece: the identity map)
 #pragma unroll
@@ -3180,12 +3180,23 @@ __global__ __launch_bounds__(kBlock) void y_piece_kernel(
                     g[a][v] = (ok && c < K) ? ycbuf[u * ldu + c] : T(0);
                 }
             }
+        };
+        auto comp = [&](T (&g)[kU][V], T (&A)[kU]) {
 #pragma unroll
             for (int a = 0; a < kU; ++a) {
                 Aacc = A[a] * Aacc;
 #pragma unroll
                 for (int v = 0; v < V; ++v) cacc[v] = A[a] * cacc[v] + g[a][v];
             }
+        };
+        T gA[kU][V], AA[kU], gB[kU][V], AB[kU];
+        load(0, gA, AA);
+        for (int x = 0; x < n; x += 2 * kU) {
+            if (x + kU < n) load(x + kU, gB, AB);
+            comp(gA, AA);
+            if (x + kU >= n) break;
+            if (x + 2 * kU < n) load(x + 2 * kU, gA, AA);
+            comp(gB, AB);
         }
 #pragma unroll
         for (int v = 0; v < V; ++v) {
