@@ -269,6 +269,10 @@ struct Buf<float> {
     __device__ static __forceinline__ void add(rsrc_t r, float *, uint32_t, uint32_t off, float v) {
         __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);  // memory-side add
     }
+    template <int AUX>
+    __device__ static __forceinline__ float lds(rsrc_t r, uint32_t voff, uint32_t soff) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX));
+    }
 };
 
 template <>
@@ -287,6 +291,10 @@ struct Buf<double> {
     __device__ static __forceinline__ void add(rsrc_t, double *base, uint32_t bytes, uint32_t off,
                                                double v) {
         if (off < bytes) atomicAdd(base + off / sizeof(double), v);
+    }
+    template <int AUX>
+    __device__ static __forceinline__ double lds(rsrc_t r, uint32_t voff, uint32_t soff) {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, AUX));
     }
 };
 
@@ -1180,6 +1188,7 @@ struct PPRing {
     static constexpr int R = 4 * hx_bank<G>();  // ring slots
     typename Lane8<T>::vec data[R][G][kWave];
     uint32_t off[R];
+    T bias[R];  // SB: the slot's item-bias delta (the row's column K, outside the lane groups)
     int head, done;
     int tail[kHxHelpers];
 };
@@ -1203,10 +1212,11 @@ __device__ __forceinline__ void set_status(int32_t *status, int32_t bit) {
 }
 
 // helper wave h of a chain: issue the atomics of the slots t = h (mod kHxHelpers)
-// (n_rows: the rows the slots' offsets may address -- 2 n_items with hot-row replicas)
-template <typename T, int G>
+// (n_rows: the rows the slots' offsets may address -- 2 n_items with hot-row replicas;
+// SB: each slot also carries the item-bias delta of column K, added by lane 0)
+template <typename T, int G, bool SB = false>
 __device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_rows,
-                               int32_t *status)
+                               int32_t *status, int K = 0)
 {
     constexpr int R = PPRing<T, G>::R;
     constexpr int U = Lane1<T, G>::U;
@@ -1249,6 +1259,9 @@ __device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_
             for (int u = 0; u < U; ++u) v[u] = img[slot * kSlotT + lane + kWave * u];
 #pragma unroll
             for (int u = 0; u < U; ++u) atom_add1(q_rs, qb, q_oob, cq1[u], off, v[u]);
+            if constexpr (SB)  // (one lane: the other lanes' offset is past the table)
+                atom_add1(q_rs, qb, q_oob, lane == 0 ? (uint32_t)K * sizeof(T) : q_oob, off,
+                          ring->bias[slot]);
         }
         t = hd;
         lds_store(&ring->tail[h], t);  // (release: the slots' reads before the count)
@@ -1278,7 +1291,7 @@ __device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_
 // replica at row n_items + i of qb: the chains of odd workgroups add its deltas there, the
 // others to the row itself, and every read of the row adds the replica (the value one row would
 // hold: no staleness added); mf_svdpp_hot_fold folds the replicas back after the chunk.
-template <typename T, int G, bool HX, bool HOT = false>
+template <typename T, int G, bool HX, bool HOT = false, bool SB = false>
 __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
@@ -1308,6 +1321,9 @@ __device__ __forceinline__ void epoch_body_pp_la(
     const uint32_t rep_shift = (uint32_t)n_items * qrow;
     const uint32_t q_oob = (HOT ? 2u : 1u) * rep_shift, y_oob = (uint32_t)n_items * yrow;
     const bool to_rep = HOT && (blockIdx.x & 1);  // this chain's hot deltas: to the replicas
+    // SB (the lane groups cover the K factor columns only, K * size a multiple of 512 B): the item
+    // bias, column K, rides beside the row as one wave-uniform element per rating
+    const uint32_t kbo = (uint32_t)K * sizeof(T);
     int pushed = 0;  // HX: ratings pushed to the ring
     uint32_t cq[G], cu[G], cq1[U], cy1[U];
     vec one[G], lrp[G], ap[G], lry[G], lrpy[G], lrq[G], nrq[G];
@@ -1402,11 +1418,13 @@ __device__ __forceinline__ void epoch_body_pp_la(
             if constexpr (HOT) gh = hot[i];
         };
         vec bank[2][kB][G];
+        T bb[SB ? 2 : 1][SB ? kB : 1];  // SB: each entry's item bias (every lane the same)
         vec rep[HOT ? 2 : 1][HOT ? kB : 1][G];  // HOT: the replica rows of a bank's entries
         T br[2][kB];
         uint32_t bo[2][kB];
         uint32_t hm[2] = {0u, 0u};  // HOT: bit d = entry d of the bank is a hot item
         vec dl[kB][G];      // the q deltas of the current bank (issued one bank late)
+        T dlb[SB ? kB : 1];  // SB: their item-bias deltas
         uint32_t dlo[kB];   // their row offsets (masked ratings: past the table)
         uint32_t go_n1, go_n2;
         T gr_n1, gr_n2;
@@ -1421,6 +1439,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 br[bk][d] = readlane(gr, d);
 #pragma unroll
                 for (int v = 0; v < G; ++v) bank[bk][d][v] = L::template lds<kSc1>(q_rs, cq[v], off);
+                if constexpr (SB) bb[bk][d] = Buf<T>::template lds<kSc1>(q_rs, kbo, off);
                 if constexpr (HOT) {  // (a uniform branch: most entries are not hot)
                     if ((hm[bk] >> d) & 1u) {
 #pragma unroll
@@ -1437,6 +1456,8 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 to_lane1<G>(dl[d], d1);
 #pragma unroll
                 for (int uu = 0; uu < U; ++uu) atom_add1(q_rs, qb, q_oob, cq1[uu], dlo[d], d1[uu]);
+                if constexpr (SB)
+                    atom_add1(q_rs, qb, q_oob, lane == 0 ? kbo : q_oob, dlo[d], dlb[d]);
             }
         };
         auto flush = [&]() {  // the float atomics of the previous bank's ratings
@@ -1467,6 +1488,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
 #pragma unroll
                     for (int v = 0; v < G; ++v) ring->data[slot][v][lane] = dl[d][v];
                     ring->off[slot] = dlo[d];
+                    if constexpr (SB) ring->bias[slot] = dlb[d];
                 }
                 pushed += kB;
                 lds_store(&ring->head, pushed);  // (release: the rows before the count)
@@ -1507,6 +1529,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 part += qrow_of(0, 0, v) * (p0[v] + m0[v]);
             }
             X = wave_sum_u(L::hsum(part));
+            if constexpr (SB) X += bb[0][0];
         }
         auto step = [&](auto full_c, auto bank_c, const int j0, const int d) {
             constexpr bool FULL = decltype(full_c)::value;
@@ -1538,10 +1561,12 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 py += qn[v] * (lrpy[v] * q);
                 dl[d][v] = err * (lrq[v] * sk) + nrq[v] * q;  // mf.pyx:489, :492
             }
+            if constexpr (SB) dlb[d] = hp.lr_bi * (err - hp.reg_bi * bb[bk][d]);  // mf.pyx:489
             const bool hot_d = HOT && to_rep && ((hm[bk] >> d) & 1u);
             dlo[d] = valid ? (hot_d ? bo[bk][d] + rep_shift : bo[bk][d]) : bo[bk][d] + q_oob;
             T Xn, Yn;
             wave_sum2_u(L::hsum(px), L::hsum(py), Xn, Yn);  // X_{k+1}, Y_{k+1}
+            if constexpr (SB) Xn += bb[bn][dn];  // (the next item's bias: s_k's column K is 1)
             err_p = valid ? err : err_p;
             c0_p = valid ? c0 : c0_p;
             X = valid ? Xn : X;
@@ -1663,7 +1688,10 @@ __global__ __launch_bounds__(kBlock) void mf_ckpt_epoch_kernel(MF_EPOCH_PARAMS)
 }
 
 // SVD++ with helper waves (MF_SVDPP_HELPERS): workgroup = chain wave 0 + kHxHelpers atomic waves
-template <typename T, int G, bool HOT>
+// SB: the lane groups cover the K factor columns only and the item bias (column K) is carried as
+// a scalar per rating (fp32 K=128: one lane group instead of two -- half the vector work and the
+// registers of a bank of 8 rows)
+template <typename T, int G, bool HOT, bool SB = false>
 __global__ __launch_bounds__(kBlock) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS, int32_t *status,
                                                              const uint8_t *hot)
 {
@@ -1676,12 +1704,12 @@ __global__ __launch_bounds__(kBlock) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS, in
     }
     __syncthreads();
     if (w == 0) {
-        epoch_body_pp_la<T, G, true, HOT>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu,
-                                          qb, ldq, yj, elog, K, hp, n_items, n_waves_req, 0,
-                                          &ring, status, hot);
+        epoch_body_pp_la<T, G, true, HOT, SB>(row_ptr, items, ratings, sched, n_sched, pu, bu,
+                                              ldu, qb, ldq, yj, elog, K, hp, n_items, n_waves_req,
+                                              0, &ring, status, hot);
         if (blockIdx.x >= n_waves_req) lds_store(&ring.done, 1);  // (no chain in this workgroup)
     } else {
-        pp_ring_helper<T, G>(&ring, w - 1, qb, ldq, (HOT ? 2 : 1) * n_items, status);
+        pp_ring_helper<T, G, SB>(&ring, w - 1, qb, ldq, (HOT ? 2 : 1) * n_items, status, K);
     }
 }
 
@@ -1712,11 +1740,17 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     if (hx && !(PP && M == kAtomic && elog && !dups))
         return set_err(MF_E_UNSUPPORTED, "helper waves: SVD++, MF_MODE_ATOMIC, deferred y, no repeated items");
     if (hot && !hx) return set_err(MF_E_ARG, "hot-row replicas: the helper-wave launch only");
-    return dispatch_g<T>(ldq, [&](auto gc) -> int {
+    // the helper-wave launch with the item bias beside the lane groups (SB) where the factor
+    // columns fill whole groups and the bias column alone would need another
+    const bool sb = hx && !hot && ((int64_t)K * sizeof(T)) % 512 == 0 &&
+                    (int64_t)K * sizeof(T) < ((int64_t)ldq * sizeof(T) + 511) / 512 * 512;
+    return dispatch_g<T>(sb ? K : ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         if constexpr (PP && M == kAtomic && V <= kLaMaxG) {
             if (hx) {  // one workgroup per chain: wave 0 trains, waves 1-3 issue the q atomics
-                auto kern = hot ? mf_svdpp_hx_kernel<T, V, true> : mf_svdpp_hx_kernel<T, V, false>;
+                auto kern = hot ? mf_svdpp_hx_kernel<T, V, true>
+                          : sb  ? mf_svdpp_hx_kernel<T, V, false, true>
+                                : mf_svdpp_hx_kernel<T, V, false>;
                 hipLaunchKernelGGL(kern, dim3(waves), dim3(kBlock), 0,
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,

@@ -345,6 +345,25 @@ def test_c3_ml1m_svdpp_k100_rmse_within_1e3(torch, ml1m):
     assert abs(got - ref) < RMSE_TOL, (got, ref)
 
 
+@pytest.mark.parametrize("K,dtype", [(128, "float32"), (64, "float64")])
+def test_svdpp_item_bias_beside_lane_groups_rmse(torch, u1, K, dtype):
+    """The helper-wave launch with the item bias carried beside the lane groups (the factor
+    columns fill whole 512-byte groups: fp32 K=128, fp64 K=64 -- C5's layout) within 1e-3
+    of the exact per-user oracle's held-out RMSE, and hot-row replicas (which keep the bias in
+    the row) within 1e-3 of it too."""
+    from surprise_amd import SVDpp
+    ts, test = u1
+    params = dict(n_factors=K, n_epochs=10, random_state=0)
+    ref = _oracle_rmse("SVDpp", params, ts, test, affine=True)
+    for opt in ({}, {"hot_rows": 16}):
+        algo = SVDpp(**params, mode="atomic", dtype=dtype)
+        algo._engine_options = opt
+        algo.fit(ts)
+        assert algo._engine.hx
+        got = _rmse(algo.test(test))
+        assert abs(got - ref) < RMSE_TOL, (opt, got, ref)
+
+
 @pytest.mark.parametrize("K", [1, 3, 17, 64, 65, 100, 128, 200, 256, 300, 512])
 def test_factor_counts_deterministic_fp32(torch, u1, K):
     """Every lane layout (V = 1, 2, 4, 8 elements per lane, padded and unpadded ld)."""
