@@ -876,7 +876,12 @@ __device__ __forceinline__ void wave_sum2_u(T x, T y, T &sx, T &sy) {
 // ap = abu, lrp = lr_bu and a constant kb added to A in that column: c's recursion
 // c_{k+1} = abu c_k + kb + lr_bu err_k is the row's own, <q_k, p_k> includes c_k and Y_k includes
 // lr_bu, so err_k = r_k - X_k - err_{k-1} Y_k with no scalar bias recursion beside it.
-template <typename T, int G, bool CK, bool ER = false>
+// SB (narrow checkpoint rows, K * size a multiple of 512 B: fp32 K=128): the lane groups cover
+// the K factor columns only; the item bias b_k (column K) is loaded beside each row as a
+// wave-uniform element and the user bias c_k = mu + bu_k is the scalar recursion
+// c_{k+1} = C0_k + lr_bu err_k, C0_k = abu c_k + kb: X_{k+1} gains b_{k+1} + C0_k and Y_{k+1}
+// gains lr_bu -- the same err_k as the in-row form, with one lane group instead of two.
+template <typename T, int G, bool CK, bool ER = false, bool SB = false>
 __device__ __forceinline__ void epoch_body_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
@@ -904,6 +909,7 @@ __device__ __forceinline__ void epoch_body_la(
     const T lr_bu = biased ? hp.lr_bu : T(0);
     const T abu = T(1) - lr_bu * hp.reg_bu;
     const T kb = hp.gm * (T(1) - abu);
+    const uint32_t kbo = (uint32_t)K * sizeof(T);  // SB: the item bias's offset in a row
     uint32_t cq[G], cu[G], cl[G];
     vec one[G], lrp[G], ap[G], kvec[G], cvec[G];
 #pragma unroll
@@ -973,6 +979,7 @@ __device__ __forceinline__ void epoch_body_la(
         };
         vec bank[2][kB][G];
         T br[2][kB];
+        T bb[SB ? 2 : 1][SB ? kB : 1];  // SB: each entry's item bias (every lane the same)
         // log rows of the current bank: CK: per pair (c, c + 1) of the user's ratings (c even) the
         // row p_{c+1} at log row c, and err_k in lane k mod kB of ev; otherwise every rating's
         // gradient row g_k = err_k p_k
@@ -988,6 +995,7 @@ __device__ __forceinline__ void epoch_body_la(
                 br[bk][d] = readlane(gr, d);
 #pragma unroll
                 for (int v = 0; v < G; ++v) bank[bk][d][v] = L::template lds<0>(q_rs, cq[v], off);
+                if constexpr (SB) bb[bk][d] = Buf<T>::template lds<0>(q_rs, kbo, off);
             }
         };
         auto flush = [&](const int j0p) {  // log rows j0p .. j0p + kB - 1
@@ -1025,6 +1033,7 @@ __device__ __forceinline__ void epoch_body_la(
         // state entering rating k: err_p = err_{k-1}, A_p = A_{k-1}, D_p = D_{k-1}, X = X_k,
         // Y = Y_k (k = 0: err_{-1} = 0, A_{-1} = p_0, D_{-1} = 0, X_0 = <q_0, p_0>)
         T err_p = T(0), X, Y = T(0);
+        T C0_p = hp.gm + bu0;  // SB: C0_{k-1} (k = 0: c_0 itself, err_{-1} = 0)
         vec A_p[G], D_p[G];
         {
             vec part = L::splat(T(0));
@@ -1035,6 +1044,7 @@ __device__ __forceinline__ void epoch_body_la(
                 part += bank[0][0][v] * p0[v];
             }
             X = wave_sum_u(L::hsum(part));
+            if constexpr (SB) X += bb[0][0] + C0_p;
         }
 
         auto step = [&](auto full_c, auto bank_c, const int j0, const int d) {
@@ -1066,10 +1076,18 @@ __device__ __forceinline__ void epoch_body_la(
             if (CK) ev = lane == d ? err : ev;
             T Xn, Yn;
             wave_sum2_u(L::hsum(px), L::hsum(py), Xn, Yn);  // X_{k+1}, Y_{k+1}
+            T C0 = T(0);
+            if constexpr (SB) {  // c_k = C0_{k-1} + lr_bu err_{k-1}; C0_k = abu c_k + kb
+                C0 = abu * (C0_p + lr_bu * err_p) + kb;
+                const int bn = d + 1 < kB ? bk : bk ^ 1, dn = d + 1 < kB ? d + 1 : 0;
+                Xn += bb[bn][dn] + C0;
+                Yn += lr_bu;
+            }
             if (FULL) {
                 err_p = err;
                 X = Xn;
                 Y = Yn;
+                if constexpr (SB) C0_p = C0;
 #pragma unroll
                 for (int v = 0; v < G; ++v) {
                     A_p[v] = A[v];
@@ -1079,6 +1097,7 @@ __device__ __forceinline__ void epoch_body_la(
                 err_p = valid ? err : err_p;
                 X = valid ? Xn : X;
                 Y = valid ? Yn : Y;
+                if constexpr (SB) C0_p = valid ? C0 : C0_p;
 #pragma unroll
                 for (int v = 0; v < G; ++v) {
                     A_p[v] = valid ? A[v] : A_p[v];
@@ -1138,13 +1157,14 @@ __device__ __forceinline__ void epoch_body_la(
         for (int v = 0; v < G; ++v) {
             const vec pn = A_p[v] + err_p * D_p[v];
             L::template st<0>(p_rs, cu[v], pn);
-            if (v == cb_grp) cn = readlane(L::get(pn, cb_e), cb_lane);
+            if (!SB && v == cb_grp) cn = readlane(L::get(pn, cb_e), cb_lane);
 #pragma unroll
             for (int e = 0; e < W; ++e) {
                 const double x = (double)L::get(pn, e);
                 sq += (lane + kWave * v) * W + e < K ? x * x : 0.0;
             }
         }
+        if constexpr (SB) cn = C0_p + lr_bu * err_p;  // c_n
         if (psq) {
             sq = wave_sum(sq);
             if (lane == 0) psq[u] = sq;
@@ -1678,13 +1698,14 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
 }
 
 // SVD checkpoint log (elog != NULL): its own kernel, so that its register allocation is its own
-// (ER: the errors go into the checkpoint rows, MF_EPOCH_ERR_IN_ROW)
-template <typename T, int G, bool ER>
+// (ER: the errors go into the checkpoint rows, MF_EPOCH_ERR_IN_ROW; SB: the biases beside the
+// lane groups, narrow rows of whole groups)
+template <typename T, int G, bool ER, bool SB = false>
 __global__ __launch_bounds__(kBlock) void mf_ckpt_epoch_kernel(MF_EPOCH_PARAMS)
 {
-    epoch_body_la<T, G, true, ER>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq,
-                                  qlog, elog, K, biased, hp, n_items, n_waves_req, xmask, psq,
-                                  err_col, ck_ld);
+    epoch_body_la<T, G, true, ER, SB>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb,
+                                      ldq, qlog, elog, K, biased, hp, n_items, n_waves_req, xmask,
+                                      psq, err_col, ck_ld);
 }
 
 // SVD++ with helper waves (MF_SVDPP_HELPERS): workgroup = chain wave 0 + kHxHelpers atomic waves
@@ -1742,9 +1763,12 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     if (hot && !hx) return set_err(MF_E_ARG, "hot-row replicas: the helper-wave launch only");
     // the helper-wave launch with the item bias beside the lane groups (SB) where the factor
     // columns fill whole groups and the bias column alone would need another
-    const bool sb = hx && !hot && ((int64_t)K * sizeof(T)) % 512 == 0 &&
-                    (int64_t)K * sizeof(T) < ((int64_t)ldq * sizeof(T) + 511) / 512 * 512;
-    return dispatch_g<T>(sb ? K : ldq, [&](auto gc) -> int {
+    const bool whole = ((int64_t)K * sizeof(T)) % 512 == 0 &&
+                       (int64_t)K * sizeof(T) < ((int64_t)ldq * sizeof(T) + 511) / 512 * 512;
+    const bool sb = hx && !hot && whole;
+    // ... and the SVD checkpoint epoch with narrow rows (the rows hold the factor columns only)
+    const bool sbk = !PP && M == kLog && elog && ck_ld < ldq && err_col <= 0 && whole;
+    return dispatch_g<T>(sb || sbk ? K : ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         if constexpr (PP && M == kAtomic && V <= kLaMaxG) {
             if (hx) {  // one workgroup per chain: wave 0 trains, waves 1-3 issue the q atomics
@@ -1765,6 +1789,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
         if constexpr (M == kLog && !PP && V <= kLaMaxG && MF_LA) {
             if (elog) {  // the checkpoint log
                 auto ck = err_col > 0 ? mf_ckpt_epoch_kernel<T, V, true>
+                          : sbk       ? mf_ckpt_epoch_kernel<T, V, false, true>
                                       : mf_ckpt_epoch_kernel<T, V, false>;
                 hipLaunchKernelGGL(ck, dim3(grid_for_waves_x(waves, xmask)), dim3(kBlock), 0,
                                    (hipStream_t)stream, csr->row_ptr, csr->items,

@@ -535,13 +535,16 @@ def test_errors_in_checkpoint_rows_equal_elog(torch, u1, monkeypatch, K, dtype, 
 @pytest.mark.parametrize("K,dtype,heavy,auto", [(128, "float32", 0.0, True),
                                                  (64, "float32", 0.25, True),
                                                  (48, "float64", 0.0, True),
+                                                 (64, "float64", 0.25, True),
                                                  (21, "float32", 0.25, False),
                                                  (20, "float64", 0.0, False)])
 def test_narrow_checkpoint_rows_match_padded_rows(torch, u1, K, dtype, heavy, auto):
     """MF_EPOCH_CKPT_NARROW (checkpoint rows of the K factor columns only, errors in elog, the
     bias column's gradient summed from the errors) against the padded rows: the same gradients,
     the bias column summed in another order (fp64 within 1e-12, fp32 within 1e-5); auto: the
-    engine picks narrow rows by itself (rows of whole 128-byte lines)."""
+    engine picks narrow rows by itself (rows of whole 128-byte lines).  fp32 K=128 and fp64
+    K=64 fill whole lane groups: the epoch kernel then also carries both biases beside the
+    groups (one lane group instead of two, the SB form of epoch_body_la)."""
     from surprise_amd.engine import MFEngine
     ts, _ = u1
     row_ptr, items, ratings = ts.csr()
