@@ -20,7 +20,8 @@ ts, _ = next(KFold(5, random_state=0).split(Dataset.load_from_arrays(u, i, r)))
 rp, it, rt = ts.csr()
 hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02, reg_pu=.02,
              reg_qi=.02, global_mean=float(ts.global_mean))
-eng = MFEngine((rp, it, rt), ts.n_items, K, hyper=hyper, mode=mode, algo=algo, heavy=0)
+eng = MFEngine((rp, it, rt), ts.n_items, K, hyper=hyper, mode=mode, algo=algo, heavy=0,
+               dtype=os.environ.get("PROBE_DTYPE", "float32"))
 rng = np.random.RandomState(0)
 eng.set_factors(rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K)),
                 yj=rng.normal(0, .1, (ts.n_items, K)) if algo == "svdpp" else None)
@@ -51,6 +52,9 @@ cases = [("full", order, None), ("top1", order[:1], None), ("top16", order[:16],
          ("full-2048waves", order, 2048), ("full-8192waves", order, 8192)]
 if len(sys.argv) > 3 and sys.argv[3] == "waves":
     cases = [("full-%dwaves" % w, order, w) for w in (2048, 4096, 6040, 8192, 12288, 16384)]
+if len(sys.argv) > 3 and sys.argv[3] == "chain":
+    cases = [("full", order, None), ("top1", order[:1], None), ("top8", order[:8], None),
+             ("top128", order[:128], None), ("top128-512waves", order[:128], 512)]
 if len(sys.argv) > 3 and sys.argv[3] == "fast":
     cases = [c for c in cases if c[0] in ("full", "top1", "drop-top64")]
 for name, s, nw in cases:
