@@ -395,6 +395,77 @@ def cpu_baselines(csr, n_items, K, n_train):
     }
 
 
+def cpu_baseline_svdpp(csr, n_items, K, n_train, target_s=8.0):
+    """SVD++ C3 beside the GPU: the fp64 C restatement of SVDpp.sgd in the reference's
+    per-rating form (oracle_svdpp_sgd <- mf.pyx:463-498: u_impl re-summed over I_u and every
+    y_j of I_u stepped, per rating, so a user's epoch costs ~ n_u^2 K).  A whole full-fold epoch
+    is minutes of CPU, so the bounded sample is one epoch over a user prefix of the same fold
+    sized to ~target_s on one core; the full-fold epoch time is that time x sum_all(n_u^2) /
+    sum_prefix(n_u^2) (the per-(rating x |I_u|) cost is flat: 485-486 ns at 100 and 300 users in
+    the build container).  One pinned core, then one pinned process per core of the box's share
+    on the same sample.  Context: the per-user affine form (O(K) per rating, the GPU kernels'
+    algebra) on one core over the whole fold."""
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    row_ptr, items, ratings = (np.asarray(a) for a in csr)
+    deg2 = np.diff(row_ptr).astype(np.float64) ** 2
+    cum = np.cumsum(deg2)
+    s_all = float(cum[-1])
+    cores = sorted(os.sched_getaffinity(0))
+    share = cores[:BOX_CPU_SHARE]
+    old = set(cores)
+
+    def prefix(s_target):
+        nu = int(min(len(deg2), np.searchsorted(cum, s_target) + 1))
+        k1 = int(row_ptr[nu])
+        return nu, (row_ptr[:nu + 1], items[:k1], ratings[:k1]), float(cum[nu - 1])
+
+    os.sched_setaffinity(0, {share[0]})
+    try:
+        nu0, sub0, s0 = prefix(2e6)
+        t0 = orc.time_svdpp_epochs(*sub0, n_items, K, 1)
+        nu, sub, s_smp = prefix(target_s * s0 / max(t0, 1e-6))
+        t1 = orc.time_svdpp_epochs(*sub, n_items, K, 1)
+        t_aff = orc.time_svdpp_epochs(row_ptr, items, ratings, n_items, K, 1, affine=True)
+    finally:
+        os.sched_setaffinity(0, old)
+    full1 = t1 * s_all / s_smp  # one core's full-fold epoch (derived from the sample)
+    with tempfile.TemporaryDirectory() as d:
+        for name, a in zip(("row_ptr", "items", "ratings"), sub):
+            np.save(os.path.join(d, name + ".npy"), a)
+        np.save(os.path.join(d, "n_items.npy"), np.asarray(n_items))
+        w = os.path.join(ROOT, "oracle", "cpu_worker.py")
+        tw = time.perf_counter()
+        procs = [subprocess.Popen([sys.executable, w, d, str(c), "1", str(K), "svdpp"],
+                                  stdout=subprocess.PIPE, text=True) for c in share]
+        outs = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in procs]
+        wall = time.perf_counter() - tw
+    full_n = max(o["seconds"] for o in outs) * s_all / s_smp  # the slowest core's full epoch
+    return {
+        "value": len(share) * n_train / full_n, "unit": "rating-updates/s", "cores": len(share),
+        "kind": "port",
+        "sample": "fp64 C restatement of SVDpp.sgd in the reference's per-rating form "
+                  "(oracle/mf_oracle.c oracle_svdpp_sgd <- mf.pyx:463-498), SVD++ K=%d: one epoch "
+                  "over the first %d users (%d ratings, sum n_u^2 = %.3g of the fold's %.3g) on "
+                  "each of %d pinned processes (wall incl. process start %.1fs); value = %d x "
+                  "the fold's %d ratings / the slowest process's epoch time scaled by the "
+                  "sum n_u^2 ratio (%.1f s per full-fold epoch per core)"
+                  % (K, nu, int(sub[0][-1]), s_smp, s_all, len(share), wall, len(share),
+                     n_train, full_n),
+        "single_core": {"value": n_train / full1, "cores": 1, "pinned": True,
+                        "full_fold_epoch_s_derived": full1,
+                        "sample": "one epoch over the first %d users on core %d: %.2fs"
+                                  % (nu, share[0], t1)},
+        "affine_form_single_core": {
+            "value": n_train / t_aff, "cores": 1, "pinned": True,
+            "note": "context, not the reference's cost: the per-user affine reformulation "
+                    "(oracle_svdpp_sgd_affine, O(K) per rating -- the algebra the GPU kernels "
+                    "use), one full-fold epoch (%.2fs)" % t_aff},
+        "host_cpus": os.cpu_count(), "cpus_allowed": len(cores), "cpu_model": cpu_model(),
+    }
+
+
 # ---------------------------------------------------------------------------- main
 def roofline_of(algo, K, dtype, n_train, ms_step, shape, phases=None):
     """The dominant kernel's roofline: SURVEY 8(d) algorithmic bytes per launch (the ratings the
@@ -536,6 +607,9 @@ def main():
         cb = result["cpu_baseline"]
         cb["gpu_over_cpu_all_cores"] = value / cb["value"]
         cb["gpu_over_cython_equivalent_single"] = value / cb["single_core"]["cython_equivalent_derived"]
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and algo == "svdpp":
+        result["cpu_baseline"] = cpu_baseline_svdpp(csr, n_items, K, n_train)
+        result["cpu_baseline"]["gpu_over_cpu"] = value / result["cpu_baseline"]["value"]
 
     if not args.no_rmse:
         result["rmse"] = rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch,
@@ -578,6 +652,11 @@ def main():
         for dt, leg in pp_legs.items():
             if dt != args.dtype:
                 result["svdpp_c3"]["%s_leg" % dt] = leg
+        if rank == 0 and not args.no_cpu_baseline:
+            cb = cpu_baseline_svdpp(csr, n_items, 100, n_train)
+            cb["gpu_over_cpu"] = result["svdpp_c3"]["value"] / cb["value"]
+            result["svdpp_c3"]["cpu_baseline"] = cb
+            note("svd++ cpu baseline done")
 
     if small and headline and args.legs and not args.no_predict:
         result["predict"] = predict_leg(csr, test, n_items, gm, torch)

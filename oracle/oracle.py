@@ -338,6 +338,22 @@ def py_svd_sgd(row_ptr, items, ratings, K, n_epochs, biased, global_mean, hp, pu
     return pu, qi, bu, bi
 
 
+def time_svdpp_epochs(row_ptr, items, ratings, n_items, K, n_epochs, seed=0, affine=False):
+    """Wall-clock of the C restatement of SVDpp.sgd (1 thread) for the SVD++ cpu_baseline leg:
+    the reference's per-rating loop (u_impl re-summed over I_u and every y_j of I_u stepped, per
+    rating: O(|I_u| K), mf.pyx:463-498), or (affine) the per-user affine form, O(K) per rating."""
+    import time
+    rng = np.random.RandomState(seed)
+    n_users = len(row_ptr) - 1
+    pu, qi, yj = init_factors(rng, n_users, n_items, K, with_yj=True)
+    hp = hyper(lr_bu=.007, lr_bi=.007, lr_pu=.007, lr_qi=.007, lr_yj=.007,
+               reg_bu=.02, reg_bi=.02, reg_pu=.02, reg_qi=.02, reg_yj=.02)
+    gm = float(np.mean(ratings))
+    t0 = time.perf_counter()
+    svdpp_sgd(row_ptr, items, ratings, n_items, K, n_epochs, gm, hp, pu, qi, yj, affine=affine)
+    return time.perf_counter() - t0
+
+
 def time_svd_epochs(row_ptr, items, ratings, n_items, K, n_epochs, seed=0):
     """Wall-clock of the C restatement (1 thread) for the cpu_baseline leg."""
     import time

@@ -428,3 +428,20 @@ def test_svdpp_affine_rule_one_group_composes_in_user_order(u1):
         Y[js] = decay ** (e - s) * Y[js] + c
     np.testing.assert_allclose(a[2], Y, rtol=0, atol=1e-11)
     np.testing.assert_allclose(a[1], Q, rtol=0, atol=1e-11)
+
+
+def test_svdpp_cpu_baseline_leg_on_a_user_prefix(u1, monkeypatch):
+    """bench.py's SVD++ cpu_baseline: the reference-order restatement on a user prefix, scaled
+    to the whole fold by sum n_u^2; one process per core of the (here: 2-core) share."""
+    import sys
+    sys.path.insert(0, os.path.dirname(GOLDEN.rstrip("/").rsplit("/", 1)[0]))
+    import bench
+    monkeypatch.setattr(bench, "BOX_CPU_SHARE", 2)
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    n = int(row_ptr[-1])
+    cb = bench.cpu_baseline_svdpp((row_ptr, items, ratings), ts.n_items, 10, n, target_s=0.2)
+    assert cb["kind"] == "port" and cb["cores"] == min(2, len(os.sched_getaffinity(0)))
+    assert cb["value"] > 0 and cb["single_core"]["value"] > 0
+    assert cb["affine_form_single_core"]["value"] > cb["single_core"]["value"]
+    assert "mf.pyx:463-498" in cb["sample"]
