@@ -81,6 +81,9 @@ def parse():
     p.add_argument("--replay-rows", type=int, default=0,
                    help="SVD checkpoint log: ratings per replay piece (0: the engine's policy, "
                         "engine.replay_piece_rows)")
+    p.add_argument("--hx-helpers", type=int, default=0,
+                   help="SVD++ helper-wave launch: helper waves per chain, 3 or 1 (0: the "
+                        "engine default)")
     p.add_argument("--hx-chains", type=int, default=0,
                    help="SVD++ helper-wave launch: user chains per CU (0: the engine default)")
     p.add_argument("--algo", default=None, choices=["svd", "svdpp"])
@@ -538,6 +541,7 @@ def main():
                        n_chunks=args.chunks or default_chunks(a, md, n_users_global),
                        **({"merge": args.merge} if args.merge else {}),
                        **({"hx_chains_per_cu": args.hx_chains} if args.hx_chains else {}),
+                       **({"helpers": args.hx_helpers} if args.hx_helpers else {}),
                        **({"hot_rows": args.hot_rows} if args.hot_rows >= 0 else {}),
                        **({"replay_rows": args.replay_rows} if args.replay_rows else {}))
         eng.set_factors(pu, qi, yj=yj)

@@ -106,6 +106,9 @@ typedef struct mf_csr {
  * (n_waves = chains) whose q deltas go through an LDS ring to three waves that issue the float
  * atomics; sched entries < 0 are skipped (a schedule laid out per chain, strided by n_waves). */
 #define MF_EPOCH_SVDPP_HELPERS 2
+/* with MF_EPOCH_SVDPP_HELPERS: ONE helper wave per chain (a workgroup of two waves) instead of
+ * three -- twice the chains per CU in the same registers (n_waves = chains, as above). */
+#define MF_EPOCH_SVDPP_ONE_HELPER 32
 /* mf_svd_epoch / mf_svd_epoch_sq with the checkpoint log (elog): err_k is written into its pair's
  * checkpoint row, padding column E + (k - c) (E = n_factors + 2 rounded up to even for fp32,
  * n_factors + 2 for fp64; needs E + 2 <= ldq) instead of elog[k]; mf_log_replay with the same

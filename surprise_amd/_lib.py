@@ -21,6 +21,7 @@ MF_MERGE_SUM, MF_MERGE_COUNT, MF_MERGE_MEAN, MF_MERGE_RECENCY = 0, 1, 2, 3
 MF_EPOCH_DUP_ITEMS = 1
 MF_EPOCH_XCD_SHIFT = 8  # flags bits 8..15: XCD mask (include/surprise_amd.h)
 MF_EPOCH_SVDPP_HELPERS = 2
+MF_EPOCH_SVDPP_ONE_HELPER = 32
 MF_EPOCH_ERR_IN_ROW = 4  # checkpoint log: errors in the checkpoint rows' padding
 MF_EPOCH_CKPT_NARROW = 16  # checkpoint log: rows of the factor columns only (errors in elog)
 

@@ -40,7 +40,7 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    bool hx, double *psq, int err_col, int ck_ld, int32_t *status,
+                    int hx, double *psq, int err_col, int ck_ld, int32_t *status,
                     const uint8_t *hot, void *stream);
 }  // namespace mf_ext
 
@@ -1200,17 +1200,17 @@ __device__ __forceinline__ void epoch_body_la(
 #endif
 template <int G>
 constexpr int hx_bank() { return G == 1 ? MF_PP_HX_BANK : MF_PP_HX_BANK_G2; }
-constexpr int kHxHelpers = 3;
+constexpr int kHxHelpers = 3;  // helper waves per chain (MF_EPOCH_SVDPP_ONE_HELPER: 1)
 constexpr int kSpinMax = 1 << 22;  // bounded spins (s_sleep 2 each, ~0.2 s): never hang the GPU
 
-template <typename T, int G>
+template <typename T, int G, int H = kHxHelpers>
 struct PPRing {
     static constexpr int R = 4 * hx_bank<G>();  // ring slots
     typename Lane8<T>::vec data[R][G][kWave];
     uint32_t off[R];
     T bias[R];  // SB: the slot's item-bias delta (the row's column K, outside the lane groups)
     int head, done;
-    int tail[kHxHelpers];
+    int tail[H];  // one per helper wave
 };
 
 // ring hand-off: the count is stored with release and read with acquire (workgroup scope: on
@@ -1231,14 +1231,14 @@ __device__ __forceinline__ void set_status(int32_t *status, int32_t bit) {
         __hip_atomic_fetch_or(status, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// helper wave h of a chain: issue the atomics of the slots t = h (mod kHxHelpers)
+// helper wave h of a chain's H: issue the atomics of the slots t = h (mod H)
 // (n_rows: the rows the slots' offsets may address -- 2 n_items with hot-row replicas;
 // SB: each slot also carries the item-bias delta of column K, added by lane 0)
-template <typename T, int G, bool SB = false>
-__device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_rows,
+template <typename T, int G, bool SB, int H>
+__device__ void pp_ring_helper(PPRing<T, G, H> *ring, int h, T *qb, int ldq, int n_rows,
                                int32_t *status, int K = 0)
 {
-    constexpr int R = PPRing<T, G>::R;
+    constexpr int R = PPRing<T, G, H>::R;
     constexpr int U = Lane1<T, G>::U;
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), q_oob = (uint32_t)n_rows * qrow;
@@ -1270,8 +1270,7 @@ __device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_
         }
         spins = 0;
         asm volatile("" ::: "memory");
-        for (int tt = t + ((h - t % kHxHelpers) + kHxHelpers) % kHxHelpers; tt < hd;
-             tt += kHxHelpers) {
+        for (int tt = t + ((h - t % H) + H) % H; tt < hd; tt += H) {
             const int slot = tt % R;
             const uint32_t off = __builtin_amdgcn_readfirstlane(ring->off[slot]);
             T v[U];
@@ -1311,12 +1310,12 @@ __device__ void pp_ring_helper(PPRing<T, G> *ring, int h, T *qb, int ldq, int n_
 // replica at row n_items + i of qb: the chains of odd workgroups add its deltas there, the
 // others to the row itself, and every read of the row adds the replica (the value one row would
 // hold: no staleness added); mf_svdpp_hot_fold folds the replicas back after the chunk.
-template <typename T, int G, bool HX, bool HOT = false, bool SB = false>
+template <typename T, int G, bool HX, bool HOT = false, bool SB = false, int H = kHxHelpers>
 __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *ycbuf, int K,
-    Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, PPRing<T, G> *ring,
+    Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, PPRing<T, G, H> *ring,
     int32_t *status, const uint8_t *__restrict__ hot = nullptr)
 {
     using L = Lane8<T>;
@@ -1482,12 +1481,12 @@ __device__ __forceinline__ void epoch_body_pp_la(
         };
         auto flush = [&]() {  // the float atomics of the previous bank's ratings
             if constexpr (HX) {  // ... handed to the helper waves through the ring
-                constexpr int R = PPRing<T, G>::R;
+                constexpr int R = PPRing<T, G, H>::R;
                 bool room = false;
                 for (int spins = 0; spins < kSpinMax; ++spins) {  // room for kB rows
                     int m = lds_load(&ring->tail[0]);
 #pragma unroll
-                    for (int h = 1; h < kHxHelpers; ++h) {
+                    for (int h = 1; h < H; ++h) {
                         const int th = lds_load(&ring->tail[h]);
                         m = th < m ? th : m;
                     }
@@ -1684,7 +1683,7 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
         if (elog) {  // deferred y (elog = ycbuf)
             epoch_body_pp_la<T, G, false>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu,
                                           qb, ldq, yj, elog, K, hp, n_items, n_waves_req, xmask,
-                                          nullptr, nullptr);
+                                          (PPRing<T, G> *)nullptr, nullptr);
             return;
         }
     }
@@ -1708,29 +1707,33 @@ __global__ __launch_bounds__(kBlock) void mf_ckpt_epoch_kernel(MF_EPOCH_PARAMS)
                                       psq, err_col, ck_ld);
 }
 
-// SVD++ with helper waves (MF_SVDPP_HELPERS): workgroup = chain wave 0 + kHxHelpers atomic waves
+// SVD++ with helper waves (MF_SVDPP_HELPERS): workgroup = chain wave 0 + H atomic waves (3, or 1
+// with MF_EPOCH_SVDPP_ONE_HELPER: a workgroup of two waves, twice the chains per CU in the same
+// registers; a helper keeps up with a chain as long as its ~2 atomics per rating stay below the
+// few dozen a wave keeps in flight for ~3000 cycles each)
 // SB: the lane groups cover the K factor columns only and the item bias (column K) is carried as
 // a scalar per rating (fp32 K=128: one lane group instead of two -- half the vector work and the
 // registers of a bank of 8 rows)
-template <typename T, int G, bool HOT, bool SB = false>
-__global__ __launch_bounds__(kBlock) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS, int32_t *status,
-                                                             const uint8_t *hot)
+template <typename T, int G, bool HOT, bool SB = false, int H = kHxHelpers>
+__global__ __launch_bounds__(kWave * (1 + H)) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS,
+                                                                     int32_t *status,
+                                                                     const uint8_t *hot)
 {
-    __shared__ PPRing<T, G> ring;
+    __shared__ PPRing<T, G, H> ring;
     const int w = threadIdx.x / kWave;
     if (threadIdx.x == 0) {
         ring.head = 0;
         ring.done = 0;
-        for (int h = 0; h < kHxHelpers; ++h) ring.tail[h] = 0;
+        for (int h = 0; h < H; ++h) ring.tail[h] = 0;
     }
     __syncthreads();
     if (w == 0) {
-        epoch_body_pp_la<T, G, true, HOT, SB>(row_ptr, items, ratings, sched, n_sched, pu, bu,
-                                              ldu, qb, ldq, yj, elog, K, hp, n_items, n_waves_req,
-                                              0, &ring, status, hot);
+        epoch_body_pp_la<T, G, true, HOT, SB, H>(row_ptr, items, ratings, sched, n_sched, pu, bu,
+                                                 ldu, qb, ldq, yj, elog, K, hp, n_items,
+                                                 n_waves_req, 0, &ring, status, hot);
         if (blockIdx.x >= n_waves_req) lds_store(&ring.done, 1);  // (no chain in this workgroup)
     } else {
-        pp_ring_helper<T, G, SB>(&ring, w - 1, qb, ldq, (HOT ? 2 : 1) * n_items, status, K);
+        pp_ring_helper<T, G, SB, H>(&ring, w - 1, qb, ldq, (HOT ? 2 : 1) * n_items, status, K);
     }
 }
 
@@ -1742,7 +1745,7 @@ template <typename T, int M, bool PP>
 int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
-                    bool hx, double *psq, int err_col, int ck_ld, int32_t *status,
+                    int hx, double *psq, int err_col, int ck_ld, int32_t *status,
                     const uint8_t *hot, void *stream)
 {
     if ((psq || err_col) && (PP || M != kLog || !elog))
@@ -1771,11 +1774,14 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     return dispatch_g<T>(sb || sbk ? K : ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         if constexpr (PP && M == kAtomic && V <= kLaMaxG) {
-            if (hx) {  // one workgroup per chain: wave 0 trains, waves 1-3 issue the q atomics
-                auto kern = hot ? mf_svdpp_hx_kernel<T, V, true>
+            if (hx) {  // one workgroup per chain: wave 0 trains, waves 1..hx issue the q atomics
+                auto kern = hx == 1 ? (hot ? mf_svdpp_hx_kernel<T, V, true, false, 1>
+                                       : sb  ? mf_svdpp_hx_kernel<T, V, false, true, 1>
+                                             : mf_svdpp_hx_kernel<T, V, false, false, 1>)
+                          : hot ? mf_svdpp_hx_kernel<T, V, true>
                           : sb  ? mf_svdpp_hx_kernel<T, V, false, true>
                                 : mf_svdpp_hx_kernel<T, V, false>;
-                hipLaunchKernelGGL(kern, dim3(waves), dim3(kBlock), 0,
+                hipLaunchKernelGGL(kern, dim3(waves), dim3(kWave * (1 + hx)), 0,
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
                                    (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
@@ -1814,7 +1820,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
 }
 template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
-    void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, bool, double *,
+    void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, int, double *,
     int, int, int32_t *, const uint8_t *, void *);
 }  // namespace mf_ext
 #else  // the main translation unit
@@ -3564,7 +3570,11 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
                  const uint8_t *hot = nullptr)
 {
     const bool dups = flags & MF_EPOCH_DUP_ITEMS;
-    const bool hx = flags & MF_EPOCH_SVDPP_HELPERS;
+    // helper waves per chain: 3, or 1 (MF_EPOCH_SVDPP_ONE_HELPER); 0 = no helper-wave launch
+    const int hx = !(flags & MF_EPOCH_SVDPP_HELPERS) ? 0
+                   : (flags & MF_EPOCH_SVDPP_ONE_HELPER) ? 1 : kHxHelpers;
+    if ((flags & MF_EPOCH_SVDPP_ONE_HELPER) && !hx)
+        return set_err(MF_E_ARG, "MF_EPOCH_SVDPP_ONE_HELPER: with MF_EPOCH_SVDPP_HELPERS only");
     const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
     if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, mode, qlog, dtype)) return rc;
     if (int rc = check_xmask(xmask)) return rc;
@@ -3641,7 +3651,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 930; }
+int mf_version(void) { return 931; }
 
 #ifndef MF_SOURCE_HASH
 #define MF_SOURCE_HASH "unknown"

@@ -42,6 +42,12 @@ def _free_events(evs):
 PIECE_ROWS = 64  # log rows summed by one wave of mf_log_reduce
 SVDPP_WAVES_PER_CU = 4  # SVD++ without helper waves: users in flight per CU
 HX_CHAINS_PER_CU = 2  # SVD++ helper-wave launch: user chains per CU (1 / 3 / 4 measured slower)
+HX_CHAINS_PER_CU_ONE = 4  # ... with one helper wave per chain (workgroups of two waves)
+# helpers=None: one helper wave per chain and HX_CHAINS_PER_CU_ONE chains per CU where an
+# epoch-chunk holds at least this many users (C5 per-rank shard, 96k users per chunk: 93.9 ->
+# 90.4 ms/epoch); below it three helpers and HX_CHAINS_PER_CU (C3, 6040 users: 4 chains per CU
+# put more users on the popular rows at once, 0.577 -> 0.728 ms)
+HX_ONE_HELPER_MIN_USERS = 50_000
 
 
 # SVD++ (atomic q rows, deferred y): at most this many users (all ranks) per epoch-chunk.  Every
@@ -348,7 +354,7 @@ class MFEngine(ItemSync, Predictor):
                  user_order=None, n_waves=0, device=None, ld=None, world=1, merge=None,
                  ckpt=True, heavy=None, err_in_row=True, narrow=None, events="native",
                  join="event",
-                 helpers=True, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
+                 helpers=None, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
                  replay_rows=None):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
@@ -368,8 +374,10 @@ class MFEngine(ItemSync, Predictor):
                       complete them (mf_launch_event); "torch": torch.cuda.Event record / wait
           join        "event": the main stream waits for the side stream's event; "kernel": the
                       heavy replay's last block waits for the light replay (mf_launch_join)
-          helpers     SVD++ atomic mode: one user chain per workgroup whose q atomics three
-                      helper waves issue (MF_EPOCH_SVDPP_HELPERS)
+          helpers     SVD++ atomic mode: one user chain per workgroup whose q atomics helper
+                      waves issue (MF_EPOCH_SVDPP_HELPERS): True three helpers, 1 one helper
+                      per chain (MF_EPOCH_SVDPP_ONE_HELPER, HX_CHAINS_PER_CU_ONE chains per CU),
+                      None by the chunk size (HX_ONE_HELPER_MIN_USERS), False none
           ydefer      SVD++ atomic mode: the users' y updates folded per item after the chunk
                       (mf_svdpp_y_fold) instead of float atomics at each user's end
           hx_chains_per_cu  the helper-wave launch's user chains per CU (HX_CHAINS_PER_CU)
@@ -550,13 +558,24 @@ class MFEngine(ItemSync, Predictor):
         # q atomics the workgroup's other three waves issue (mf_svdpp_epoch flag
         # MF_EPOCH_SVDPP_HELPERS); the chains take users in a longest-first balanced layout
         self.dup_items = int(_has_duplicate_items(row_ptr, items))
-        self.hx = self.ydefer and self.ldq * esz <= 1024 and not self.dup_items and bool(helpers)
+        self.hx = self.ydefer and self.ldq * esz <= 1024 and not self.dup_items and \
+            (helpers is None or bool(helpers))
+        # helper waves per chain: 3 (helpers=True) or 1 (helpers=1: MF_EPOCH_SVDPP_ONE_HELPER);
+        # None: by the users per epoch-chunk (HX_ONE_HELPER_MIN_USERS)
+        if helpers is None:
+            big = max((len(c) for c in self.sched), default=0) >= HX_ONE_HELPER_MIN_USERS
+            self.hx_helpers = 1 if big else 3
+        else:
+            self.hx_helpers = 1 if helpers is not True and int(helpers) == 1 else 3
+        self._hx_flags = _lib.MF_EPOCH_SVDPP_HELPERS | (
+            _lib.MF_EPOCH_SVDPP_ONE_HELPER if self.hx_helpers == 1 else 0)
         self.hx_sched = []
         # the helper-wave launch's status word (mf_svdpp_epoch): checked in get_factors
         self._hx_status = torch.zeros(1, dtype=torch.int32, device=dev) if self.hx else None
         if self.hx:
             props = torch.cuda.get_device_properties(self.dev)
-            cpc = HX_CHAINS_PER_CU if hx_chains_per_cu is None else int(hx_chains_per_cu)
+            cpc = (HX_CHAINS_PER_CU if self.hx_helpers == 3 else HX_CHAINS_PER_CU_ONE) \
+                if hx_chains_per_cu is None else int(hx_chains_per_cu)
             self.hx_chains = max(1, cpc) * props.multi_processor_count
             for us in self.sched:
                 self.hx_sched.append(to_dev(chain_schedule(us.cpu().numpy(), row_ptr,
@@ -805,7 +824,7 @@ class MFEngine(ItemSync, Predictor):
         lx = (~self.heavy_xcd & 0xFF) if hv is not None and self.heavy_xcd else 0
         if self.hx:
             hs = self.hx_sched[c]
-            self._epoch(hs, hs.numel(), self.hx_chains, _lib.MF_EPOCH_SVDPP_HELPERS, st)
+            self._epoch(hs, hs.numel(), self.hx_chains, self._hx_flags, st)
             if self.hot_list is not None:
                 _lib.call("mf_svdpp_hot_fold", self._ptr(self.qb), self.ldq, self.n_items,
                           self._ptr(self.hot_list), self.hot_list.numel(), self.dtype, st)

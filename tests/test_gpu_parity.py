@@ -181,12 +181,13 @@ def test_svdpp_parallel_rmse_within_1e3(torch, golden, u1, name, mode):
 
 
 @pytest.mark.parametrize("opt", [{"helpers": False}, {"ydefer": False},
-                                 {"hx_chains_per_cu": 1}])
+                                 {"hx_chains_per_cu": 1}, {"helpers": 1}])
 def test_svdpp_atomic_alternatives_rmse_within_1e3(torch, golden, u1, opt):
     """SVD++'s non-default atomic-mode paths (MFEngine helpers=False: the chain wave issues its
     own q atomics; ydefer=False: y_j updated by float atomics at each user's end;
-    hx_chains_per_cu=1: one helper-wave chain per CU) within 1e-3 of the reference's held-out
-    RMSE, like the default."""
+    hx_chains_per_cu=1: one helper-wave chain per CU; helpers=1: one helper wave per chain,
+    4 chains per CU -- MF_EPOCH_SVDPP_ONE_HELPER) within 1e-3 of the reference's held-out RMSE,
+    like the default."""
     from surprise_amd import SVDpp
     meta, _ = golden
     case = meta["cases"]["svdpp_k20_e20"]
@@ -196,6 +197,10 @@ def test_svdpp_atomic_alternatives_rmse_within_1e3(torch, golden, u1, opt):
     algo.fit(ts)
     eng = algo._engine
     want = {"helpers": (False, True), "ydefer": (False, False), "hx_chains_per_cu": (True, True)}
+    if opt.get("helpers") == 1:
+        want["helpers"] = (True, True)
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        assert eng.hx_helpers == 1 and eng.hx_chains == 4 * cus
     assert (eng.hx, eng.ydefer) == want[next(iter(opt))]
     assert abs(_rmse(algo.test(test)) - case["rmse"]) < RMSE_TOL
 

@@ -29,16 +29,21 @@ for k in [int(x) for x in sys.argv[1:]] or [1]:
     rp_k = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     it_k = np.concatenate([it[rp[x]:rp[x + 1]] for x in users]).astype(np.int32)
     rt_k = np.concatenate([rt[rp[x]:rp[x + 1]] for x in users])
-    for algo, mode in (("svd", "log"), ("svdpp", "atomic")):
-        for dt in ("float32", "float64"):
+    variants = [("svd", "log", {}), ("svdpp", "atomic", {})]
+    if os.environ.get("CHAIN_PP_VARIANTS"):
+        variants = [("svdpp", "atomic", {}), ("svdpp", "atomic", {"helpers": False}),
+                    ("svdpp", "atomic", {"hot_rows": 0}),
+                    ("svdpp", "atomic", {"helpers": False, "hot_rows": 0})]
+    for algo, mode, kw in variants:
+        for dt in ("float32",) if kw else ("float32", "float64"):
             rng = np.random.RandomState(0)
             eng = MFEngine((rp_k, it_k, rt_k), ts.n_items, K, algo=algo, mode=mode, dtype=dt,
-                           hyper=bench.hyper_for(algo, float(ts.global_mean)))
+                           hyper=bench.hyper_for(algo, float(ts.global_mean)), **kw)
             eng.set_factors(rng.normal(0, .1, (k, K)), rng.normal(0, .1, (ts.n_items, K)),
                             yj=rng.normal(0, .1, (ts.n_items, K)) if algo == "svdpp" else None)
             eng._prepare(None)
             steps = 30
             sec, _ = bench.run_steps(eng, None, steps, 3, torch, instrument=False)
             us = sec / steps * 1e6
-            print("%-6s %-8s users %4d  max chain %4d  %8.1f us/epoch  %6.1f ns/rating"
+            print(kw, "%-6s %-8s users %4d  max chain %4d  %8.1f us/epoch  %6.1f ns/rating"
                   % (algo, dt, k, lens.max(), us, us * 1e3 / lens.max()), flush=True)
