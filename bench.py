@@ -81,6 +81,9 @@ def parse():
     p.add_argument("--replay-rows", type=int, default=0,
                    help="SVD checkpoint log: ratings per replay piece (0: the engine's policy, "
                         "engine.replay_piece_rows)")
+    p.add_argument("--heavy", type=float, default=-1,
+                   help="SVD checkpoint log: users in the heavy launch (MFEngine heavy; -1: the "
+                        "engine's policy)")
     p.add_argument("--hx-helpers", type=int, default=0,
                    help="SVD++ helper-wave launch: helper waves per chain, 3 or 1 (0: the "
                         "engine default)")
@@ -542,6 +545,7 @@ def main():
                        **({"merge": args.merge} if args.merge else {}),
                        **({"hx_chains_per_cu": args.hx_chains} if args.hx_chains else {}),
                        **({"helpers": args.hx_helpers} if args.hx_helpers else {}),
+                       **({"heavy": args.heavy} if args.heavy >= 0 else {}),
                        **({"hot_rows": args.hot_rows} if args.hot_rows >= 0 else {}),
                        **({"replay_rows": args.replay_rows} if args.replay_rows else {}))
         eng.set_factors(pu, qi, yj=yj)
