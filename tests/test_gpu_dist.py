@@ -69,8 +69,11 @@ def _same_on_every_rank(res, keys=("pu", "qi", "bu", "bi")):
             np.testing.assert_array_equal(r[k], res[0][k], err_msg=k)
 
 
-def test_two_ranks_log_mode_equals_one_gpu(torch, tmp_path):
-    res = _ranks(tmp_path, algo="SVD", mode="log")
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_n_ranks_log_mode_equals_one_gpu(torch, tmp_path, world):
+    """2 / 4 / 8 ranks (all on the box's GPU, gloo): the log schedule's multi-rank fold is one
+    GPU's arithmetic -- fp64 factors equal the single-GPU fit to 1e-9."""
+    res = _ranks(tmp_path, world=world, algo="SVD", mode="log")
     _same_on_every_rank(res)
     a, rmse = _single("SVD", "log")
     for k in ("pu", "qi", "bu", "bi"):
@@ -90,23 +93,25 @@ def test_two_ranks_atomic_mode_rmse_vs_reference(torch, tmp_path, golden, algo):
     assert abs(float(res[0]["rmse"]) - meta["cases"][name]["rmse"]) < 1e-3
 
 
-def test_two_ranks_svdpp_tracks_multirank_oracle(torch, tmp_path, golden):
-    """The GPU's 2-rank SVD++ schedule against the oracle's statement of the same rule
-    (oracle_svdpp_sgd_groups_merge, merge=2, merge_y=4) on u1, K=20, E=20, fp64."""
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_n_ranks_svdpp_tracks_multirank_oracle(torch, tmp_path, golden, world):
+    """The GPU's 2 / 4 / 8-rank SVD++ schedule (C5's path) against the oracle's statement of the
+    same rule (oracle_svdpp_sgd_groups_merge, merge=2, merge_y=4) on u1, K=20, E=20, fp64."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     from surprise_amd.dist import shard_users
-    res = _ranks(tmp_path, algo="SVDpp", mode="atomic", epochs=20)
+    res = _ranks(tmp_path, world=world, algo="SVDpp", mode="atomic", epochs=20)
+    _same_on_every_rank(res, ("pu", "qi", "bu", "bi", "yj"))
     ts, test = _u1()
     row_ptr, items, ratings = ts.csr()
     rng = np.random.RandomState(0)
     pu, qi, yj = orc.init_factors(rng, ts.n_users, ts.n_items, 20, with_yj=True)
     hp = orc.hyper(lr_bu=.007, lr_bi=.007, lr_pu=.007, lr_qi=.007, lr_yj=.007, reg_bu=.02,
                    reg_bi=.02, reg_pu=.02, reg_qi=.02, reg_yj=.02)
-    b = shard_users(row_ptr, 2)
+    b = shard_users(row_ptr, world)
     g = (np.searchsorted(b, np.arange(ts.n_users), side="right") - 1).astype(np.int32)
     pu, qi, yj, bu, bi = orc.svdpp_sgd_groups_merge(row_ptr, items, ratings, ts.n_items, 20, 20,
-                                                    ts.global_mean, hp, pu, qi, yj, g, 2)
+                                                    ts.global_mean, hp, pu, qi, yj, g, world)
     u = np.array([ts._raw2inner_id_users.get(x[0], -1) for x in test], np.int32)
     i = np.array([ts._raw2inner_id_items.get(x[1], -1) for x in test], np.int32)
     est = orc.svdpp_predict(u, i, row_ptr, items, 20, ts.global_mean, pu, qi, yj, bu, bi)
