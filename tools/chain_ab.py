@@ -47,6 +47,14 @@ for dt in ("float64", "float32"):
         t = timed(b)
         print("%-8s one launch, the top %4d users only: epoch kernel %.1f us (%.1f ns/rating of "
               "the top chain)" % (dt, k, t, t * 1e3 / deg[top]), flush=True)
+    ep = b._epoch_sq
+    for k, m in ((128, 0x01), (128, 0x03), (32, 0x01), (1, 0x01)):
+        b.logs[0]["sched"] = torch.tensor(np.sort(order[:k]), dtype=torch.int32, device="cuda")
+        b._epoch_sq = lambda s_, n, w, st, x=0, _m=m: ep(s_, n, n, st, _m)  # one wave per user
+        t = timed(b)
+        print("%-8s one launch, the top %4d users only, on XCD mask %#04x: epoch kernel %.1f us"
+              % (dt, k, m, t), flush=True)
+    b._epoch_sq = ep
     b.logs[0]["sched"] = full
     t = timed(b)
     print("%-8s one launch, every user: epoch kernel %.1f us" % (dt, t), flush=True)
