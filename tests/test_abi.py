@@ -80,3 +80,19 @@ def test_library_hash_is_the_committed_sources(lib):
     from surprise_amd import build
     assert lib.mf_source_hash().decode() == build.source_hash()
     assert build.embedded_hash() == build.source_hash()
+
+
+def test_python_constants_equal_the_header_defines():
+    """Every MF_* integer constant surprise_amd._lib mirrors equals its #define in
+    include/surprise_amd.h (flags such as MF_EPOCH_SVDPP_ONE_HELPER cross the ABI as ints)."""
+    import re
+    hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                       "surprise_amd.h")
+    defines = {m.group(1): int(m.group(2), 0) for m in
+               re.finditer(r"^#define\s+(MF_\w+)\s+(0x[0-9a-fA-F]+|\d+)\b", open(hdr).read(), re.M)}
+    mirrored = {k: v for k, v in vars(_lib).items() if k.startswith("MF_") and isinstance(v, int)}
+    assert mirrored, "no constants mirrored"
+    missing = sorted(k for k in mirrored if k not in defines)
+    assert not missing, missing
+    for k, v in mirrored.items():
+        assert defines[k] == v, (k, defines[k], v)
