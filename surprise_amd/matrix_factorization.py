@@ -235,10 +235,13 @@ class _MFBase(AlgoBase):
         lo, hi = ts.rating_scale
         est = np.fmax(lo, np.fmin(hi, est))  # algo_base.py:166-169 (NaN -> upper bound)
         reason = "User and item are unkown."
-        ok, bad = {"was_impossible": False}, {"was_impossible": True, "reason": reason}
         if isinstance(ruids, np.ndarray):  # (column-native testset: Python scalars, as listed)
             ruids, riids = ruids.tolist(), riids.tolist()
-        return [Prediction(a, b, c, e, dict(bad) if x else dict(ok))
+        # (Prediction is a namedtuple: tuple.__new__ is its _make without the length check; a
+        # fresh details dict per prediction, as the reference builds them)
+        new, P = tuple.__new__, Prediction
+        return [new(P, (a, b, c, e, {"was_impossible": True, "reason": reason} if x
+                        else {"was_impossible": False}))
                 for a, b, c, e, x in zip(ruids, riids, (r - ts.offset).tolist(), est.tolist(),
                                          impossible.tolist())]
 
