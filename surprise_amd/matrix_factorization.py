@@ -29,6 +29,7 @@ The fork's per-fit side effects in SVD.fit (:158-169: a print and an unused
 """
 from __future__ import annotations
 
+import gc
 import operator
 
 import numpy as np
@@ -239,11 +240,19 @@ class _MFBase(AlgoBase):
             ruids, riids = ruids.tolist(), riids.tolist()
         # (Prediction is a namedtuple: tuple.__new__ is its _make without the length check; a
         # fresh details dict per prediction, as the reference builds them)
+        # (the cyclic GC stays off while 2 x len(testset) containers are created: its passes
+        # over every live object would otherwise grow with the caller's heap)
         new, P = tuple.__new__, Prediction
-        return [new(P, (a, b, c, e, {"was_impossible": True, "reason": reason} if x
-                        else {"was_impossible": False}))
-                for a, b, c, e, x in zip(ruids, riids, (r - ts.offset).tolist(), est.tolist(),
-                                         impossible.tolist())]
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            return [new(P, (a, b, c, e, {"was_impossible": True, "reason": reason} if x
+                            else {"was_impossible": False}))
+                    for a, b, c, e, x in zip(ruids, riids, (r - ts.offset).tolist(),
+                                             est.tolist(), impossible.tolist())]
+        finally:
+            if was:
+                gc.enable()
 
     def test_metrics(self, testset):
         """(rmse, mae) of the model on a testset -- accuracy.rmse(algo.test(testset)) and
