@@ -283,7 +283,8 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
 #define MF_MERGE_COUNT 1 /* count-aware: SUM while a row's steps are small, count-weighted MEAN
                             once they saturate (item factors and biases)                           */
 #define MF_MERGE_MEAN  2 /* count-weighted MEAN: sum_r (n_r / N) d_r (SVD++ implicit factors)      */
-#define MF_MERGE_RECENCY 3 /* mf_log_apply: sums weighted by recency (mf_recency_t), the default  */
+#define MF_MERGE_RECENCY 3 /* mf_log_apply: sums weighted by recency (mf_recency_t), the default;
+                              mf_item_merge: each rank's delta decayed by the later ranks' steps */
 
 /*
  * Item-side merge of an epoch-chunk across ranks for MF_MODE_PLAIN /
@@ -297,7 +298,13 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
  *                   in column bias_col (-1: none) and eta = lr_qi (<pu^2> + reg_qi) in columns
  *                   < n_factors, <pu^2> being the mean squared entry of pu[:, :n_factors]
  *                   ([n_users][ldu], reduced on the device into `work`, 2 doubles of scratch);
- *   MF_MERGE_MEAN:  w_r(i) = n_r / N.
+ *   MF_MERGE_MEAN:  w_r(i) = n_r / N;
+ *   MF_MERGE_RECENCY (n_replicas 1; counts[i] = N_>r(i), the ratings of item i on the ranks after
+ *                   this one in the chunk, totals unused): w(i) = (1-eta)^{N_>r(i)}, eta as for
+ *                   MF_MERGE_COUNT -- the ranks' steps composed in rank order, each step decaying
+ *                   the row by (1 - eta) to first order, so rank r's delta is carried through the
+ *                   later ranks' steps (the reference applies them after it; SVD++'s multi-rank q
+ *                   / b merge, oracle_svdpp_sgd_groups_merge(merge=3)).
  * apply != 0: snap += delta and every replica := snap.  apply == 0: only delta_out is written
  * (the caller all-reduces it with RCCL SUM, then calls mf_item_apply).
  */

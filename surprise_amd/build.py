@@ -100,5 +100,24 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None, o
     return out
 
 
+# test builds: the product sources with a test switch (tests load them in a child process
+# through SURPRISE_AMD_LIB, after checking their embedded hash against source_hash(extra))
+TEST_VARIANTS = {
+    # the SVD++ helper-wave launch's bounded waits give up at once on request (status word bits
+    # 0x100 / 0x200): tests/test_gpu_ext.py forces MF_HX_HELPER_TIMEOUT / MF_HX_CHAIN_FALLBACK
+    "spintest": ("-DMF_HX_SPIN_TEST",),
+}
+VARIANT_DIR = os.path.join(_HERE, "variants")
+
+
+def variant_path(name: str) -> str:
+    return os.path.join(VARIANT_DIR, "libsurprise_amd_%s.so" % name)
+
+
+def build_test_variants(force: bool = False) -> list:
+    os.makedirs(VARIANT_DIR, exist_ok=True)
+    return [build(force=force, out=variant_path(n), extra=x) for n, x in TEST_VARIANTS.items()]
+
+
 if __name__ == "__main__":
     print(build(force=True, verbose=True))

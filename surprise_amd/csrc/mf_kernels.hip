@@ -1202,6 +1202,19 @@ template <int G>
 constexpr int hx_bank() { return G == 1 ? MF_PP_HX_BANK : MF_PP_HX_BANK_G2; }
 constexpr int kHxHelpers = 3;  // helper waves per chain (MF_EPOCH_SVDPP_ONE_HELPER: 1)
 constexpr int kSpinMax = 1 << 22;  // bounded spins (s_sleep 2 each, ~0.2 s): never hang the GPU
+// MF_HX_SPIN_TEST (a test build, tests/test_gpu_ext.py): bits of the status word set by the caller
+// before the launch make the bounded waits give up at once -- 0x100 the helpers' wait for rows,
+// 0x200 the chain's wait for ring room -- so the failure paths run on purpose
+#ifdef MF_HX_SPIN_TEST
+constexpr int32_t kSpinTestHelper = 0x100, kSpinTestChain = 0x200;
+__device__ __forceinline__ int spin_bound(const int32_t *status, int32_t bit) {
+    return status && (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)
+               ? 0 : kSpinMax;
+}
+#else
+constexpr int32_t kSpinTestHelper = 0, kSpinTestChain = 0;
+__device__ __forceinline__ int spin_bound(const int32_t *, int32_t) { return kSpinMax; }
+#endif
 
 template <typename T, int G, int H = kHxHelpers>
 struct PPRing {
@@ -1251,6 +1264,7 @@ __device__ void pp_ring_helper(PPRing<T, G, H> *ring, int h, T *qb, int ldq, int
     }
     const T *img = (const T *)&ring->data[0][0][0];
     constexpr int kSlotT = G * kWave * (int)(sizeof(typename Lane8<T>::vec) / sizeof(T));
+    const int spin_max = spin_bound(status, kSpinTestHelper);
     int t = 0, spins = 0;
     while (true) {
         int hd = lds_load(&ring->head);
@@ -1261,7 +1275,7 @@ __device__ void pp_ring_helper(PPRing<T, G, H> *ring, int h, T *qb, int ldq, int
                 if (t >= hd) break;
             } else {
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > kSpinMax) {  // (never hang the GPU: report and stop)
+                if (++spins > spin_max) {  // (never hang the GPU: report and stop)
                     set_status(status, kHxHelperTimeout);
                     break;
                 }
@@ -1344,6 +1358,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
     // bias, column K, rides beside the row as one wave-uniform element per rating
     const uint32_t kbo = (uint32_t)K * sizeof(T);
     int pushed = 0;  // HX: ratings pushed to the ring
+    const int chain_spins = HX ? spin_bound(status, kSpinTestChain) : 0;
     uint32_t cq[G], cu[G], cq1[U], cy1[U];
     vec one[G], lrp[G], ap[G], lry[G], lrpy[G], lrq[G], nrq[G];
     const T dc = T(1) - hp.lr_yj * hp.reg_yj;
@@ -1483,7 +1498,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
             if constexpr (HX) {  // ... handed to the helper waves through the ring
                 constexpr int R = PPRing<T, G, H>::R;
                 bool room = false;
-                for (int spins = 0; spins < kSpinMax; ++spins) {  // room for kB rows
+                for (int spins = 0; spins < chain_spins; ++spins) {  // room for kB rows
                     int m = lds_load(&ring->tail[0]);
 #pragma unroll
                     for (int h = 1; h < H; ++h) {
@@ -1967,11 +1982,12 @@ __global__ __launch_bounds__(kBlock) void user_sq_reduce_kernel(const double *__
 template <typename T>
 __global__ __launch_bounds__(kBlock) void item_merge_kernel(
     T *tab, T *snap, int n_items, int ld, int n_fac, int bias_col, int n_rep,
-    const int32_t *__restrict__ counts, const int32_t *__restrict__ totals, int mean,
+    const int32_t *__restrict__ counts, const int32_t *__restrict__ totals, int rule,
     double l1m_bias, double lr_fac, double reg_fac, const double *__restrict__ p2stat,
     T *__restrict__ delta, int apply)
 {
     const int64_t total = (int64_t)n_items * ld, stride = total;
+    const bool mean = rule == MF_MERGE_MEAN, rec = rule == MF_MERGE_RECENCY;
     double l1m_fac = 0;
     if (counts && !mean) l1m_fac = log1p(-lr_fac * (p2stat[0] / p2stat[1] + reg_fac));
     for (int64_t x = (int64_t)blockIdx.x * kBlock + threadIdx.x; x < total;
@@ -1983,12 +1999,14 @@ __global__ __launch_bounds__(kBlock) void item_merge_kernel(
                                  : (c == bias_col ? l1m_bias : (c < n_fac ? l1m_fac : 0.0)));
         const T s0 = snap[x];
         T acc = T(0);
-        const double N = counts ? (double)totals[i] : 0.0;
-        const double gN = l != 0.0 ? -expm1(N * l) : 0.0;
+        const double N = counts && !rec ? (double)totals[i] : 0.0;
+        const double gN = l != 0.0 && !rec ? -expm1(N * l) : 0.0;
         for (int r = 0; r < n_rep; ++r) {
             const T d = tab[r * stride + x] - s0;
             double w = 1.0;
-            if (l != 0.0) {
+            if (rec) {  // this rank's steps decayed by the later ranks' steps: (1 - eta)^{N_>r}
+                w = exp((double)counts[(int64_t)r * n_items + i] * l);
+            } else if (l != 0.0) {
                 const double n = (double)counts[(int64_t)r * n_items + i];
                 w = n > 0 ? (mean ? n / N : (n / N) * gN / -expm1(n * l)) : 0.0;
             }
@@ -3988,10 +4006,11 @@ int mf_item_merge(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
 {
     if (!tab || !snap || n_items < 0 || ld < 1 || n_replicas < 1)
         return set_err(MF_E_ARG, "bad item table");
-    if (rule < MF_MERGE_SUM || rule > MF_MERGE_MEAN) return set_err(MF_E_ARG, "bad merge rule");
+    if (rule < MF_MERGE_SUM || rule > MF_MERGE_RECENCY) return set_err(MF_E_ARG, "bad merge rule");
     if (rule == MF_MERGE_SUM) counts = nullptr;
     const int mean = rule == MF_MERGE_MEAN;
-    if (counts && !totals) return set_err(MF_E_ARG, "counted merge needs totals");
+    if (counts && !totals && rule != MF_MERGE_RECENCY)
+        return set_err(MF_E_ARG, "counted merge needs totals");
     if (counts && !mean && (!hp || !pu || !work || n_users < 1 || ldu < n_factors))
         return set_err(MF_E_ARG, "count-aware merge needs hp, pu, work");
     if (rule != MF_MERGE_SUM && !counts) return set_err(MF_E_ARG, "counted merge needs counts");
@@ -4019,12 +4038,12 @@ int mf_item_merge(void *tab, void *snap, int32_t n_items, int32_t ld, int32_t n_
     if (dtype == MF_F32)
         hipLaunchKernelGGL(item_merge_kernel<float>, dim3(g), dim3(kBlock), 0, st, (float *)tab,
                            (float *)snap, n_items, ld, n_factors, bias_col, n_replicas, counts,
-                           totals, mean, l1m_bias, lr_fac, reg_fac, (const double *)work,
+                           totals, rule, l1m_bias, lr_fac, reg_fac, (const double *)work,
                            (float *)delta_out, apply);
     else
         hipLaunchKernelGGL(item_merge_kernel<double>, dim3(g), dim3(kBlock), 0, st, (double *)tab,
                            (double *)snap, n_items, ld, n_factors, bias_col, n_replicas, counts,
-                           totals, mean, l1m_bias, lr_fac, reg_fac, (const double *)work,
+                           totals, rule, l1m_bias, lr_fac, reg_fac, (const double *)work,
                            (double *)delta_out, apply);
     return check_launch("item_merge_kernel");
 }

@@ -117,12 +117,14 @@ class DistContext:
         self.host_staged = self.backend == "gloo"
 
     @classmethod
-    def from_env(cls, backend: str | None = None):
+    def from_env(cls, backend: str | None = None, single_rank_group: bool = False):
         """Join (or reuse) the default process group described by torchrun's env vars and bind
-        this process to its GPU (LOCAL_RANK); None for a single-process run."""
+        this process to its GPU (LOCAL_RANK); None for a single-process run, unless
+        single_rank_group (a world of one rank: exercises the backend's collectives alone)."""
         import torch
         import torch.distributed as dist
-        if int(os.environ.get("WORLD_SIZE", "1")) <= 1 and not dist.is_initialized():
+        if (int(os.environ.get("WORLD_SIZE", "1")) <= 1 and not dist.is_initialized()
+                and not single_rank_group):
             return None
         if not dist.is_initialized():
             backend = backend or os.environ.get("SURPRISE_AMD_DIST_BACKEND", "nccl")

@@ -80,11 +80,13 @@ def default_ld(n_factors: int, dtype: int) -> int:
 ITEM_ROW_ALIGN = 64  # bytes
 
 
-def default_ldq(n_factors: int, dtype: int) -> int:
-    """Item row length: n_factors + the item-bias column + the constant column of the user bias
-    (the SVD log's lookahead body), padded to a 64-byte multiple."""
+def default_ldq(n_factors: int, dtype: int, user_bias_col: bool = False) -> int:
+    """Item row length: n_factors + the item-bias column [+ the constant column of the user bias,
+    read only by the SVD log's lookahead body: user_bias_col], padded to a 64-byte multiple.
+    (Reserving the extra column everywhere would push fp64 K=127 / fp32 K=255 rows past 1 KiB and
+    cost SVD++ its helper-wave launch there.)"""
     per = ITEM_ROW_ALIGN // (4 if dtype == _lib.MF_F32 else 8)
-    return -(-(n_factors + 2) // per) * per
+    return -(-(n_factors + 1 + int(bool(user_bias_col))) // per) * per
 
 
 def stable_argsort(keys):
@@ -398,7 +400,6 @@ class MFEngine(ItemSync, Predictor):
         self.K = int(n_factors)
         # (n_factors = 0 -- the biases alone, baseline_sgd -- still gets a non-empty user row)
         self.ld = int(ld) if ld else (default_ld(self.K, self.dtype) if self.K else 16)
-        self.ldq = default_ldq(self.K, self.dtype)
         row_ptr, items, ratings = csr
         row_ptr = np.asarray(row_ptr, np.int64)
         self.n_users = len(row_ptr) - 1
@@ -408,14 +409,16 @@ class MFEngine(ItemSync, Predictor):
         if self.deterministic:
             mode, n_chunks, n_waves = "plain", 1, 1
         self.mode = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
+        # (the user-bias column of the SVD log's lookahead body: that schedule's rows only)
+        self.ldq = default_ldq(self.K, self.dtype,
+                               user_bias_col=algo == "svd" and self.mode == _lib.MF_MODE_LOG)
         # item-side merge rule: the log fold weights each logged gradient by its recency
-        # (MF_MERGE_RECENCY); the snapshot-delta merges of the other modes (several
-        # ranks) by the count-aware rule
+        # (MF_MERGE_RECENCY); SVD++'s snapshot-delta merge of q / b across ranks
+        # carries each rank's delta through the later ranks' steps (mf_item_merge's
+        # MF_MERGE_RECENCY); other snapshot merges by the count-aware rule
         if merge is None:
-            merge = "recency" if self.mode == _lib.MF_MODE_LOG else "count"
-        if merge == "recency" and self.mode != _lib.MF_MODE_LOG:
-            raise ValueError("merge='recency' is the log schedule's fold (mode='log')")
-        self.recency = merge == "recency"
+            merge = "recency" if (self.mode == _lib.MF_MODE_LOG or algo == "svdpp") else "count"
+        self.recency = merge == "recency" and self.mode == _lib.MF_MODE_LOG
         self.n_chunks = max(1, int(n_chunks))
         if events not in ("native", "torch") or join not in ("event", "kernel"):
             raise ValueError("events must be 'native' or 'torch', join 'event' or 'kernel'")
@@ -719,7 +722,44 @@ class MFEngine(ItemSync, Predictor):
             self.qb_s.copy_(self.qb)
         if self.yj_s is not None:
             self.yj_s.copy_(self.yj)
+        if self._hx_status is not None:  # (a re-seeded model starts with a clean status word)
+            self._hx_status.zero_()
+            self._hx_seen = None
         self._sq_valid = False
+
+    def run_epochs(self, n_epochs, ctx=None, on_epoch=None):
+        """ItemSync.run_epochs + the SVD++ helper-wave status word read at every epoch boundary
+        without a sync: each epoch's end copies it to pinned host memory behind an event, and
+        the next epoch boundary reads the copy once its event has completed -- a helper that
+        timed out (lost q deltas) stops training within about an epoch instead of at
+        get_factors."""
+        if self._hx_status is None:
+            return ItemSync.run_epochs(self, n_epochs, ctx, on_epoch)
+
+        def boundary(epoch):
+            self._check_hx_status(block=False)
+            if on_epoch is not None:
+                on_epoch(epoch)
+        return ItemSync.run_epochs(self, n_epochs, ctx, boundary)
+
+    def _check_hx_status(self, block):
+        """Raise if a helper wave has reported MF_HX_HELPER_TIMEOUT; block=False reads only a copy
+        whose event has completed and starts the next copy."""
+        t = self.torch
+        seen = getattr(self, "_hx_seen", None)
+        if seen is not None and (block or seen[1].query()):
+            seen[1].synchronize()
+            if int(seen[0][0]) & _lib.MF_HX_HELPER_TIMEOUT:
+                raise _lib.SurpriseAMDError(
+                    "an SVD++ helper wave timed out waiting for q deltas and stopped: item "
+                    "updates were lost (mf_svdpp_epoch status)")
+            seen = None
+        if seen is None and not block:
+            host = t.empty(1, dtype=t.int32, pin_memory=True)
+            host.copy_(self._hx_status, non_blocking=True)
+            ev = t.cuda.Event()
+            ev.record(self.stream)
+            self._hx_seen = (host, ev)
 
     def get_factors(self, ctx=None):
         """Host fp64 copies (pu, qi, bu, bi, yj) with the padding columns dropped.  With ctx
@@ -729,7 +769,8 @@ class MFEngine(ItemSync, Predictor):
         if getattr(self, "_join_words", None) is not None and int(self._join_words[608]) != 0:
             raise _lib.SurpriseAMDError("the in-kernel join of the two replays timed out: the "
                                         "item folds since are invalid")
-        if getattr(self, "_hx_status", None) is not None and int(self._hx_status[0]) & 1:
+        if getattr(self, "_hx_status", None) is not None and \
+                int(self._hx_status[0]) & _lib.MF_HX_HELPER_TIMEOUT:
             raise _lib.SurpriseAMDError("an SVD++ helper wave timed out waiting for q deltas and "
                                         "stopped: item updates were lost (mf_svdpp_epoch status)")
         K = self.K
@@ -1000,13 +1041,21 @@ class MFEngine(ItemSync, Predictor):
         self._ctx = ctx
         self.totals = []
         self._pos0 = []
+        self._after = []  # (snapshot merge by recency: per chunk, the item counts of later ranks)
+        snap_rec = not self.is_log and self.merge_rule == "recency"
         for t in self._totals_local:
             tt = self.torch.from_numpy(t).to(self.dev)
             if ctx is not None and ctx.world > 1:
-                if self.recency:  # this rank's ratings of an item follow the earlier ranks'
+                if self.recency or snap_rec:
+                    # this rank's ratings of an item follow the earlier ranks' and precede the
+                    # later ranks'
                     every = ctx.all_gather_rows(tt[None].to(self.torch.int64),
                                                 [1] * ctx.world).cpu()
-                    self._pos0.append(every[:ctx.rank].sum(0).to(self.torch.int32).to(self.dev))
+                    to32 = lambda x: x.to(self.torch.int32).to(self.dev)
+                    if self.recency:
+                        self._pos0.append(to32(every[:ctx.rank].sum(0)))
+                    else:
+                        self._after.append(to32(every[ctx.rank + 1:].sum(0)))
                 ctx.all_reduce_sum(tt)
             self.totals.append(tt)
         self._yaff = []
@@ -1039,6 +1088,11 @@ class MFEngine(ItemSync, Predictor):
         if self.merge_rule == "count" and self.totals is None:
             self._prepare(None)
         return self.merge_rule == "count"
+
+    def _snap_rule(self):
+        """mf_item_merge's rule for the snapshot tables (several ranks, not the log)."""
+        return {"count": _lib.MF_MERGE_COUNT, "recency": _lib.MF_MERGE_RECENCY,
+                "sum": _lib.MF_MERGE_SUM}[self.merge_rule]
 
     def _log_rule(self):
         """mf_log_apply's merge rule."""
@@ -1089,11 +1143,10 @@ class MFEngine(ItemSync, Predictor):
 
     def _snap_tables(self):
         """(table, snapshot, ld, bias_col, rule) of the tables merged by snapshot deltas."""
-        count = self._count_rule()
+        self._count_rule()  # (prepares the counts)
         tabs = []
         if self.qb_s is not None:
-            tabs.append((self.qb, self.qb_s, self.ldq, self.K,
-                         _lib.MF_MERGE_COUNT if count else _lib.MF_MERGE_SUM))
+            tabs.append((self.qb, self.qb_s, self.ldq, self.K, self._snap_rule()))
         if self.yj_s is not None:
             # SVD++ implicit factors: the ranks' end-of-user affine maps composed in rank order
             # (mf_item_affine, dist.py)
@@ -1107,7 +1160,9 @@ class MFEngine(ItemSync, Predictor):
     def sync_items(self, ctx):
         """The chunk's item-side exchange: one rank folds locally; several ranks fill ONE packed
         buffer (the log sums, or q's and y's snapshot deltas side by side), SUM-all-reduce it
-        once (one RCCL collective per chunk, nothing serialised behind another) and apply it.
+        once and apply it: one RCCL collective per chunk (the checkpoint log's next <p^2> rides in
+        the buffer; the gradient log, ckpt=False, all-reduces its <p^2> at the chunk start -- a
+        second, 16-byte collective).
         self._sync_events (dict of "ar_begin" / "ar_end" torch events, set by bench.py's
         instrumented epochs) brackets the collective on the engine's stream."""
         if ctx is None or ctx.world == 1:
@@ -1166,8 +1221,10 @@ class MFEngine(ItemSync, Predictor):
                 x += 1
                 continue
             use_counts = rule != _lib.MF_MERGE_SUM
+            # (MF_MERGE_RECENCY: the item's ratings on the later ranks in place of n_r)
+            cnt = self._after[c] if rule == _lib.MF_MERGE_RECENCY else self.counts[c]
             _lib.call("mf_item_merge", self._ptr(tab), self._ptr(snap), self.n_items, ld, self.K,
-                      bias_col, 1, rule, self._ptr(self.counts[c]) if use_counts else None,
+                      bias_col, 1, rule, self._ptr(cnt) if use_counts else None,
                       self._ptr(self.totals[c]) if use_counts else None,
                       ctypes.byref(self._hyper),
                       ctypes.c_void_p(self.pu.data_ptr() +

@@ -1,13 +1,14 @@
 """Cross-validation harness around the hot path, mirroring
-surprise/model_selection/split.py (get_cv :44-55, KFold :58-122, PredefinedKFold
-:654-685) and surprise/model_selection/validation.py (cross_validate :29-142,
-fit_and_score :683-769).  ShuffleSplit / train_test_split / print_summary are not
-on the SVD path (out of scope) and are not mirrored.
+surprise/model_selection/split.py (get_cv :44-55, KFold :58-122, ShuffleSplit :422-540,
+train_test_split :543-576, PredefinedKFold :654-685) and
+surprise/model_selection/validation.py (cross_validate :29-142, fit_and_score :683-769,
+print_summary :772-811).
 
 Index logic is the reference's, so a fold built here holds the same ratings in
 the same order as the reference's fold for the same seed; array-native
 datasets (``RatingColumns``) are indexed without Python tuples.
 """
+import math
 import numbers
 import time
 
@@ -69,6 +70,67 @@ class KFold:
         return self.n_splits
 
 
+class ShuffleSplit:
+    """split.py:422-540: n_splits independent random (trainset, testset) splits.  test_size /
+    train_size: a float is a proportion (test rounded up, train down), an int a count, None the
+    complement of the other; permutations come from get_rng(random_state) (np.arange without
+    shuffle).  The trainset takes the first train_size ratings of the permutation, the testset
+    the next test_size."""
+
+    def __init__(self, n_splits=5, test_size=.2, train_size=None, random_state=None,
+                 shuffle=True):
+        if n_splits <= 0:
+            raise ValueError("n_splits = {0} should be strictly greater than 0.".format(n_splits))
+        if test_size is not None and test_size <= 0:
+            raise ValueError("test_size={0} should be strictly greater than 0".format(test_size))
+        if train_size is not None and train_size <= 0:
+            raise ValueError("train_size={0} should be strictly greater than 0".format(train_size))
+        self.n_splits = n_splits
+        self.test_size = test_size
+        self.train_size = train_size
+        self.random_state = random_state
+        self.shuffle = shuffle
+
+    def validate_train_test_sizes(self, test_size, train_size, n_ratings):
+        """(train count, test count) for n_ratings ratings; ValueError as the reference."""
+        for name, v in (("test_size", test_size), ("train_size", train_size)):
+            if v is not None and v >= n_ratings:
+                raise ValueError("{0}={1} should be less than the number of ratings {2}"
+                                 .format(name, v, n_ratings))
+        if np.asarray(test_size).dtype.kind == "f":
+            test_size = math.ceil(test_size * n_ratings)
+        if train_size is None:
+            train_size = n_ratings - test_size
+        elif np.asarray(train_size).dtype.kind == "f":
+            train_size = math.floor(train_size * n_ratings)
+        if test_size is None:
+            test_size = n_ratings - train_size
+        if train_size + test_size > n_ratings:
+            raise ValueError("The sum of train_size and test_size ({0}) should be smaller than "
+                             "the number of ratings {1}.".format(train_size + test_size,
+                                                                 n_ratings))
+        return int(train_size), int(test_size)
+
+    def split(self, data):
+        n = len(data.raw_ratings)
+        n_train, n_test = self.validate_train_test_sizes(self.test_size, self.train_size, n)
+        rng = get_rng(self.random_state)
+        for _ in range(self.n_splits):
+            perm = rng.permutation(n) if self.shuffle else np.arange(n)
+            yield (data.construct_trainset(_subset(data.raw_ratings, perm[:n_train])),
+                   data.construct_testset(_subset(data.raw_ratings,
+                                                  perm[n_train:n_train + n_test])))
+
+    def get_n_folds(self):
+        return self.n_splits
+
+
+def train_test_split(data, test_size=.2, train_size=None, random_state=None, shuffle=True):
+    """split.py:543-576: one ShuffleSplit split -> (trainset, testset)."""
+    return next(ShuffleSplit(n_splits=1, test_size=test_size, train_size=train_size,
+                             random_state=random_state, shuffle=shuffle).split(data))
+
+
 class PredefinedKFold:
     """split.py:654-685."""
 
@@ -126,9 +188,28 @@ def cross_validate(algo, data, measures=["rmse", "mae"], cv=None, return_train_m
     ret["fit_time"] = fit_times
     ret["test_time"] = test_times
     ret["num_tested"] = [num_tested for _ in fit_times]
-    if verbose:  # (the reference's print_summary table is not on the hot path)
-        for m, vals in test_measures.items():
-            print("{} (testset): mean {:1.4f} std {:1.4f}".format(m.upper(), np.mean(vals),
-                                                                  np.std(vals)))
+    if verbose:
+        print_summary(algo, measures, test_measures, train_measures, fit_times, test_times,
+                      cv.n_splits)
     return ret
+
+
+def print_summary(algo, measures, test_measures, train_measures, fit_times, test_times,
+                  n_splits):
+    """validation.py:772-811: the per-fold table cross_validate(verbose=True) prints."""
+    print("Evaluating {0} of algorithm {1} on {2} split(s).".format(
+        ", ".join(m.upper() for m in measures), algo.__class__.__name__, n_splits))
+    print()
+    fmt = "{:<18}" + "{:<8}" * (n_splits + 2)
+
+    def row(label, vals, f):
+        return fmt.format(label, *[f.format(v) for v in vals] +
+                          [f.format(np.mean(vals)), f.format(np.std(vals))])
+
+    lines = [fmt.format("", *["Fold {0}".format(i + 1) for i in range(n_splits)] +
+                        ["Mean", "Std"])]
+    lines += [row(k.upper() + " (testset)", v, "{:1.4f}") for k, v in test_measures.items()]
+    lines += [row(k.upper() + " (trainset)", v, "{:1.4f}") for k, v in train_measures.items()]
+    lines += [row("Fit time", fit_times, "{:.2f}"), row("Test time", test_times, "{:.2f}")]
+    print("\n".join(lines))
 

@@ -6,6 +6,12 @@ on the GPU box).
             SVD K=128, the reference loop restated (oracle_svd_sgd <- mf.pyx:241-262)
   c5shard   the first 1.25M users of configs[4]'s shape (every item: 1M; one of 8 ranks' share),
             SVD++ K=128 in the exact per-user form (oracle_svdpp_sgd_affine <- mf.pyx:463-498)
+  c5at8_cN  the same 1.25M users in C5@8's multi-rank schedule: split 8 ways by
+            dist.shard_users (bench.py --gpus 8), each rank's users dealt into N epoch-chunks by
+            dist.chunk_users, the ranks' q / b deltas merged by the count-aware rule and their y
+            maps composed in rank order (oracle_svdpp_sgd_groups_merge(merge=2, merge_y=4) -- the
+            GPU's multi-rank SVD++ rule, surprise_amd/dist.py).  N = 2 puts 625k users (78k per
+            rank) in a chunk: C5@8's chunk at 16 chunks per epoch over 10M users
 
 Same CSR, held-out triples, initial factors (init_tables), global mean and hyper-parameters as
 `bench.py --shape c4` / `--shape c5 --users 1250000` (imported from bench.py, not re-stated).
@@ -35,6 +41,27 @@ import oracle as orc  # noqa: E402
 OUT = os.path.join(HERE, "scale_golden.json")
 CASES = {"c4": dict(shape="c4", users=0, algo="svd", K=128),
          "c5shard": dict(shape="c5", users=1_250_000, algo="svdpp", K=128)}
+for _n in (2, 4, 8):
+    CASES["c5at8_c%d" % _n] = dict(shape="c5", users=1_250_000, algo="svdpp", K=128, groups=8,
+                                   chunks=_n)
+
+
+def group_schedule(row_ptr, groups, chunks):
+    """(group_of_user, chunk_of_user) of bench.py --gpus `groups` --chunks `chunks`: contiguous
+    user ranges of equal rating count (dist.shard_users), each rank's users dealt into its
+    epoch-chunks by dist.chunk_users on rank-local ids (MFEngine's chunking)."""
+    from surprise_amd.dist import chunk_users, shard_users
+    n = len(row_ptr) - 1
+    b = shard_users(row_ptr, groups)
+    g_of = np.zeros(n, np.int32)
+    c_of = np.zeros(n, np.int32)
+    for g in range(groups):
+        lo, hi = int(b[g]), int(b[g + 1])
+        g_of[lo:hi] = g
+        loc = np.asarray(row_ptr[lo:hi + 1], np.int64) - int(row_ptr[lo])
+        for c, us in enumerate(chunk_users(np.arange(hi - lo), loc, chunks)):
+            c_of[lo + np.asarray(us, np.int64)] = c
+    return g_of, c_of
 
 
 def main():
@@ -57,9 +84,18 @@ def main():
     print("%s: %s (%.0fs)" % (a.case, desc, time.time() - t0), flush=True)
     bu, bi = np.zeros(len(row_ptr) - 1), np.zeros(n_items)
     curve, secs = [], []
+    groups = c.get("groups")
+    if groups:
+        g_of, c_of = group_schedule(row_ptr, groups, c["chunks"])
     for e in range(a.epochs):
         t1 = time.time()
-        if svdpp:
+        if groups:
+            pu, qi, yj, bu, bi = orc.svdpp_sgd_groups_merge(
+                row_ptr, items, ratings, n_items, K, 1, gm, hp, pu, qi, yj, g_of, groups, c_of,
+                c["chunks"], merge=2, merge_y=4, bu=bu, bi=bi)
+            est = orc.svdpp_predict(tu, ti, row_ptr, items, K, gm, pu, qi, yj, bu, bi)
+            imp = np.zeros(len(tu), bool)
+        elif svdpp:
             pu, qi, yj, bu, bi = orc.svdpp_sgd(row_ptr, items, ratings, n_items, K, 1, gm, hp,
                                                pu, qi, yj, bu, bi, affine=True)
             est = orc.svdpp_predict(tu, ti, row_ptr, items, K, gm, pu, qi, yj, bu, bi)
@@ -78,7 +114,9 @@ def main():
         "data_fingerprint": bench.data_fingerprint(csr, (tu, ti, tr)),
         "rmse_by_epoch": curve,
         "global_mean_rmse": orc.rmse(tr, np.full(len(tr), gm)),
-        "oracle": ("oracle_svdpp_sgd_affine (mf.pyx:463-498)" if svdpp
+        "oracle": (("oracle_svdpp_sgd_groups_merge(merge=2, merge_y=4): %d ranks x %d epoch-"
+                    "chunks, per-user affine form inside a rank" % (groups, c["chunks"]))
+                   if groups else "oracle_svdpp_sgd_affine (mf.pyx:463-498)" if svdpp
                    else "oracle_svd_sgd (mf.pyx:241-262)") + ", fp64, one host thread",
         "oracle_seconds_per_epoch": float(np.mean(secs)),
         "generator": "tests/golden/make_scale_golden.py %s --epochs %d" % (a.case, a.epochs),

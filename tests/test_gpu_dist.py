@@ -96,7 +96,8 @@ def test_two_ranks_atomic_mode_rmse_vs_reference(torch, tmp_path, golden, algo):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_n_ranks_svdpp_tracks_multirank_oracle(torch, tmp_path, golden, world):
     """The GPU's 2 / 4 / 8-rank SVD++ schedule (C5's path) against the oracle's statement of the
-    same rule (oracle_svdpp_sgd_groups_merge, merge=2, merge_y=4) on u1, K=20, E=20, fp64."""
+    same rule (oracle_svdpp_sgd_groups_merge, merge=3: q / b deltas carried through the later
+    ranks' steps; merge_y=4) on u1, K=20, E=20, fp64."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     from surprise_amd.dist import shard_users
@@ -111,7 +112,8 @@ def test_n_ranks_svdpp_tracks_multirank_oracle(torch, tmp_path, golden, world):
     b = shard_users(row_ptr, world)
     g = (np.searchsorted(b, np.arange(ts.n_users), side="right") - 1).astype(np.int32)
     pu, qi, yj, bu, bi = orc.svdpp_sgd_groups_merge(row_ptr, items, ratings, ts.n_items, 20, 20,
-                                                    ts.global_mean, hp, pu, qi, yj, g, world)
+                                                    ts.global_mean, hp, pu, qi, yj, g, world,
+                                                    merge=3, merge_y=4)
     u = np.array([ts._raw2inner_id_users.get(x[0], -1) for x in test], np.int32)
     i = np.array([ts._raw2inner_id_items.get(x[1], -1) for x in test], np.int32)
     est = orc.svdpp_predict(u, i, row_ptr, items, 20, ts.global_mean, pu, qi, yj, bu, bi)
@@ -158,3 +160,24 @@ def test_bench_two_ranks_spawned(torch):
     assert r["roofline"]["dominant_kernel"]["kernel"] == "mf_ckpt_epoch_kernel"
     assert r["roofline"]["phases_gpu_ms"]["allreduce_ms_per_chunk"] > 0
     assert r["rmse"]["gpu"] < r["rmse"]["global_mean_baseline"]
+
+
+def test_rccl_single_rank_collectives(torch, tmp_path):
+    """The RCCL path (backend "nccl", device-resident collectives -- DistContext's
+    non-host-staged branches) before the driver's 8-GPU run needs it: a world-size-1 process group
+    joined through DistContext.from_env in a fresh child process; all_reduce_sum (fp32 / fp64),
+    all_reduce_max, broadcast, all_gather_rows and check_agreement on device tensors, then an
+    engine fit carrying the context.  (RCCL refuses two ranks on one GPU: the multi-rank merges
+    are rehearsed over gloo above.)"""
+    out = str(tmp_path / "rccl.json")
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", LOCAL_WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run([sys.executable, os.path.join(HERE, "_rccl_worker.py"), out], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.load(open(out))
+    assert r["backend"] == "nccl" and r["world"] == 1 and r["rank"] == 0
+    assert r["host_staged"] is False
+    assert r["sum_float32"] and r["sum_float64"]
+    assert r["max"] == [3, -7, 11] and r["broadcast"] == [2.5] * 5
+    assert r["gather_equal"] and r["agreement"] and r["engine_finite"]

@@ -11,8 +11,9 @@ Tolerances:
   * every parallel schedule ("log" = auto, "atomic"): held-out RMSE within 1e-3 of the
     reference on the same seed -- the bar BASELINE.json's north_star sets.  The exception is
     svd_k100_e20_unbiased (reference RMSE 2.28: the unbiased K=100 model diverges on u1, and
-    any parallel order moves it by > 1e-2 -- measured with the oracle alone); there
-    the log kernel is held to its oracle instead.
+    the log schedule moves it by +5.5e-2 -- its CPU oracle alone does the same, DESIGN.md 5);
+    there the log kernel is held to its oracle, the delta is recorded with an explicit bound
+    and the deterministic mode meets the reference.
 """
 import os
 import pickle
@@ -132,6 +133,24 @@ def test_log_mode_long_runs_track_deltalog_oracle(torch, golden, u1, name):
     got32 = _rmse(SVD(**case["params"]).fit(ts).test(test))
     assert abs(got64 - ref) < 1e-6, (got64, ref)
     assert abs(got32 - ref) < 1e-4, (got32, ref)
+
+
+def test_unbiased_k100_u1_delta_against_reference_is_recorded(torch, golden, u1):
+    """svd_k100_e20_unbiased (mf.pyx:238-239, 253-255: no biases, mu = 0): the reference's
+    held-out RMSE is 2.2754 -- the model diverges on u1 (the global mean alone scores 1.137).
+    The default parallel schedule ends +5.5e-2 from it: it does NOT meet the 1e-3 bar here
+    (DESIGN.md 5); its CPU restatement (oracle_svd_sgd_deltalog, merge=3) ends at the same
+    +5.51e-2, so the schedule, not the kernel, moves the diverging model.  The delta is bounded
+    so a change is visible; the deterministic mode (one wave, the reference's order) meets the
+    reference to 1e-6 in fp64."""
+    from surprise_amd import SVD
+    meta, _ = golden
+    case = meta["cases"]["svd_k100_e20_unbiased"]
+    ts, test = u1
+    delta = _rmse(SVD(**case["params"], dtype="float64").fit(ts).test(test)) - case["rmse"]
+    assert 0.050 < delta < 0.060, delta
+    exact = _rmse(SVD(**case["params"], dtype="float64", deterministic=True).fit(ts).test(test))
+    assert abs(exact - case["rmse"]) < 1e-6, exact
 
 
 def test_log_mode_is_bit_reproducible(torch, u1):
@@ -338,15 +357,47 @@ def test_c2_ml1m_svd_k100_e20_rmse_within_1e3(torch, ml1m, mode):
 
 
 @pytest.mark.slow
-def test_c3_ml1m_svdpp_k100_rmse_within_1e3(torch, ml1m):
+def test_headline_configuration_fp64_matches_deltalog_oracle(torch, ml1m):
+    """The bench headline's own kernel configuration at factor level: SVD K=100 in fp64 on the
+    ML-1M-shape fold through the default path, which at this size splits every epoch into the
+    128 heaviest users' launch on XCD 0 beside the other users' on XCDs 1-7, each with its own
+    checkpoint replay, both groups' piece sums folded by one mf_log_apply (the split u1 is too
+    small to take).  pu, qi, bu, bi after 3 epochs equal oracle_svd_sgd_deltalog(merge=3) -- the
+    schedule restated on the CPU, pinned to the reference by the u1 goldens -- to 1e-9."""
+    from surprise_amd import SVD
+    ts, test = ml1m
+    params = dict(n_factors=100, n_epochs=3, random_state=0)
+    algo = SVD(**params, dtype="float64").fit(ts)
+    eng = algo._engine
+    assert eng.ckpt and eng.logs[0]["heavy"] is not None, "the heavy/light split is off"
+    assert eng.logs[0]["heavy"]["sched"].numel() == eng.HEAVY_USERS
+    assert eng.heavy_xcd == 1, "the XCD-masked launches are off"
+    row_ptr, items, ratings = ts.csr()
+    P, f = run_oracle_log("SVD", params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
+                          merge=3)
+    for k in ("pu", "qi", "bu", "bi"):
+        np.testing.assert_allclose(getattr(algo, k), f[k], rtol=0, atol=1e-9, err_msg=k)
+    ref = _oracle_test_rmse(P, f, "SVD", ts, list(test))[1]
+    assert abs(_rmse(algo.test(test)) - ref) < 1e-9
+
+
+_C3_REF = {}
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("dtype", ["float32", "float64"])
+def test_c3_ml1m_svdpp_k100_rmse_within_1e3(torch, ml1m, dtype):
     """BASELINE configs[2]: SVD++ n_factors=100 on the ML-1M shape at the reference's default 20
-    epochs (mf.pyx:389-411); the oracle is the exact per-user affine form of SVDpp.sgd in fp64
-    (pinned bit-for-bit to the literal form on u1, tests/test_oracle_golden.py)."""
+    epochs (mf.pyx:389-411), in the product's fp32 and in the reference's fp64 arithmetic; the
+    oracle is the exact per-user affine form of SVDpp.sgd in fp64 (pinned bit-for-bit to the
+    literal form on u1, tests/test_oracle_golden.py)."""
     from surprise_amd import SVDpp
     ts, test = ml1m
     params = dict(n_factors=100, n_epochs=20, random_state=0)
-    ref = _oracle_rmse("SVDpp", params, ts, test, affine=True)
-    got = _rmse(SVDpp(**params).fit(ts).test(test))
+    if "ref" not in _C3_REF:
+        _C3_REF["ref"] = _oracle_rmse("SVDpp", params, ts, test, affine=True)
+    ref = _C3_REF["ref"]
+    got = _rmse(SVDpp(**params, dtype=dtype).fit(ts).test(test))
     assert abs(got - ref) < RMSE_TOL, (got, ref)
 
 

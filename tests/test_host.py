@@ -355,3 +355,121 @@ def test_testset_columns_list_and_column_native():
     su, si, sr = a._columns(st)
     assert su.tolist() == ru and si.tolist() == ri and sr.tolist() == r.tolist()
     assert a._columns([])[2].shape == (0,)
+
+
+# ------------------------------------------------------------------ fcp / ShuffleSplit /
+# train_test_split / print_summary (the reference's tests: test_accuracy.py:49-69,
+# test_split.py:94-229, validation.py:772-811)
+
+def _pred(true_r, est, u0=None):
+    return u0, None, true_r, est, None
+
+
+def test_fcp_known_answers():
+    """test_accuracy.py:49-69."""
+    preds = [_pred(0, 0, "u1"), _pred(1, 1, "u1"), _pred(2, 2, "u2"), _pred(100, 100, "u2")]
+    assert accuracy.fcp(preds, verbose=False) == 1
+    with pytest.raises(ValueError):
+        accuracy.fcp([_pred(0, 0, "u1"), _pred(0, 0, "u1")], verbose=False)
+    with pytest.raises(ValueError):
+        accuracy.fcp([_pred(0, 0, "u1")], verbose=False)
+    preds = [_pred(1, 0, "u1"), _pred(0, 1, "u1"), _pred(2, 0, "u2"), _pred(0, 2, "u2")]
+    assert accuracy.fcp(preds, verbose=False) == 0
+    with pytest.raises(ValueError):
+        accuracy.fcp([])
+    # the reference's means run over the users with at least one pair of each kind
+    preds = [_pred(1, 1, "a"), _pred(2, 2, "a"), _pred(3, 3, "a"),
+             _pred(1, 2, "b"), _pred(2, 1, "b")]
+    assert accuracy.fcp(preds, verbose=False) == 3 / (3 + 1)
+
+
+def test_cross_validate_fcp_measure_resolves(u1):
+    """fit_and_score resolves measures by name (validation.py:754-756): 'fcp' is one of them."""
+    from surprise_amd.model_selection import fit_and_score
+
+    class ByItem(AlgoBase):
+        def fit(self, trainset):
+            AlgoBase.fit(self, trainset)
+            return self
+
+        def estimate(self, u, i):
+            return 1.0 + (i % 5 if isinstance(i, int) else 0)
+
+    ts, test = u1
+    m = fit_and_score(ByItem(), ts, list(test), ["rmse", "fcp"])[0]
+    assert set(m) == {"rmse", "fcp"} and 0 < m["fcp"] < 1
+
+
+def _custom_data():
+    return Dataset.load_from_file(os.path.join(GOLDEN, "custom_dataset"),
+                                  Reader(line_format="user item rating", sep=" ", skip_lines=3,
+                                         rating_scale=(1, 5)))
+
+
+def test_shuffle_split_like_reference():
+    """test_split.py:94-178 on the reference's custom_dataset (5 ratings)."""
+    from surprise_amd.model_selection import ShuffleSplit
+    data = _custom_data()
+    with pytest.raises(ValueError):
+        ShuffleSplit(n_splits=0)
+    for kw in (dict(test_size=10), dict(train_size=10), dict(test_size=3, train_size=3)):
+        with pytest.raises(ValueError):
+            next(ShuffleSplit(**kw).split(data))
+    for kw in (dict(test_size=3, train_size=0), dict(test_size=0, train_size=3)):
+        with pytest.raises(ValueError):
+            ShuffleSplit(**kw)
+    next(ShuffleSplit(test_size=1, train_size=1).split(data))
+    for kw, n_test, n_train in ((dict(test_size=1), 1, 4), (dict(test_size=.2), 1, 4),
+                                (dict(test_size=2, train_size=2), 2, 2),
+                                (dict(test_size=None, train_size=2), 3, 2),
+                                (dict(test_size=None, train_size=.2), 4, 1), ({}, 1, 4)):
+        splits = list(ShuffleSplit(**kw).split(data))
+        assert all(len(te) == n_test and tr.n_ratings == n_train for tr, te in splits), kw
+    assert len(list(ShuffleSplit().split(data))) == 5
+    ss = ShuffleSplit(random_state=None)
+    assert [te for _, te in ss.split(data)] != [te for _, te in ss.split(data)]
+    for ss in (ShuffleSplit(random_state=1), ShuffleSplit(random_state=1, shuffle=False)):
+        assert [te for _, te in ss.split(data)] == [te for _, te in ss.split(data)]
+    # index logic: the permutation's first train_size ratings train, the next test_size test
+    tr, te = next(ShuffleSplit(n_splits=1, test_size=2, train_size=2, random_state=7)
+                  .split(data))
+    perm = np.random.RandomState(7).permutation(5)
+    assert te == [data.raw_ratings[i][:3] for i in perm[2:4]]
+    assert sorted(r for _, _, r in tr.all_ratings()) == sorted(
+        data.raw_ratings[i][2] + tr.offset for i in perm[:2])
+
+
+def test_train_test_split_like_reference():
+    """test_split.py:181-229."""
+    from surprise_amd.model_selection import train_test_split
+    data = _custom_data()
+    for kw, n_test, n_train in ((dict(test_size=2, train_size=None), 2, 3),
+                                (dict(test_size=.2, train_size=None), 1, 4),
+                                (dict(test_size=2, train_size=3), 2, 3),
+                                (dict(test_size=None, train_size=2), 3, 2),
+                                (dict(test_size=None, train_size=.2), 4, 1)):
+        tr, te = train_test_split(data, **kw)
+        assert len(te) == n_test and tr.n_ratings == n_train, kw
+    # random_state=None: the global numpy RNG moves on between calls (a single 1-rating testset
+    # repeats with probability 1/5, so compare a few draws)
+    draws = [train_test_split(data, random_state=None)[1] for _ in range(8)]
+    assert any(d != draws[0] for d in draws[1:])
+    assert train_test_split(data, random_state=1)[1] == train_test_split(data, random_state=1)[1]
+    assert train_test_split(data, random_state=1, shuffle=None)[1] == \
+        train_test_split(data, random_state=1, shuffle=None)[1]
+
+
+def test_print_summary_table(capsys):
+    from surprise_amd.model_selection import print_summary
+    print_summary(SVD(), ["rmse", "mae"], {"rmse": np.array([1.0, 0.5]),
+                                           "mae": np.array([0.8, 0.6])},
+                  {}, (1.0, 3.0), (0.25, 0.75), 2)
+    out = capsys.readouterr().out.splitlines()
+    assert out[0] == "Evaluating RMSE, MAE of algorithm SVD on 2 split(s)."
+    assert out[1] == ""
+    assert out[2].split() == ["Fold", "1", "Fold", "2", "Mean", "Std"]
+    assert out[3].split() == ["RMSE", "(testset)", "1.0000", "0.5000", "0.7500", "0.2500"]
+    assert out[4].split() == ["MAE", "(testset)", "0.8000", "0.6000", "0.7000", "0.1000"]
+    assert out[5].split() == ["Fit", "time", "1.00", "3.00", "2.00", "1.00"]
+    assert out[6].split() == ["Test", "time", "0.25", "0.75", "0.50", "0.25"]
+    assert out[3].index("1.0000") == 18  # '{:<18}' label column, '{:<8}' per value

@@ -369,10 +369,12 @@ def _groups_of(row_ptr, world):
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("name", ["svdpp_k20_e20", "svdpp_k100_e20"])
-def test_svdpp_multirank_rule_within_1e3_of_reference(golden, u1, world, name):
+@pytest.mark.parametrize("merge", [2, 3])
+def test_svdpp_multirank_rule_within_1e3_of_reference(golden, u1, world, name, merge):
     """The SVD++ multi-rank schedule of the GPU path (dist.py): users sharded by contiguous
-    rating-balanced ranges, q/b by the count-aware merge, y_j by the affine composition of the
-    ranks' end-of-user maps in rank order (merge_y=4) -- within the north-star 1e-3 of the
+    rating-balanced ranges, q/b by the rank-order composition (merge=3, the product's rule) or
+    the count-aware merge (2, round 3's), y_j by the affine composition of the ranks'
+    end-of-user maps in rank order (merge_y=4) -- within the north-star 1e-3 of the
     reference's RMSE (golden) at 2, 4 and 8 ranks."""
     meta, _ = golden
     case = meta["cases"][name]
@@ -383,10 +385,45 @@ def test_svdpp_multirank_rule_within_1e3_of_reference(golden, u1, world, name):
                                   P.init_mean, P.init_std_dev, with_yj=True)
     pu, qi, yj, bu, bi = orc.svdpp_sgd_groups_merge(
         row_ptr, items, ratings, ts.n_items, P.n_factors, P.n_epochs, ts.global_mean,
-        orc.svd_hyper(P), pu, qi, yj, _groups_of(row_ptr, world), world, merge=2, merge_y=4)
+        orc.svd_hyper(P), pu, qi, yj, _groups_of(row_ptr, world), world, merge=merge,
+        merge_y=4)
     f = dict(pu=pu, qi=qi, yj=yj, bu=bu, bi=bi)
     rmse = _oracle_test_rmse(P, f, "SVDpp", ts, list(test))[1]
     assert abs(rmse - case["rmse"]) < 1e-3, (world, rmse, case["rmse"])
+
+
+def test_svdpp_rank_order_q_merge_composes_the_ranks_steps(u1):
+    """merge=3 restated: each group's chunk alone (the oracle with only that group's users
+    active) moves q / b from the chunk start x_s to x_g; the merged row is
+    x_s + sum_g (1 - eta)^{N_>g} (x_g - x_s), N_>g = the item's ratings in later groups,
+    eta = lr_qi (<pu^2> + reg_qi) for q (<pu^2> over every user at the chunk start) and
+    lr_bi (1 + reg_bi) for b."""
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    K, n_items, G = 6, ts.n_items, 3
+    rng = np.random.RandomState(5)
+    pu, qi, yj = orc.init_factors(rng, ts.n_users, n_items, K, with_yj=True)
+    hp = orc.hyper(lr_bu=.007, lr_bi=.007, lr_pu=.007, lr_qi=.007, lr_yj=.007, reg_bu=.02,
+                   reg_bi=.02, reg_pu=.02, reg_qi=.02, reg_yj=.02)
+    g_of = _groups_of(row_ptr, G)
+    got = orc.svdpp_sgd_groups_merge(row_ptr, items, ratings, n_items, K, 1, ts.global_mean, hp,
+                                     pu.copy(), qi.copy(), yj.copy(), g_of, G, merge=3,
+                                     merge_y=4)
+    user_of = np.repeat(np.arange(ts.n_users), np.diff(row_ptr))
+    eta_q = .007 * ((pu ** 2).mean() + .02)
+    eta_b = .007 * (1 + .02)
+    want_q, want_b = qi.copy(), np.zeros(n_items)
+    for g in range(G):
+        alone = np.where(g_of == g, 0, -1).astype(np.int32)  # (other users: no chunk)
+        x = orc.svdpp_sgd_groups_merge(row_ptr, items, ratings, n_items, K, 1, ts.global_mean,
+                                       hp, pu.copy(), qi.copy(), yj.copy(),
+                                       np.zeros(ts.n_users, np.int32), 1, alone, 1, merge=0,
+                                       merge_y=4)
+        later = np.bincount(items[g_of[user_of] > g], minlength=n_items)
+        want_q += (1 - eta_q) ** later[:, None] * (x[1] - qi)
+        want_b += (1 - eta_b) ** later * x[4]
+    np.testing.assert_allclose(got[1], want_q, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(got[4], want_b, rtol=0, atol=1e-12)
 
 
 def test_svdpp_affine_rule_one_group_composes_in_user_order(u1):
