@@ -104,6 +104,8 @@ def parse():
     p.add_argument("--no-rmse", action="store_true")
     p.add_argument("--no-svdpp", action="store_true", help="skip the SVD++ C3 leg")
     p.add_argument("--no-predict", action="store_true", help="skip the batched test() leg")
+    p.add_argument("--no-c4", action="store_true",
+                   help="skip the C4 leg (BASELINE configs[3]'s shape on this GPU)")
     p.add_argument("--users", type=int, default=0,
                    help="c4 / c5: train only the first N users of the shape (a user-prefix "
                         "subsample that keeps every item; 0 = all)")
@@ -275,20 +277,31 @@ def run_steps(eng, ctx, steps, warmup, torch, instrument=True):
         phases.update({"pre_ms": span("begin", "start") * n, "epoch_kernel_ms": span("start", "end") * n,
                   "replay_ms": span("end", "end_r") * n, "fold_sync_ms": span("end_r", "done") * n,
                   "step_gpu_ms": span("begin", "done") * n, "instrumented_steps": len(recs) // n})
-        # the epoch kernel's launches (the dominant kernel): each one's span on its own stream
-        # and the ratings it trains -- roofline_of's per-launch figures
-        launches = []
+        # the epoch kernel (the dominant kernel): each launch's span on its own stream, the
+        # ratings it trains, and the kernel's wall span per chunk -- its launches of a split chunk
+        # (heavy users on the main stream, the rest on the side stream) run concurrently, so
+        # the span is from the first launch's start to the last one's end
+        per_launch, spans = {}, []
         for e in recs:
             n_r = eng.epoch_launch_ratings(e["chunk"])
-            spans = [e["start"].elapsed_time(e["end"])]
+            t_main = e["start"].elapsed_time(e["end"])
             if len(n_r) > 1:
-                spans.append(e["l_start"].elapsed_time(e["l_end"]))
-            launches += list(zip(spans, n_r))
-        phases["epoch_launches"] = {"per_step": len(launches) / max(len(recs) // n, 1),
-                                    "avg_us": float(np.mean([t for t, _ in launches])) * 1e3,
-                                    "avg_ratings": float(np.mean([r for _, r in launches])),
-                                    "ms_and_ratings": [[round(t, 4), r] for t, r in
-                                                       launches[:2 * n]]}
+                t0 = e["start"].elapsed_time(e["l_start"])
+                t1 = e["start"].elapsed_time(e["l_end"])
+                per_launch.setdefault("heavy", []).append((t_main, n_r[0]))
+                per_launch.setdefault("light", []).append((t1 - t0, n_r[1]))
+                spans.append((max(t_main, t1) - min(0.0, t0), sum(n_r)))
+            else:
+                per_launch.setdefault("all", []).append((t_main, n_r[0]))
+                spans.append((t_main, n_r[0]))
+        steps_i = max(len(recs) // n, 1)
+        phases["epoch_kernel"] = {
+            "span_ms_per_step": float(np.sum([t for t, _ in spans])) / steps_i,
+            "ratings_per_step": float(np.sum([r for _, r in spans])) / steps_i,
+            "launches": {k: {"per_step": len(v) / steps_i,
+                             "avg_us": float(np.mean([t for t, _ in v])) * 1e3,
+                             "ratings": float(np.mean([r for _, r in v]))}
+                         for k, v in per_launch.items()}}
         if multi:  # the exchange: one SUM all-reduce per chunk (ms per chunk and per step)
             ar = span("ar_begin", "ar_end")
             phases.update({"allreduce_ms_per_chunk": ar, "allreduce_ms": ar * n,
@@ -473,37 +486,154 @@ def cpu_baseline_svdpp(csr, n_items, K, n_train, target_s=8.0):
 
 
 # ---------------------------------------------------------------------------- main
-def roofline_of(algo, K, dtype, n_train, ms_step, shape, phases=None):
-    """The dominant kernel's roofline: SURVEY 8(d) algorithmic bytes per launch (the ratings the
-    epoch-kernel launch trains x B per update) / its average launch duration (HIP events on the
-    stream it runs on, the instrumented epochs after the timed region), against the HBM peak;
-    beside it the whole step's (algorithmic bytes of a step / the step time).  traffic = the
-    measured HBM-side bytes per launch of that kernel (PMC, profiles/traffic_*)."""
-    B = algorithmic_bytes_per_update(algo, K, ELEM_BYTES[dtype])
-    step_achieved = B * n_train / (ms_step * 1e-3) / 1e9
+def layout_of(eng):
+    """What the executed-byte model needs of an engine: element size, row strides, the log's
+    form, and per epoch-kernel launch the ratings and users it trains (chunk 0 = every chunk's
+    shape: chunks deal users round-robin)."""
+    s = eng.pu.element_size()
+    lay = {"s": s, "K": eng.K, "ldq": eng.ldq, "ld": eng.ld, "algo": eng.algo,
+           "ckpt": bool(eng.ckpt), "narrow": bool(getattr(eng, "narrow", False)),
+           "err_in_row": bool(eng.ckpt and eng.err_in_row),
+           "ldc": int(getattr(eng, "ldc", eng.ldq)), "hx": bool(getattr(eng, "hx", False)),
+           "n_items": eng.n_items, "n_chunks": eng.n_chunks, "launches": {}}
+    deg = np.diff(eng._row_ptr_h)
+    for c in range(eng.n_chunks):
+        lg = eng.logs[c] if eng.ckpt else None
+        groups = ([("heavy", lg["heavy"]), ("light", lg)] if lg is not None and lg["heavy"]
+                  else [("all", lg)])
+        for name, g in groups:
+            us = (g["sched"] if g is not None else eng.sched[c]).cpu().numpy()
+            us = us[us >= 0]
+            d = lay["launches"].setdefault(name, {"ratings": 0, "users": 0, "pieces": 0})
+            d["ratings"] += int(deg[us].sum())
+            d["users"] += len(us)
+            d["pieces"] += int(g["n_pieces"]) if g is not None else 0
+    return lay
+
+
+def executed_bytes(lay, ratings, users, pieces=0, whole_step=False):
+    """Bytes the launch (or, whole_step, the whole step's kernels) must move by the work it
+    executes -- every array it reads or writes once per use, caches ignored:
+      SVD checkpoint log, epoch kernel: per rating the CSR entry (4 + s), the item row gather
+        ((K + 2) s: factors, b_i, the constant column of the user bias; narrow rows: (K + 1) s)
+        and half a packed checkpoint row (ldc s / 2, + s of elog when the errors are not in the
+        rows); per user its row read and written once (2 (K + 1) s) + row_ptr / sched / user_sq;
+        whole step adds the replay (per rating its pair's row ldc s + perm / ck / rpos 12 B
+        (+ s elog); per piece the item row and the piece sums) and the fold (per piece the sums,
+        per item its row read + written).
+      SVD++ helper-wave launch: per rating the CSR entry, the q row read and its delta atomic
+        (2 (K + 1) s) and the y row of the user's start-of-user implicit sum (K s); per user its
+        row read + written and its y map (c_u) written; whole step adds the y fold (per rating
+        the user's c_u row, per item its y row read + written).
+    SURVEY 8(d)'s figure (12 + 4 s (K + 1) per update, + 2 s K for SVD++) also counts a p_u gather
+    and scatter per rating, which the register-resident user row never performs."""
+    s, K, ldq = lay["s"], lay["K"], lay["ldq"]
+    if lay["algo"] == "svd" and lay["ckpt"]:
+        q = (K + 1) * s if lay["narrow"] else (K + 2) * s
+        log = lay["ldc"] * s / 2 + (0 if lay["err_in_row"] else s)
+        b = ratings * (4 + s + q + log) + users * (2 * (K + 1) * s + 16 + 4 + 8)
+        if whole_step:
+            b += ratings * (lay["ldc"] * s + 12 + (0 if lay["err_in_row"] else s))
+            b += pieces * ((K + 1) * s + 2 * ldq * s + 8)
+            b += lay["n_chunks"] * lay["n_items"] * (2 * ldq * s + 8)
+        return b
+    if lay["algo"] == "svdpp":
+        b = ratings * (4 + s + 2 * (K + 1) * s + K * s) + users * (2 * (K + 1) * s + K * s + 20)
+        if whole_step:
+            b += ratings * (K * s + 4) + lay["n_chunks"] * lay["n_items"] * 2 * lay["ld"] * s
+        return b
+    return ratings * algorithmic_bytes_per_update(lay["algo"], K, s)
+
+
+def roofline_of(algo, K, dtype, n_train, ms_step, shape, phases=None, lay=None, chain=None):
+    """The dominant kernel's roofline.  The dominant kernel is the epoch kernel; one "launch" in
+    the contract's sense is its invocation over one step's ratings, whose launches of a split
+    chunk (the heavy users' on XCD 0, the others' on XCDs 1-7) run concurrently -- so its
+    duration is their wall span (HIP events on both streams, the instrumented epochs after the
+    timed region) and kernel time per step never exceeds the step.  achieved = the executed
+    bytes of that work (executed_bytes) / the span; each launch is also reported on its own
+    (heavy = the critical path), the whole step beside it, and SURVEY 8(d)'s byte figure as a
+    labelled rate (no frac: it counts traffic the kernel does not perform).  traffic = the
+    kernel's measured HBM bytes per step (2 x FETCH_SIZE + WRITE_SIZE, profiles/traffic_*).
+    chain: the heaviest user's chain timed alone -- the latency roof of the critical launch."""
+    s = ELEM_BYTES[dtype]
+    B8 = algorithmic_bytes_per_update(algo, K, s)
     traffic, tinfo = traffic_for(algo, K, shape, dtype)
-    el = (phases or {}).get("epoch_launches")
+    ek = (phases or {}).get("epoch_kernel")
     kname = "mf_svdpp_hx_kernel" if algo == "svdpp" else "mf_ckpt_epoch_kernel"
-    if el:
-        achieved = B * el["avg_ratings"] / (el["avg_us"] * 1e-6) / 1e9
-        per_launch = None
-        if tinfo and kname in (tinfo.get("per_kernel") or {}):
-            pk = tinfo["per_kernel"][kname]
-            per_launch = pk["bytes_per_step"] / max(pk["dispatches_per_step"], 1e-9)
-        dom = {"kernel": kname, "launches_per_step": el["per_step"],
-               "avg_launch_us": el["avg_us"], "algorithmic_bytes_per_launch": B * el["avg_ratings"],
-               "traffic_per_launch": per_launch}
-    else:
-        achieved, dom = step_achieved, None
-    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": (dom or {}).get("traffic_per_launch") if dom else traffic,
-            "dominant_kernel": dom, "step_achieved": step_achieved,
-            "step_frac": step_achieved / HBM_PEAK_GBS, "step_traffic": traffic,
-            "algorithmic_bytes_per_update": B, "updates_per_step": n_train,
-            "algorithmic_bytes_per_step": B * n_train,
-            "traffic_breakdown": tinfo.get("per_kernel") if tinfo else None,
-            "traffic_source": tinfo.get("source") if tinfo else None}
+    gbs = lambda b, ms: b / (ms * 1e-3) / 1e9
+    out = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    if not (ek and lay):
+        a = gbs(B8 * n_train, ms_step)
+        out.update(achieved=a, frac=a / HBM_PEAK_GBS, traffic=traffic)
+        return out
+    L = lay["launches"]
+    tot_r = sum(v["ratings"] for v in L.values())
+    tot_u = sum(v["users"] for v in L.values())
+    tot_p = sum(v["pieces"] for v in L.values())
+    ex = executed_bytes(lay, tot_r, tot_u)
+    span = ek["span_ms_per_step"]
+    k_traffic = None
+    if tinfo and kname in (tinfo.get("per_kernel") or {}):
+        k_traffic = tinfo["per_kernel"][kname]["bytes_per_step"]
+    a = gbs(ex, span)
+    out.update(achieved=a, frac=a / HBM_PEAK_GBS, traffic=k_traffic)
+    launches = {}
+    for name, v in ek["launches"].items():
+        lv = L.get(name, {"users": 0})
+        b = executed_bytes(lay, v["ratings"], lv["users"] / max(lay["n_chunks"], 1))
+        launches[name] = {"avg_us": v["avg_us"], "per_step": v["per_step"],
+                          "ratings": v["ratings"], "executed_bytes": b,
+                          "achieved": gbs(b, v["avg_us"] * 1e-3),
+                          "frac": gbs(b, v["avg_us"] * 1e-3) / HBM_PEAK_GBS}
+    step_b = executed_bytes(lay, tot_r, tot_u, tot_p, whole_step=True)
+    out["dominant_kernel"] = {
+        "kernel": kname, "unit": "its invocation over one step's %d ratings (%d launch(es), "
+                                 "concurrent when split)" % (tot_r, len(launches)),
+        "span_us_per_step": span * 1e3, "executed_bytes_per_step": ex,
+        "executed_bytes_per_update": ex / max(tot_r, 1), "traffic_per_step": k_traffic,
+        "launches": launches}
+    out["step"] = {"ms": ms_step, "executed_bytes": step_b, "achieved": gbs(step_b, ms_step),
+                   "frac": gbs(step_b, ms_step) / HBM_PEAK_GBS, "traffic": traffic,
+                   "traffic_frac": (gbs(traffic, ms_step) / HBM_PEAK_GBS) if traffic else None}
+    out["survey_8d"] = {"bytes_per_update": B8, "rate_over_span": gbs(B8 * tot_r, span),
+                        "rate_over_step": gbs(B8 * n_train, ms_step),
+                        "note": "SURVEY 8(d)'s algorithmic figure, a rate only (no frac): it "
+                                "counts a p_u gather + scatter per rating that the register-"
+                                "resident user row never performs"}
+    if chain:
+        crit = launches.get("heavy", launches.get("all"))
+        chain = dict(chain)
+        if crit:
+            chain["critical_launch_us"] = crit["avg_us"]
+            chain["frac"] = chain["alone_us"] / crit["avg_us"]
+        out["critical_path_bound"] = "chain latency: the heaviest user's ratings are sequential"
+        out["chain_latency"] = chain
+    out["traffic_breakdown"] = tinfo.get("per_kernel") if tinfo else None
+    out["traffic_source"] = tinfo.get("source") if tinfo else None
+    return out
+
+
+def time_top_chain(eng, torch, reps=3):
+    """The heaviest user's chain alone on the GPU (one wave, the product epoch kernel with its
+    checkpoint rows): the latency roof of a launch that trains that user.  Run after the
+    instrumented epochs (it moves that user's row and log rows; nothing reads them after)."""
+    if not (eng.algo == "svd" and eng.ckpt):
+        return None
+    deg = np.diff(eng._row_ptr_h)
+    top = int(np.argmax(deg))
+    sched = torch.tensor([top], dtype=torch.int32, device=eng.dev)
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(eng.stream)
+        eng._epoch_sq(sched, 1, 1, eng._st())
+        b.record(eng.stream)
+        eng.stream.synchronize()
+        ts.append(a.elapsed_time(b))
+    t = float(np.median(ts)) * 1e3
+    return {"top_user_ratings": int(deg[top]), "alone_us": t,
+            "ns_per_rating": t * 1e3 / max(int(deg[top]), 1), "reps": reps}
 
 
 def main():
@@ -591,22 +721,15 @@ def main():
         "per_gpu_value": value / world,
         "device_bytes_per_rank_max": dev_bytes,
     }
-    rl = roofline_of(algo, K, args.dtype, n_train, ms_step, args.shape, phases)
+    lay = layout_of(eng)
+    chain = time_top_chain(eng, torch) if args.shape == "ml-1m" else None
+    rl = roofline_of(algo, K, args.dtype, n_train, ms_step, args.shape, phases, lay, chain)
     rl.update({
-        "kernel": "dominant: the epoch kernel's launches (%s); step (%s): %s" % (
-            (rl["dominant_kernel"] or {}).get("kernel"), mode,
+        "kernel": "dominant: %s; step (%s): %s" % (
+            (rl.get("dominant_kernel") or {}).get("kernel"), mode,
             "mf_ckpt_epoch_kernel (heavy + light users) + log_replay_kernel (both groups) "
             "+ log_apply_kernel" if mode == "log" else "mf_svdpp_hx_kernel + y fold (+ merge)"),
-        "phases_gpu_ms": phases,
-        "note": "achieved = algorithmic bytes per launch of the dominant kernel (SURVEY 8(d): a "
-                "gather + scatter of the user and item rows per rating, s = %d bytes per "
-                "element, x the ratings the launch trains) / its average launch duration (HIP "
-                "events on its own stream); step_achieved = the same over the whole step. "
-                "traffic = that kernel's measured HBM-side bytes per launch (2 x FETCH_SIZE + "
-                "WRITE_SIZE, PMC), step_traffic = every kernel's per step. Where the tables are "
-                "L2/MALL-resident (ML-1M: 3 MB item table) the algorithmic bytes exceed what HBM "
-                "moves and frac can pass 1: the launch is bound by the heaviest user's "
-                "sequential chain (1805 ratings), not by HBM" % ELEM_BYTES[args.dtype]})
+        "phases_gpu_ms": phases, "note": ROOFLINE_NOTE})
     result["roofline"] = rl
 
     oracle_cache = {}
@@ -631,10 +754,12 @@ def main():
         eng = None
         e32 = make_engine(dt=other)
         el2, ph = run_steps(e32, None, args.steps, args.warmup, torch)
+        lay2, chain2 = layout_of(e32), time_top_chain(e32, torch)
         del e32
         ms2 = el2 / args.steps * 1e3
         leg = {"dtype": other, "value": n_train * args.steps / el2, "ms_per_step": ms2,
-               "roofline": roofline_of(algo, K, other, n_train, ms2, args.shape, ph)}
+               "roofline": roofline_of(algo, K, other, n_train, ms2, args.shape, ph, lay2,
+                                       chain2)}
         leg["roofline"]["phases_gpu_ms"] = ph
         if not args.no_rmse:
             leg["rmse"] = rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world,
@@ -649,8 +774,9 @@ def main():
             pp = make_engine("svdpp", 100, "atomic", dt)
             n2 = max(10, args.steps // 2)
             e2, ph2 = run_steps(pp, None, n2, 2, torch)
+            lay_pp = layout_of(pp)
             del pp
-            rl2 = roofline_of("svdpp", 100, dt, n_train, e2 / n2 * 1e3, args.shape, ph2)
+            rl2 = roofline_of("svdpp", 100, dt, n_train, e2 / n2 * 1e3, args.shape, ph2, lay_pp)
             rl2["phases_gpu_ms"] = ph2
             pp_legs[dt] = {"value": n_train * n2 / e2, "unit": "rating-updates/s", "steps": n2,
                            "ms_per_step": e2 / n2 * 1e3, "roofline": rl2}
@@ -669,11 +795,63 @@ def main():
     if small and headline and args.legs and not args.no_predict:
         result["predict"] = predict_leg(csr, test, n_items, gm, torch)
 
+    if small and headline and args.legs and not args.no_c4:
+        eng = None
+        result["c4"] = c4_leg(torch)
+        note("c4 leg done")
+
     if rank == 0:
         print(json.dumps(result), flush=True)
     if ctx is not None:
         ctx.barrier()
         ctx.dist.destroy_process_group()
+
+
+ROOFLINE_NOTE = (
+    "dominant kernel = the epoch kernel, one launch = its invocation over a step's ratings (a "
+    "split chunk's heavy and light launches run concurrently on two streams: duration = their "
+    "wall span). achieved = the bytes the executed work moves (executed_bytes(): per rating the "
+    "CSR entry, the item row gather and half a packed checkpoint row; per user its row once) / "
+    "that span; traffic = its measured HBM bytes per step (2 x FETCH_SIZE + WRITE_SIZE, "
+    "separate --pmc passes); launches = each launch on its own (heavy = the critical path); "
+    "step = every kernel of the step over ms_per_step; survey_8d = SURVEY 8(d)'s figure as a "
+    "rate only. ML-1M's critical launch is bound by the heaviest user's sequential chain "
+    "(chain_latency: that chain timed alone on the GPU), not by HBM: its item table is "
+    "L2-resident; the HBM-bound configuration is the c4 leg")
+
+
+def c4_leg(torch, steps=5, warmup=2):
+    """BASELINE configs[3]'s shape on this one GPU (2M users x 200k items, 99M training ratings,
+    SVD K=128 fp32, the checkpoint log, one epoch per step): the HBM-bound configuration
+    (its tables exceed the caches), with its own roofline and traffic (profiles/
+    traffic_svd_k128_c4.json).  Held-out RMSE at E=20: tests/test_gpu_scale.py."""
+    from types import SimpleNamespace
+    from surprise_amd.engine import MFEngine
+    a = SimpleNamespace(shape="c4", users=0)
+    t0 = time.perf_counter()
+    csr, _, n_items, _, desc = workload(a, 0, 1)
+    n_train = len(csr[1])
+    gm = float(csr[2].sum()) / n_train
+    K = 128
+    pu, qi, _ = init_tables("c4", 0, len(csr[0]) - 1, n_items, K, False, 0)
+    eng = MFEngine(csr, n_items, K, algo="svd", hyper=hyper_for("svd", gm), mode="log",
+                   dtype="float32")
+    eng.set_factors(pu, qi)
+    eng._prepare(None)
+    prep = time.perf_counter() - t0
+    el, ph = run_steps(eng, None, steps, warmup, torch)
+    lay = layout_of(eng)
+    ms = el / steps * 1e3
+    del eng
+    torch.cuda.empty_cache()
+    rl = roofline_of("svd", K, "f32", n_train, ms, "c4", ph, lay)
+    rl["phases_gpu_ms"] = ph
+    rl["note"] = ROOFLINE_NOTE
+    return {"config": "BASELINE configs[3]'s shape on one GPU: " + desc + "; SVD K=128 f32, "
+                      "checkpoint log, one epoch per step",
+            "value": n_train * steps / el, "unit": "rating-updates/s", "steps": steps,
+            "warmup": warmup, "ms_per_step": ms, "dtype": "f32", "host_prep_s": prep,
+            "roofline": rl}
 
 
 def oracle_rmse(args, csr, test, n_items, K, gm, cache):

@@ -162,10 +162,12 @@ def svd_sgd_groups(row_ptr, items, ratings, n_items, K, n_epochs, biased, global
 
 def svdpp_sgd_groups_merge(row_ptr, items, ratings, n_items, K, n_epochs, global_mean, hp,
                            pu, qi, yj, group_of_user, n_groups, chunk_of_user=None, n_chunks=1,
-                           merge=2, merge_y=4, bu=None, bi=None):
+                           merge=2, merge_y=4, bu=None, bi=None, bias_fold=False):
     """SVD++ G-group schedule (multi-rank semantics): q/b merged by `merge` (0 SUM, 1 MEAN,
-    2 count-aware), y by `merge_y` (4: the GPU's affine composition in group order, users
-    reading the chunk-start y).  Returns (pu, qi, yj, bu, bi)."""
+    2 count-aware, 3 rank-order composition), y by `merge_y` (4: the GPU's affine composition in
+    group order, users reading the chunk-start y); bias_fold: item biases read at the chunk start
+    and their steps folded per item with recency weights after the chunk.
+    Returns (pu, qi, yj, bu, bi)."""
     row_ptr, items, ratings = _csr_args(row_ptr, items, ratings)
     n_users = len(row_ptr) - 1
     pu = np.ascontiguousarray(pu, dtype=np.float64)
@@ -176,11 +178,12 @@ def svdpp_sgd_groups_merge(row_ptr, items, ratings, n_items, K, n_epochs, global
     g = np.ascontiguousarray(group_of_user, dtype=np.int32)
     c = (np.zeros(n_users, np.int32) if chunk_of_user is None
          else np.ascontiguousarray(chunk_of_user, dtype=np.int32))
-    lib().oracle_svdpp_sgd_groups_merge(
+    lib().oracle_svdpp_sgd_groups_merge_b(
         ctypes.c_int64(n_users), ctypes.c_int64(n_items), _p(row_ptr), _p(items), _p(ratings),
         ctypes.c_int32(K), ctypes.c_int32(n_epochs), ctypes.c_double(global_mean),
         ctypes.byref(hp), _p(g), ctypes.c_int32(n_groups), _p(c), ctypes.c_int32(n_chunks),
-        ctypes.c_int32(merge), ctypes.c_int32(merge_y), _p(pu), _p(qi), _p(yj), _p(bu), _p(bi))
+        ctypes.c_int32(merge), ctypes.c_int32(merge_y), ctypes.c_int32(int(bias_fold)), _p(pu),
+        _p(qi), _p(yj), _p(bu), _p(bi))
     return pu, qi, yj, bu, bi
 
 

@@ -6,12 +6,13 @@ on the GPU box).
             SVD K=128, the reference loop restated (oracle_svd_sgd <- mf.pyx:241-262)
   c5shard   the first 1.25M users of configs[4]'s shape (every item: 1M; one of 8 ranks' share),
             SVD++ K=128 in the exact per-user form (oracle_svdpp_sgd_affine <- mf.pyx:463-498)
-  c5at8_cN  the same 1.25M users in C5@8's multi-rank schedule: split 8 ways by
+  c5at8_cN_mM  the same 1.25M users in C5@8's multi-rank schedule: split 8 ways by
             dist.shard_users (bench.py --gpus 8), each rank's users dealt into N epoch-chunks by
-            dist.chunk_users, the ranks' q / b deltas merged by the count-aware rule and their y
-            maps composed in rank order (oracle_svdpp_sgd_groups_merge(merge=2, merge_y=4) -- the
-            GPU's multi-rank SVD++ rule, surprise_amd/dist.py).  N = 2 puts 625k users (78k per
-            rank) in a chunk: C5@8's chunk at 16 chunks per epoch over 10M users
+            dist.chunk_users, the ranks' q / b deltas merged by rule M (3: carried through the
+            later ranks' steps -- the GPU's MF_MERGE_RECENCY; 2: round 3's count-aware rule) and
+            their y maps composed in rank order (oracle_svdpp_sgd_groups_merge(merge=M,
+            merge_y=4)).  N = 2 puts 625k users (78k per rank) in a chunk: C5@8's chunk at 16
+            chunks per epoch over 10M users
 
 Same CSR, held-out triples, initial factors (init_tables), global mean and hyper-parameters as
 `bench.py --shape c4` / `--shape c5 --users 1250000` (imported from bench.py, not re-stated).
@@ -42,8 +43,9 @@ OUT = os.path.join(HERE, "scale_golden.json")
 CASES = {"c4": dict(shape="c4", users=0, algo="svd", K=128),
          "c5shard": dict(shape="c5", users=1_250_000, algo="svdpp", K=128)}
 for _n in (2, 4, 8):
-    CASES["c5at8_c%d" % _n] = dict(shape="c5", users=1_250_000, algo="svdpp", K=128, groups=8,
-                                   chunks=_n)
+    for _m in (2, 3):  # the q / b merge: 2 count-aware (round 3), 3 rank-order composition
+        CASES["c5at8_c%d_m%d" % (_n, _m)] = dict(shape="c5", users=1_250_000, algo="svdpp",
+                                                 K=128, groups=8, chunks=_n, merge=_m)
 
 
 def group_schedule(row_ptr, groups, chunks):
@@ -92,7 +94,7 @@ def main():
         if groups:
             pu, qi, yj, bu, bi = orc.svdpp_sgd_groups_merge(
                 row_ptr, items, ratings, n_items, K, 1, gm, hp, pu, qi, yj, g_of, groups, c_of,
-                c["chunks"], merge=2, merge_y=4, bu=bu, bi=bi)
+                c["chunks"], merge=c["merge"], merge_y=4, bu=bu, bi=bi)
             est = orc.svdpp_predict(tu, ti, row_ptr, items, K, gm, pu, qi, yj, bu, bi)
             imp = np.zeros(len(tu), bool)
         elif svdpp:
@@ -114,8 +116,9 @@ def main():
         "data_fingerprint": bench.data_fingerprint(csr, (tu, ti, tr)),
         "rmse_by_epoch": curve,
         "global_mean_rmse": orc.rmse(tr, np.full(len(tr), gm)),
-        "oracle": (("oracle_svdpp_sgd_groups_merge(merge=2, merge_y=4): %d ranks x %d epoch-"
-                    "chunks, per-user affine form inside a rank" % (groups, c["chunks"]))
+        "oracle": (("oracle_svdpp_sgd_groups_merge(merge=%d, merge_y=4): %d ranks x %d epoch-"
+                    "chunks, per-user affine form inside a rank" % (c.get("merge"), groups,
+                                                                   c["chunks"]))
                    if groups else "oracle_svdpp_sgd_affine (mf.pyx:463-498)" if svdpp
                    else "oracle_svd_sgd (mf.pyx:241-262)") + ", fp64, one host thread",
         "oracle_seconds_per_epoch": float(np.mean(secs)),

@@ -156,8 +156,13 @@ def test_bench_two_ranks_spawned(torch):
     assert len(lines) == 1, p.stdout[-2000:]
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["scaling"] == "weak"
-    assert r["value"] > 0 and r["roofline"]["frac"] > 0
-    assert r["roofline"]["dominant_kernel"]["kernel"] == "mf_ckpt_epoch_kernel"
+    rl = r["roofline"]
+    assert r["value"] > 0 and 0 < rl["frac"] <= 1.0
+    assert rl["dominant_kernel"]["kernel"] == "mf_ckpt_epoch_kernel"
+    # the kernel's time per step never exceeds the step; no launch passes the peak
+    assert rl["dominant_kernel"]["span_us_per_step"] <= r["ms_per_step"] * 1e3
+    assert all(0 < x["frac"] <= 1.0 for x in rl["dominant_kernel"]["launches"].values())
+    assert rl["step"]["frac"] <= 1.0
     assert r["roofline"]["phases_gpu_ms"]["allreduce_ms_per_chunk"] > 0
     assert r["rmse"]["gpu"] < r["rmse"]["global_mean_baseline"]
 

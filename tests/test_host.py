@@ -473,3 +473,29 @@ def test_print_summary_table(capsys):
     assert out[5].split() == ["Fit", "time", "1.00", "3.00", "2.00", "1.00"]
     assert out[6].split() == ["Test", "time", "0.25", "0.75", "0.50", "0.25"]
     assert out[3].index("1.0000") == 18  # '{:<18}' label column, '{:<8}' per value
+
+
+def test_roofline_executed_bytes_and_span_bounds():
+    """bench.roofline_of on a made-up split step: the dominant kernel's rate uses the concurrent
+    launches' wall span, every launch and the step report frac <= 1 for plausible timings, and
+    SURVEY 8(d)'s figure rides as a rate without a frac."""
+    import bench
+    lay = {"s": 8, "K": 100, "ldq": 104, "ld": 104, "algo": "svd", "ckpt": True, "narrow": False,
+           "err_in_row": True, "ldc": 104, "hx": False, "n_items": 3706, "n_chunks": 1,
+           "launches": {"heavy": {"ratings": 121840, "users": 128, "pieces": 3000},
+                        "light": {"ratings": 678327, "users": 5912, "pieces": 14000}}}
+    per_r = 4 + 8 + 102 * 8 + 104 * 8 / 2
+    assert bench.executed_bytes(lay, 1, 0) == per_r
+    ph = {"epoch_kernel": {"span_ms_per_step": 0.246, "ratings_per_step": 800167,
+                           "launches": {"heavy": {"per_step": 1, "avg_us": 246.0,
+                                                  "ratings": 121840},
+                                        "light": {"per_step": 1, "avg_us": 131.0,
+                                                  "ratings": 678327}}}}
+    rl = bench.roofline_of("svd", 100, "f64", 800167, 0.294, "ml-1m", ph, lay,
+                           {"top_user_ratings": 1805, "alone_us": 199.0})
+    dk = rl["dominant_kernel"]
+    assert abs(rl["achieved"] - dk["executed_bytes_per_step"] / 0.246e-3 / 1e9) < 1e-6
+    assert 0 < rl["frac"] <= 1 and rl["step"]["frac"] <= 1
+    assert all(0 < v["frac"] <= 1 for v in dk["launches"].values())
+    assert "frac" not in rl["survey_8d"]
+    assert abs(rl["chain_latency"]["frac"] - 199 / 246) < 1e-12
