@@ -84,6 +84,12 @@ def parse():
     p.add_argument("--heavy", type=float, default=-1,
                    help="SVD checkpoint log: users in the heavy launch (MFEngine heavy; -1: the "
                         "engine's policy)")
+    p.add_argument("--gram", type=int, default=-1,
+                   help="SVD checkpoint log: the heavy users by the blocked solve (1) or the "
+                        "lookahead chain (0); -1: the engine's policy")
+    p.add_argument("--xcd-split", type=int, default=-1,
+                   help="SVD checkpoint log: heavy launch on XCD 0, the rest on XCDs 1-7 (1 / 0; "
+                        "-1: the engine's policy)")
     p.add_argument("--hx-helpers", type=int, default=0,
                    help="SVD++ helper-wave launch: helper waves per chain, 3 or 1 (0: the "
                         "engine default)")
@@ -104,6 +110,9 @@ def parse():
     p.add_argument("--no-rmse", action="store_true")
     p.add_argument("--no-svdpp", action="store_true", help="skip the SVD++ C3 leg")
     p.add_argument("--no-predict", action="store_true", help="skip the batched test() leg")
+    p.add_argument("--no-chain-probe", action="store_true",
+                   help="skip timing the heaviest user's chain alone (profiling runs: its extra "
+                        "epoch-kernel launches would mix into the kernel's statistics)")
     p.add_argument("--no-c4", action="store_true",
                    help="skip the C4 leg (BASELINE configs[3]'s shape on this GPU)")
     p.add_argument("--users", type=int, default=0,
@@ -627,13 +636,15 @@ def time_top_chain(eng, torch, reps=3):
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(eng.stream)
-        eng._epoch_sq(sched, 1, 1, eng._st())
+        eng._heavy_epoch(sched, 1, eng._st())  # (the kernel the heavy launch uses)
         b.record(eng.stream)
         eng.stream.synchronize()
         ts.append(a.elapsed_time(b))
     t = float(np.median(ts)) * 1e3
     return {"top_user_ratings": int(deg[top]), "alone_us": t,
-            "ns_per_rating": t * 1e3 / max(int(deg[top]), 1), "reps": reps}
+            "ns_per_rating": t * 1e3 / max(int(deg[top]), 1), "reps": reps,
+            "kernel": "mf_svd_gram_kernel (blocked solve)" if eng.gram else
+                      "mf_ckpt_epoch_kernel (lookahead chain)"}
 
 
 def main():
@@ -677,7 +688,9 @@ def main():
                        **({"helpers": args.hx_helpers} if args.hx_helpers else {}),
                        **({"heavy": args.heavy} if args.heavy >= 0 else {}),
                        **({"hot_rows": args.hot_rows} if args.hot_rows >= 0 else {}),
-                       **({"replay_rows": args.replay_rows} if args.replay_rows else {}))
+                       **({"replay_rows": args.replay_rows} if args.replay_rows else {}),
+                       **({"gram": bool(args.gram)} if args.gram >= 0 else {}),
+                       **({"xcd_split": bool(args.xcd_split)} if args.xcd_split >= 0 else {}))
         eng.set_factors(pu, qi, yj=yj)
         eng._prepare(ctx)  # global per-item counts (all ranks)
         return eng
@@ -722,7 +735,8 @@ def main():
         "device_bytes_per_rank_max": dev_bytes,
     }
     lay = layout_of(eng)
-    chain = time_top_chain(eng, torch) if args.shape == "ml-1m" else None
+    chain = time_top_chain(eng, torch) if args.shape == "ml-1m" and not args.no_chain_probe \
+        else None
     rl = roofline_of(algo, K, args.dtype, n_train, ms_step, args.shape, phases, lay, chain)
     rl.update({
         "kernel": "dominant: %s; step (%s): %s" % (
@@ -742,9 +756,18 @@ def main():
         result["cpu_baseline"] = cpu_baseline_svdpp(csr, n_items, K, n_train)
         result["cpu_baseline"]["gpu_over_cpu"] = value / result["cpu_baseline"]["value"]
 
+    def reseed(e, a=algo, k=K):
+        """The timed engine again from the initial factors (the rmse leg reuses its device
+        layout instead of building another one: C5 / C4 host preparation takes minutes)."""
+        pu, qi, yj = init_tables(args.shape, rank, n_users, n_items, k, a == "svdpp",
+                                 getattr(workload, "user_lo", 0))
+        e.set_factors(pu, qi, yj=yj)
+        e._prepare(ctx)
+        return e
+
     if not args.no_rmse:
         result["rmse"] = rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch,
-                                  make_engine, oracle_cache)
+                                  lambda: reseed(eng), oracle_cache)
         note("rmse leg done")
 
     small = world == 1 and args.shape == "ml-1m" and K == 100
@@ -754,8 +777,8 @@ def main():
         eng = None
         e32 = make_engine(dt=other)
         el2, ph = run_steps(e32, None, args.steps, args.warmup, torch)
-        lay2, chain2 = layout_of(e32), time_top_chain(e32, torch)
-        del e32
+        lay2 = layout_of(e32)
+        chain2 = None if args.no_chain_probe else time_top_chain(e32, torch)
         ms2 = el2 / args.steps * 1e3
         leg = {"dtype": other, "value": n_train * args.steps / el2, "ms_per_step": ms2,
                "roofline": roofline_of(algo, K, other, n_train, ms2, args.shape, ph, lay2,
@@ -763,7 +786,8 @@ def main():
         leg["roofline"]["phases_gpu_ms"] = ph
         if not args.no_rmse:
             leg["rmse"] = rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world,
-                                   torch, lambda: make_engine(dt=other), oracle_cache)
+                                   torch, lambda: reseed(e32), oracle_cache)
+        del e32
         result["%s_leg" % other] = leg
 
     if small and algo == "svd" and not args.no_svdpp:

@@ -238,6 +238,24 @@ int mf_svd_epoch_sq(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                     const mf_hyper_t *hp, void *qlog, void *elog, double *user_sq,
                     int32_t n_waves, int32_t flags, int32_t dtype, void *stream);
 
+/*
+ * mf_svd_epoch_sq for the heaviest users by a blocked solve (replaces the same loop,
+ * matrix_factorization.pyx:241-262, for the users it is given): one workgroup per user; over
+ * every block of 16 ratings the errors are the solution of a unit lower-triangular system built
+ * from the block's item-row Gram matrix (MFMA) and the row at the block's start, so the
+ * sequential chain per rating is one readlane + FMA instead of two 64-lane reductions.  Writes
+ * exactly what mf_svd_epoch_sq with MF_EPOCH_ERR_IN_ROW writes for those users (the user's row
+ * and bias, its packed checkpoint rows with their errors, user_sq[u]) -- equal up to rounding.
+ * Needs the MF_MODE_LOG item layout (column n_factors + 1 of qb = 1), ldq >= n_factors + 4
+ * (fp32: the error columns, as MF_EPOCH_ERR_IN_ROW), ldq * size <= 1 KiB, no user listing an
+ * item twice.  n_blocks: workgroups of the launch (0: one per scheduled user; users are taken
+ * strided); flags: MF_EPOCH_XCD_SHIFT's mask only.
+ */
+int mf_svd_epoch_gram(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
+                      void *bu, int32_t ldu, const void *qb, int32_t ldq, int32_t n_factors,
+                      int32_t biased, const mf_hyper_t *hp, void *qlog, double *user_sq,
+                      int32_t n_blocks, int32_t flags, int32_t dtype, void *stream);
+
 /* user_sq[r] = sum_{c < n_cols} x[r * ld + c]^2 (fp64) for r < n_rows: initial user_sq. */
 int mf_user_sq(const void *pu, int64_t n_rows, int32_t n_cols, int32_t ld, double *user_sq,
                int32_t dtype, void *stream);

@@ -68,6 +68,8 @@ SIGNATURES = {
                         _vp],
     "mf_svd_epoch_sq": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32,
                         _i32, ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i32, _i32, _i32, _vp],
+    "mf_svd_epoch_gram": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32,
+                          _i32, ctypes.POINTER(MfHyper), _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_sumsq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
     "mf_user_sq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
     "mf_user_sq_reduce": [_vp, _i64, _i32, _vp, _vp],

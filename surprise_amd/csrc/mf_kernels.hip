@@ -2545,6 +2545,288 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     }
 }
 
+// ---------------------------------------------------------------- blocked solve (heaviest users)
+//
+// SVD checkpoint log with the errors in the rows, one WORKGROUP per user.  The lookahead body
+// pays ~48 instructions per rating on one wave (two 64-lane reductions): the heaviest user's
+// chain of 1805 ratings is the ML-1M step's critical path.  Unrolled over a block of kGB = 16
+// ratings that starts at the user row P (column K: the constant 1 of the item bias, K+1:
+// c = mu + bu), the reference recursion (mf.pyx:247-262) makes every error a linear function of
+// the block's earlier errors:
+//   err_m = rhs_m - sum_{t<m} L_mt err_t
+//   rhs_m = r_m - a^m <q_m, P>_fac - q_m[K] P[K] - abu^m c - kb (1 + abu + ... + abu^(m-1))
+//   L_mt  = a^(m-1-t) lr_pu <q_m, q_t>_fac + abu^(m-1-t) lr_bu
+// (a = 1 - lr_pu reg_pu, abu = 1 - lr_bu reg_bu, kb = mu (1 - abu); column K+1 of every item row
+// is 1).  Per block: wave 0 solves the 16 errors (16 x readlane + FMA -- no reduction on the
+// chain) while waves 1-3 build the NEXT block's Gram matrix <q_m, q_t> with MFMA (16x16x4) and
+// gather the block after it into LDS; then every wave runs the row recursion with lane = column
+// (the checkpoint rows of the block's pairs, its end row) and the next block's <q_m, P>.  Same
+// arithmetic as the lookahead body up to rounding: fp64 equals oracle_svd_sgd_deltalog to 1e-9.
+constexpr int kGB = 16;  // ratings per block (one 16x16 MFMA tile)
+template <typename T>
+struct GramCols { static constexpr int n = 1024 / (int)sizeof(T); };  // rows of <= 1 KiB
+
+template <typename T>
+struct GramMfma;
+template <>
+struct GramMfma<double> {
+    typedef double acc __attribute__((ext_vector_type(4)));
+    __device__ static __forceinline__ acc step(double a, double b, acc c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    // C/D of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 r
+    __device__ static __forceinline__ int row(int lane, int r) { return (lane >> 4) + 4 * r; }
+};
+template <>
+struct GramMfma<float> {
+    typedef float acc __attribute__((ext_vector_type(4)));
+    __device__ static __forceinline__ acc step(float a, float b, acc c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    // the standard 16x16 C/D map: col = lane & 15, row = 4 (lane >> 4) + r
+    __device__ static __forceinline__ int row(int lane, int r) { return 4 * (lane >> 4) + r; }
+};
+
+// a workgroup barrier that orders LDS only: __syncthreads() also waits for every outstanding
+// global load and store (vmcnt(0)), which would drain the row prefetches and the checkpoint-row
+// stores at every one of the block's three barriers
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+constexpr int kGWin = 1024;  // item ids / ratings of a user staged in LDS at a time
+constexpr int kGSlots = 4;   // item-row blocks in the LDS ring: b, b+1, b+2, and b+3 in flight
+
+// LDS bytes of the dynamic ring of mf_svd_gram_kernel (kGSlots blocks of kGB rows)
+int gram_ring_bytes(int ldq, int esz) { return kGSlots * kGB * ldq * esz; }
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void mf_svd_gram_kernel(
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
+    const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
+    T *__restrict__ pu, T *__restrict__ bu, int ldu, const T *__restrict__ qb, int ldq, int K,
+    int biased, Hyper<T> hp, T *__restrict__ qlog, double *__restrict__ psq, int err_col,
+    int xmask)
+{
+    // the block ring: kGSlots x kGB item rows packed at stride ldq (LDS-DMA writes 1-KiB pieces
+    // lane-linearly, and a block of 16 rows of a 64-byte multiple is whole pieces)
+    extern __shared__ __attribute__((aligned(16))) char gram_ring[];
+    __shared__ T gp[3][kGB][kGB];     // the helpers' partial Gram matrices
+    __shared__ T lm[2][kGB][kGB];     // L of the current / next block
+    __shared__ T pw[3][kGB + 1];      // a^k, abu^k, kb (1 + .. + abu^(k-1))
+    __shared__ T E[kGB], X0[kGB], P[GramCols<T>::n];
+    __shared__ int32_t ids[kGWin];    // item ids / ratings [win0, win0 + kGWin) of the user
+    __shared__ T rtw[kGWin];
+    __shared__ double sqw[kBlock / kWave];
+    using MF = GramMfma<T>;
+    const int tid = threadIdx.x, w = tid / kWave, lane = tid & (kWave - 1);
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    int64_t slot = blockIdx.x, n_slots = gridDim.x;
+    if (xmask) {  // this block's slot among the launch's blocks on the XCDs of xmask
+        const int x = __builtin_amdgcn_readfirstlane(xcc_id());
+        if (!((xmask >> x) & 1)) return;
+        const int c = __builtin_popcount(xmask), rank = __builtin_popcount(xmask & ((1 << x) - 1));
+        slot = (int64_t)(blockIdx.x >> 3) * c + rank;
+        n_slots = (int64_t)(gridDim.x >> 3) * c;
+    }
+    const T lr_bu = biased ? hp.lr_bu : T(0);
+    const T a = T(1) - hp.lr_pu * hp.reg_pu, abu = T(1) - lr_bu * hp.reg_bu;
+    const T kb = hp.gm * (T(1) - abu);
+    if (tid <= kGB) {
+        T x = T(1), y = T(1), g = T(0);
+        for (int t = 0; t < tid; ++t) {
+            g += kb * y;
+            x *= a;
+            y *= abu;
+        }
+        pw[0][tid] = x;
+        pw[1][tid] = y;
+        pw[2][tid] = g;
+    }
+    // the row recursion's column (waves 0, 2, 3: wave 1 issues the LDS-DMA and keeps its memory
+    // counter to those loads) and its constants (ap, lrp, kvec of epoch_body_la)
+    const int c = w == 0 ? lane : (w >= 2 ? (w - 1) * kWave + lane : -1);
+    const bool col = c >= 0 && c < ldq;
+    const bool fac = c >= 0 && c < K, ub = c == K + 1;
+    const T apc = fac ? a : (ub ? abu : T(1));
+    const T lrpc = fac ? hp.lr_pu : (ub ? lr_bu : T(0));
+    const T kvc = ub ? kb : T(0);
+    const int nk = (K + 3) / 4;  // MFMA k-steps over the factor columns
+    const uint32_t rowb = (uint32_t)ldq * sizeof(T);
+    const int pieces = (int)(kGB * rowb / 1024);  // LDS-DMA instructions per block
+    auto ring = [&](int b) -> T * { return (T *)(gram_ring + (size_t)(b % kGSlots) * kGB * rowb); };
+
+    for (int64_t sidx = slot; sidx < n_sched; sidx += n_slots) {
+        const int u = sched[sidx];
+        if (u < 0) continue;
+        const int64_t s = row_ptr[u];
+        const int n = (int)(row_ptr[u + 1] - s);
+        if (n <= 0) continue;
+        const int nb = (n + kGB - 1) / kGB;
+        const int32_t *__restrict__ it = items + s;
+        const T *__restrict__ rr = ratings + s;
+        T *__restrict__ lrows = qlog + ck_row0(s, u) * ldq;
+        int win0 = 0;
+        auto load_win = [&](int j0) {  // every thread: the id / rating window from rating j0
+            win0 = j0;
+            for (int x = tid; x < kGWin && j0 + x < n; x += kBlock) {
+                ids[x] = it[j0 + x];
+                rtw[x] = rr[j0 + x];
+            }
+        };
+        // wave 1: block b's rows gathered by index into its ring slot (global_load_lds, 16 B
+        // per lane: piece i of the block is bytes [1024 i, 1024 (i + 1)) of its packed rows)
+        auto dma = [&](int b) {
+            const char *q8 = (const char *)qb;
+            char *dst = (char *)ring(b);
+            for (int i = 0; i < pieces; ++i) {
+                const uint32_t x = (uint32_t)i * 1024u + (uint32_t)lane * 16u;
+                const int r = (int)(x / rowb);
+                const uint32_t cb = x - (uint32_t)r * rowb;
+                const int j = b * kGB + r;
+                const int64_t id = ids[(j < n ? j : n - 1) - win0];
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(q8 + id * rowb + cb),
+                    (__attribute__((address_space(3))) void *)(dst + i * 1024), 16, 0, 0);
+            }
+        };
+        // helper h of 3: its k-steps of the Gram matrix of block b, into gp[h]
+        auto gram = [&](int b, int h) {
+            const T *R = ring(b);
+            typename MF::acc acc = {T(0), T(0), T(0), T(0)};
+            const int r = lane & 15, kq = lane >> 4;
+            for (int ks = h * nk / 3; ks < (h + 1) * nk / 3; ++ks) {
+                const int cc = 4 * ks + kq;
+                const T v = cc < K ? R[r * ldq + cc] : T(0);
+                acc = MF::step(v, v, acc);  // A[r][k] = B[k][r] = q_r[cc]
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) gp[h][MF::row(lane, i)][lane & 15] = acc[i];
+        };
+        // L of block b from the helpers' partials (thread = entry (m, t))
+        auto combine = [&](int b) {
+            const int m = tid >> 4, t = tid & 15;
+            T v = T(0);
+            if (t < m) {
+                const T g = gp[0][m][t] + gp[1][m][t] + gp[2][m][t];
+                v = pw[0][m - 1 - t] * hp.lr_pu * g + pw[1][m - 1 - t] * lr_bu;
+            }
+            lm[b & 1][m][t] = v;
+        };
+        // <q_m, P>_fac of block b (thread = (m, 16-lane part); DPP sums inside each row of 16)
+        auto x0 = [&](int b) {
+            const T *R = ring(b);
+            const int m = tid >> 4, part = tid & 15;
+            T acc = T(0);
+            for (int cc = part; cc < K; cc += 16) acc += R[m * ldq + cc] * P[cc];
+            acc += dpp<0xB1>(acc);
+            acc += dpp<0x4E>(acc);
+            acc += dpp<0x141>(acc);
+            acc += dpp<0x140>(acc);
+            if (part == 0) X0[m] = acc;
+        };
+
+        load_win(0);
+        if (col) {  // P = [p_u | 1 | mu + bu | 0..]
+            const T bu0 = bu[u];
+            P[c] = fac ? pu[(int64_t)u * ldu + c]
+                       : (c == K ? (biased ? T(1) : T(0)) : (ub ? hp.gm + bu0 : T(0)));
+        }
+        lds_barrier();
+        if (wu == 1) {
+            for (int b = 0; b < 3 && b < nb; ++b) dma(b);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        lds_barrier();
+        if (w > 0) gram(0, w - 1);
+        lds_barrier();
+        combine(0);
+        x0(0);
+        lds_barrier();
+        for (int b = 0; b < nb; ++b) {
+            const T *R = ring(b);
+            const int len = n - b * kGB < kGB ? n - b * kGB : kGB;
+            // ---- A: wave 0 solves block b; wave 1 starts block b+3's gather; waves 1-3 build
+            // block b+1's Gram matrix
+            if (wu == 0) {
+                const int m = lane & 15;
+                const int j = b * kGB + m;
+                T rhs = (j < n ? rtw[j - win0] : T(0)) - pw[0][m] * X0[m] - R[m * ldq + K] * P[K] -
+                        pw[1][m] * P[K + 1] - pw[2][m];
+                T Lr[kGB];
+#pragma unroll
+                for (int t = 0; t < kGB; ++t) Lr[t] = lm[b & 1][m][t];
+#pragma unroll
+                for (int t = 0; t < kGB; ++t) {
+                    if (t < len) {  // (L[m][t] = 0 for t >= m: lane t keeps err_t)
+                        const T e = readlane(rhs, t);
+                        rhs -= Lr[t] * e;
+                    }
+                }
+                if (lane < len) E[lane] = rhs;
+            } else {
+                if (wu == 1 && b + 3 < nb) dma(b + 3);
+                if (b + 1 < nb) gram(b + 1, w - 1);
+            }
+            lds_barrier();
+            // ---- B: L of block b+1; the row recursion over block b (lane = column): the
+            // checkpoint row p_{c+1} of every pair (c, c+1) with its two errors, the end row
+            if (b + 1 < nb) combine(b + 1);
+            if (col) {
+                T p = P[c];
+                for (int t = 0; t < len; ++t) {
+                    const T e = E[t];
+                    p = (apc * p + kvc) + e * (lrpc * R[t * ldq + c]);
+                    if (!(t & 1)) {
+                        const int64_t pair = (b * kGB + t) >> 1;
+                        if (c < err_col) lrows[pair * ldq + c] = p;
+                        else if (c == err_col) lrows[pair * ldq + c] = e;
+                        else if (c == err_col + 1) lrows[pair * ldq + c] = t + 1 < len ? E[t + 1] : T(0);
+                    }
+                }
+                P[c] = p;
+            }
+            lds_barrier();
+            // ---- C: <q_m, P> of block b+1; wave 1 retires block b+2's gather (block b+3's stays
+            // in flight); the next id / rating window before the blocks after b+1 need it
+            if (b + 1 < nb) x0(b + 1);
+            if (wu == 1 && b + 3 < nb) {
+                // (vmcnt's field is 6 bits: at most 63 pieces, i.e. rows of <= 4 KiB)
+                if (pieces == 13) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+                else if (pieces == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+                else if (pieces == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else if (wu == 1) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            const int jn = (b + 5) * kGB;  // (block b+4's gather and the chain's ratings of b+1)
+            if (jn - kGB < n && jn > win0 + kGWin) {
+                lds_barrier();
+                if (wu == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                load_win((b + 1) * kGB);
+            }
+            lds_barrier();
+        }
+        // the user's final row, bias and |p_u|^2 (mf.pyx:264-267; the log fold's <p^2>)
+        double sq = 0;
+        if (col) {
+            const T p = P[c];
+            if (fac) {
+                pu[(int64_t)u * ldu + c] = p;
+                sq = (double)p * (double)p;
+            }
+            if (ub) bu[u] = p - hp.gm;
+        }
+        sq = wave_sum(sq);
+        if (lane == 0) sqw[w] = sq;
+        lds_barrier();
+        if (tid == 0 && psq) psq[u] = sqw[0] + sqw[1] + sqw[2] + sqw[3];
+        lds_barrier();
+    }
+}
+
 // ---------------------------------------------------------------- NMF
 //
 // NMF.sgd (matrix_factorization.pyx:646-735): within an epoch the factors are constant; every
@@ -3747,6 +4029,46 @@ int mf_svd_epoch_sq(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, nullptr, qlog, elog,
                                n_factors, biased, hp, MF_MODE_LOG, n_waves, flags, dtype, stream,
                                user_sq);
+}
+
+int mf_svd_epoch_gram(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
+                      void *bu, int32_t ldu, const void *qb, int32_t ldq, int32_t n_factors,
+                      int32_t biased, const mf_hyper_t *hp, void *qlog, double *user_sq,
+                      int32_t n_blocks, int32_t flags, int32_t dtype, void *stream)
+{
+    const int K = n_factors;
+    if (int rc = check_epoch(csr, sched, pu, bu, qb, hp, K, ldu, ldq, MF_MODE_LOG, qlog, dtype))
+        return rc;
+    const int esz = dtype == MF_F32 ? 4 : 8;
+    // (the row recursion runs one column per thread of three waves: ldq <= 192)
+    if (K < 1 || (int64_t)ldq * esz > 1024 || ldq > 3 * kWave)
+        return set_err(MF_E_UNSUPPORTED, "mf_svd_epoch_gram: 1 <= n_factors, rows of <= 1 KiB, "
+                                         "ldq <= 192");
+    const int err_col = err_column(K, ldq, dtype);
+    if (err_col <= 0) return set_err(MF_E_UNSUPPORTED, "mf_svd_epoch_gram: no error columns");
+    if (flags & ~(0xFF << MF_EPOCH_XCD_SHIFT))
+        return set_err(MF_E_ARG, "mf_svd_epoch_gram: only the XCD mask flag");
+    const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
+    if (int rc = check_xmask(xmask)) return rc;
+    if (n_sched <= 0) return 0;
+    int64_t blocks = n_blocks > 0 ? n_blocks : n_sched;
+    if (xmask) {
+        const int cnt = __builtin_popcount(xmask);
+        blocks = 8 * ((blocks + cnt - 1) / cnt);
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const int ring = gram_ring_bytes(ldq, esz);
+    if (dtype == MF_F32)
+        hipLaunchKernelGGL(mf_svd_gram_kernel<float>, dim3((unsigned)blocks), dim3(kBlock), ring, st,
+                           csr->row_ptr, csr->items, (const float *)csr->ratings, sched, n_sched,
+                           (float *)pu, (float *)bu, ldu, (const float *)qb, ldq, K, biased,
+                           cast_hyper<float>(hp), (float *)qlog, user_sq, err_col, xmask);
+    else
+        hipLaunchKernelGGL(mf_svd_gram_kernel<double>, dim3((unsigned)blocks), dim3(kBlock), ring, st,
+                           csr->row_ptr, csr->items, (const double *)csr->ratings, sched, n_sched,
+                           (double *)pu, (double *)bu, ldu, (const double *)qb, ldq, K, biased,
+                           cast_hyper<double>(hp), (double *)qlog, user_sq, err_col, xmask);
+    return check_launch("mf_svd_gram_kernel");
 }
 
 int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,

@@ -357,7 +357,7 @@ class MFEngine(ItemSync, Predictor):
                  ckpt=True, heavy=None, err_in_row=True, narrow=None, events="native",
                  join="event",
                  helpers=None, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
-                 replay_rows=None):
+                 replay_rows=None, gram=None, xcd_split=None):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -386,7 +386,11 @@ class MFEngine(ItemSync, Predictor):
           replay_rows checkpoint log: ratings per replay piece (None: replay_piece_rows())
           hot_rows    the helper-wave launch: items whose q row gets a delta replica
                       (mf_svdpp_epoch's hot rows): None = auto (hot_items()), 0 = none, n = the
-                      n most-rated items"""
+                      n most-rated items
+          gram        checkpoint log, split chunk: the heavy users by the blocked solve
+                      (mf_svd_epoch_gram, where the rows carry their errors); None / False: the
+                      lookahead chain (mf_svd_epoch_sq)
+          xcd_split   the heavy launch on XCD 0, the rest on XCDs 1-7 (None: without gram)"""
         torch = _lib.require_gpu()
         self.torch = torch
         self.algo = algo
@@ -467,15 +471,6 @@ class MFEngine(ItemSync, Predictor):
         ap = 1.0 - h.get("lr_pu", 0.0) * h.get("reg_pu", 0.0)
         self.ckpt = (self.mode == _lib.MF_MODE_LOG and bool(ckpt) and algo == "svd"
                      and esz_q <= 1024 and abs(ap) >= 0.5)
-        # ... and then splits each chunk's users in two launches on two streams: the heaviest
-        # users (their sequential chains bound a small epoch) on one XCD beside the rest on the
-        # other seven, whose log replay then overlaps the heavy chains
-        if heavy is None:
-            heavy = self._auto_heavy(row_ptr)
-        # the heavy launch keeps to XCD 0 and the rest to the other seven (disjoint L2s: the
-        # rest's log replay then does not evict the heavy chains' item rows) -- where the device
-        # deals workgroups round-robin over 8 XCDs (mf_xcd_layout), else no XCD masks
-        self.heavy_xcd = 1 if heavy > 0 and _lib.xcd_layout_ok() else 0
         # checkpoint log with MF_EPOCH_ERR_IN_ROW where the row has room: each pair's two errors
         # ride in its checkpoint row's padding (the replay gathers no elog entries)
         e0 = ((self.K + 3) & ~1) if self.dtype == _lib.MF_F32 else self.K + 2
@@ -490,6 +485,28 @@ class MFEngine(ItemSync, Predictor):
         # (read-only after construction: elog is sized for it)
         self._err_in_row = (self.ckpt and not self.narrow and e0 + 2 <= self.ldq
                             and bool(err_in_row))
+        # (a user listing an item twice: the kernels forward rows in registers)
+        self.dup_items = int(_has_duplicate_items(row_ptr, items, self.n_items, torch, dev))
+        # gram=True: the heaviest users by the blocked solve (mf_svd_epoch_gram: one workgroup
+        # per user, the block's errors from its item-row Gram matrix) instead of the lookahead
+        # body's chain, where the checkpoint rows carry their errors.  Off by default: equal to
+        # the oracle to 1e-9, but measured slower (ML-1M fp64, the top user alone: 578 us vs the
+        # lookahead chain's 187 us)
+        self.gram = (self.ckpt and self._err_in_row and not self.narrow and not self.dup_items
+                     and self.K >= 1 and bool(gram))
+        # ... and then splits each chunk's users in two launches on two streams: the heaviest
+        # users (their sequential chains bound a small epoch) beside the rest, whose log replay
+        # then overlaps the heavy users' work
+        if heavy is None:
+            heavy = self._auto_heavy(row_ptr)
+        # xcd_split: the heavy launch keeps to XCD 0 and the rest to the other seven (disjoint
+        # L2s: the rest's log replay does not evict the heavy chains' item rows) -- where the
+        # device deals workgroups round-robin over 8 XCDs (mf_xcd_layout), else no XCD masks;
+        # None: split for the lookahead chains, not for the blocked solve (its heavy users finish
+        # early, the rest then use every XCD)
+        if xcd_split is None:
+            xcd_split = not self.gram
+        self.heavy_xcd = 1 if heavy > 0 and xcd_split and _lib.xcd_layout_ok() else 0
         C = _lib.load().mf_ckpt_interval() if self.ckpt else 0
         _pu = []
         pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
@@ -560,7 +577,6 @@ class MFEngine(ItemSync, Predictor):
         # ... with helper waves (rows <= 1 KiB, no repeated items): one user chain per CU whose
         # q atomics the workgroup's other three waves issue (mf_svdpp_epoch flag
         # MF_EPOCH_SVDPP_HELPERS); the chains take users in a longest-first balanced layout
-        self.dup_items = int(_has_duplicate_items(row_ptr, items))
         self.hx = self.ydefer and self.ldq * esz <= 1024 and not self.dup_items and \
             (helpers is None or bool(helpers))
         # helper waves per chain: 3 (helpers=True) or 1 (helpers=1: MF_EPOCH_SVDPP_ONE_HELPER);
@@ -681,6 +697,7 @@ class MFEngine(ItemSync, Predictor):
         return self._err_in_row
 
     HEAVY_USERS = 128     # users in the heavy launch (measured: 64 0.231, 128 0.224, 256 0.232 ms)
+    HEAVY_USERS_GRAM = 256  # ... with the blocked solve (one workgroup per user)
     HEAVY_MAX_NNZ = 8_000_000
 
     def _auto_heavy(self, row_ptr):
@@ -694,7 +711,7 @@ class MFEngine(ItemSync, Predictor):
         if (props.multi_processor_count != 256 or nnz > self.n_chunks * self.HEAVY_MAX_NNZ
                 or self.n_users < 16 * self.HEAVY_USERS):
             return 0.0
-        return float(self.HEAVY_USERS)
+        return float(self.HEAVY_USERS_GRAM if self.gram else self.HEAVY_USERS)
 
     # ------------------------------------------------------------------ state in / out
     def set_factors(self, pu, qi, bu=None, bi=None, yj=None):
@@ -898,6 +915,18 @@ class MFEngine(ItemSync, Predictor):
                   (_lib.MF_EPOCH_CKPT_NARROW if self.narrow else 0) |
                   (xmask << _lib.MF_EPOCH_XCD_SHIFT), self.dtype, st)
 
+    def _heavy_epoch(self, sched, n_sched, st, xmask=0):
+        """The heavy users' epoch launch: the blocked solve (gram) or one lookahead chain per
+        user."""
+        if not self.gram:
+            self._epoch_sq(sched, n_sched, n_sched, st, xmask)
+            return
+        _lib.call("mf_svd_epoch_gram", ctypes.byref(self._csr), self._ptr(sched), n_sched,
+                  self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb), self.ldq,
+                  self.K, int(self.biased), ctypes.byref(self._hyper),
+                  ctypes.c_void_p(self._qlog_base), self._ptr(self.user_sq), 0,
+                  xmask << _lib.MF_EPOCH_XCD_SHIFT, self.dtype, st)
+
     def _sq_reduce(self, out, st):
         _lib.call("mf_user_sq_reduce", self._ptr(self.user_sq), self.n_users, self.K,
                   self._ptr(out), st)
@@ -954,7 +983,7 @@ class MFEngine(ItemSync, Predictor):
                     _lib.call("mf_event_record", self._nev["fork"], st)
                 _lib.call("mf_stream_wait_event", sh, self._nev["fork"])
             n_h = hv["sched"].numel()  # (the longest path first: the host may lag the GPU)
-            self._epoch_sq(hv["sched"], n_h, n_h, st, self.heavy_xcd)
+            self._heavy_epoch(hv["sched"], n_h, st, self.heavy_xcd)
             if "end" in ev:
                 ev["end"].record(self.stream)
             if "l_start" in ev:  # (the light epoch kernel's own span, on its stream)
@@ -1256,11 +1285,21 @@ class MFEngine(ItemSync, Predictor):
                           self._ptr(bufs[x]), self.dtype, st)
             x += 1
 
-def _has_duplicate_items(row_ptr, items) -> bool:
-    """True if some user lists the same item twice (the kernels then forward rows in registers)."""
+def _has_duplicate_items(row_ptr, items, n_items=None, torch=None, dev=None) -> bool:
+    """True if some user lists the same item twice (the kernels then forward rows in registers).
+    Keys user * n_items + item sorted on the device when torch / dev are given (C5's 1B ratings:
+    a host sort would take minutes), else on the host."""
     row_ptr = np.asarray(row_ptr, np.int64)
     if len(items) == 0:
         return False
+    if torch is not None and dev is not None:
+        n = int(n_items) if n_items else int(np.max(items)) + 1
+        lens = torch.from_numpy(np.diff(row_ptr)).to(dev)
+        users = torch.repeat_interleave(torch.arange(len(lens), device=dev), lens)
+        key = users * n + torch.from_numpy(np.asarray(items, np.int32)).to(dev).to(torch.int64)
+        del users
+        key = torch.sort(key).values
+        return bool((key[1:] == key[:-1]).any().item())
     users = np.repeat(np.arange(len(row_ptr) - 1, dtype=np.int64), np.diff(row_ptr))
     key = users * (int(np.max(items)) + 1) + np.asarray(items, np.int64)
     return len(np.unique(key)) != len(key)

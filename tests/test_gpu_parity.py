@@ -259,6 +259,39 @@ def test_batched_test_equals_per_call_estimate(torch, u1):
         assert [p[:3] for p in fast] == [p[:3] for p in slow]
 
 
+@pytest.mark.parametrize("name", ["svd_k20_e5", "svd_k20_e5_unbiased", "svd_k10_e3_hyper"])
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_blocked_solve_heavy_users_match_deltalog_oracle(torch, golden, u1, name, dtype):
+    """The heavy users' blocked solve (mf_svd_epoch_gram: 16-rating blocks, the errors from the
+    block's item-row Gram matrix) forced on u1's 64 heaviest users beside the lookahead chains of
+    the rest -- partial blocks, odd rating counts, the unbiased layout and separate lr / reg per
+    parameter included -- against oracle_svd_sgd_deltalog(merge=3): fp64 to 1e-9, fp32 to 1e-4;
+    and equal to the same split without the blocked solve (gram=False) within rounding."""
+    from surprise_amd import SVD
+    meta, _ = golden
+    if name == "svd_k20_e5_unbiased":  # (fp64 K=5 rows have no room for the error columns)
+        params = dict(meta["cases"]["svd_k20_e5"]["params"], biased=False)
+    else:
+        params = meta["cases"][name]["params"]
+    ts, test = u1
+    row_ptr, items, ratings = ts.csr()
+    P, f = run_oracle_log("SVD", params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
+                          merge=3)
+    fits = {}
+    for gram in (True, False):
+        algo = SVD(**params, dtype=dtype)
+        algo._engine_options = {"heavy": 64, "gram": gram}
+        algo.fit(ts)
+        eng = algo._engine
+        assert eng.logs[0]["heavy"] is not None and eng.gram == gram
+        fits[gram] = algo
+    tol = 1e-9 if dtype == "float64" else 1e-4
+    for k in ("pu", "qi", "bu", "bi"):
+        np.testing.assert_allclose(getattr(fits[True], k), f[k], rtol=0, atol=tol, err_msg=k)
+        np.testing.assert_allclose(getattr(fits[True], k), getattr(fits[False], k), rtol=0,
+                                   atol=tol, err_msg=k)
+
+
 def test_unknown_user_and_item_match_reference(torch, golden):
     """test_algorithms.py:28-57 with the reference's estimates as known answers."""
     from surprise_amd import SVD, SVDpp, Dataset, Reader
@@ -360,9 +393,9 @@ def test_c2_ml1m_svd_k100_e20_rmse_within_1e3(torch, ml1m, mode):
 def test_headline_configuration_fp64_matches_deltalog_oracle(torch, ml1m):
     """The bench headline's own kernel configuration at factor level: SVD K=100 in fp64 on the
     ML-1M-shape fold through the default path, which at this size splits every epoch into the
-    128 heaviest users' launch on XCD 0 beside the other users' on XCDs 1-7, each with its own
-    checkpoint replay, both groups' piece sums folded by one mf_log_apply (the split u1 is too
-    small to take).  pu, qi, bu, bi after 3 epochs equal oracle_svd_sgd_deltalog(merge=3) -- the
+    128 heaviest users' launch on XCD 0 beside the other users' on XCDs 1-7, each group with
+    its own checkpoint replay, both groups' piece sums folded by one mf_log_apply (the split u1
+    is too small to take).  pu, qi, bu, bi after 3 epochs equal oracle_svd_sgd_deltalog(merge=3) -- the
     schedule restated on the CPU, pinned to the reference by the u1 goldens -- to 1e-9."""
     from surprise_amd import SVD
     ts, test = ml1m
