@@ -682,7 +682,7 @@ def main():
                                  getattr(workload, "user_lo", 0))
         eng = MFEngine(csr, n_items, k, algo=a, hyper=hyper_for(a, gm), mode=md,
                        dtype=TORCH_DTYPE[dt], world=world,
-                       n_chunks=args.chunks or default_chunks(a, md, n_users_global),
+                       n_chunks=args.chunks or default_chunks(a, md, n_users_global, world),
                        **({"merge": args.merge} if args.merge else {}),
                        **({"hx_chains_per_cu": args.hx_chains} if args.hx_chains else {}),
                        **({"helpers": args.hx_helpers} if args.hx_helpers else {}),

@@ -50,20 +50,23 @@ HX_CHAINS_PER_CU_ONE = 4  # ... with one helper wave per chain (workgroups of tw
 HX_ONE_HELPER_MIN_USERS = 50_000
 
 
-# SVD++ (atomic q rows, deferred y): at most this many users (all ranks) per epoch-chunk.  Every
-# user of a chunk reads the chunk-start y_j; measured on C5's per-rank shard (1.25M users, K=128,
-# 20 epochs) the held-out RMSE is +2.7e-3 from the reference with 1 chunk, +8.1e-4 with 4,
-# +2.1e-4 with 16 (epoch 139 / 140 / 147 ms); ML-1M's 6040 users pass with 1
-SVDPP_USERS_PER_CHUNK = 100_000
-SVDPP_MAX_CHUNKS = 16  # (each chunk is one exchange of q and y on several ranks: 1 GB at C5)
+# SVD++ (atomic q rows, deferred y): at most this many users OF ONE RANK per epoch-chunk.  Every
+# user of a chunk reads the chunk-start y_j.  Measured on C5's shard (1.25M users, K=128, E=20,
+# held-out RMSE - the sequential oracle): one rank at 1 / 2 / 4 / 16 chunks +2.7e-3 / +2.5e-3 /
+# +8.1e-4 / +2.1e-4; the same users over 8 ranks at 2 chunks (78k users per rank and chunk, 625k
+# in all: C5@8's geometry) +1.6e-4 (profiles/r4_gloo8_c5.json) -- the staleness that costs
+# accuracy is y's within one rank; across ranks the rank-order merge composes it.
+# ML-1M's 6040 users pass with 1 chunk.  No cap: one GPU holding all 10M C5 users runs 125 chunks.
+SVDPP_USERS_PER_CHUNK = 80_000
 
 
-def default_chunks(algo: str, mode: str, n_users_total: int) -> int:
+def default_chunks(algo: str, mode: str, n_users_total: int, world: int = 1) -> int:
     """Epoch-chunks of the default schedules: 1 for SVD's log (the recency fold holds C4 at 20
-    epochs with one), SVD++: one per SVDPP_USERS_PER_CHUNK users of every rank, at most
-    SVDPP_MAX_CHUNKS."""
+    epochs with one); SVD++: one per SVDPP_USERS_PER_CHUNK users of a rank (n_users_total over
+    `world` ranks), so C5@8 (10M users) runs 16 chunks and the C5 shard on one GPU 16 too."""
     if algo == "svdpp" and mode == "atomic":
-        return max(1, min(SVDPP_MAX_CHUNKS, -(-int(n_users_total) // SVDPP_USERS_PER_CHUNK)))
+        per_rank = -(-int(n_users_total) // max(1, int(world)))
+        return max(1, -(-per_rank // SVDPP_USERS_PER_CHUNK))
     return 1
 
 

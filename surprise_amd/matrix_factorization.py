@@ -18,7 +18,7 @@ no CPU fallback.  Extra, keyword-only device options:
                      float atomics), "plain" (shared rows, plain stores) or "auto" ("log" for
                      SVD, "atomic" for SVD++)
   chunks_per_epoch   epoch-chunks (item merges / all-reduces per epoch); "auto" (default): 1
-                     for SVD, one per 100,000 users for SVD++ (engine.default_chunks)
+                     for SVD, one per 80,000 users of a rank for SVD++ (engine.default_chunks)
   deterministic      one wavefront, users in Trainset order: the reference's exact sequence
   n_waves            wavefronts per launch (0 = fill the GPU)
   distributed        opt-in: shard users over the torch.distributed ranks of the job (one
@@ -147,7 +147,7 @@ class _MFBase(AlgoBase):
         chunks = self.chunks_per_epoch
         if chunks == "auto":
             from .engine import default_chunks
-            chunks = default_chunks(self._algo, self._resolve_mode(), n_users)
+            chunks = default_chunks(self._algo, self._resolve_mode(), n_users, world)
         eng = MFEngine(csr, n_items, self.n_factors, algo=self._algo,
                        hyper=self._hyper(global_mean), biased=getattr(self, "biased", True),
                        dtype=self.dtype, mode=self._resolve_mode(),

@@ -499,3 +499,19 @@ def test_roofline_executed_bytes_and_span_bounds():
     assert all(0 < v["frac"] <= 1 for v in dk["launches"].values())
     assert "frac" not in rl["survey_8d"]
     assert abs(rl["chain_latency"]["frac"] - 199 / 246) < 1e-12
+
+
+def test_default_chunks_counts_users_per_rank():
+    """SVD++'s epoch-chunks follow the users of ONE rank (engine.SVDPP_USERS_PER_CHUNK): C5@8
+    (10M users, 8 ranks) and the C5 shard on one GPU both run 16 chunks of <= 80k users per rank,
+    the geometries the scale tests pin; one GPU with all of C5 runs 125; SVD's log runs 1."""
+    from surprise_amd.engine import SVDPP_USERS_PER_CHUNK, default_chunks
+    assert default_chunks("svdpp", "atomic", 10_000_000, 8) == 16
+    assert default_chunks("svdpp", "atomic", 1_250_000) == 16
+    assert default_chunks("svdpp", "atomic", 1_250_000, 8) == 2
+    assert default_chunks("svdpp", "atomic", 10_000_000) == 125
+    assert default_chunks("svdpp", "atomic", 6040) == 1
+    assert default_chunks("svd", "log", 10_000_000) == 1
+    for users, world in ((10_000_000, 8), (1_250_000, 1), (999_999, 3)):
+        c = default_chunks("svdpp", "atomic", users, world)
+        assert -(-users // world) <= c * SVDPP_USERS_PER_CHUNK
