@@ -335,6 +335,12 @@ def sum_over_ranks(ctx, xs, torch):
     return t.cpu().tolist()
 
 
+def shape_key(shape, users=0):
+    """Name of a workload's measured-traffic file: the shape, with _u<N> for a c4 / c5 user
+    prefix (the C5 shard is c5_u1250000; the full 1B-rating C5 is c5)."""
+    return shape + ("_u%d" % users if users and shape in ("c4", "c5") else "")
+
+
 def traffic_for(algo, K, shape, dtype="f32"):
     """Measured HBM-side bytes per step (profiles/traffic_<algo>_k<K>_<shape>[_f64].json, written
     by tools/profile.sh from separate rocprofv3 --pmc passes)."""
@@ -653,6 +659,16 @@ def main():
     if world == 1 and args.gpus > 1:
         spawn_ranks(args.gpus)  # exits
     rank = int(os.environ.get("RANK", "0"))
+    if args.shape in ("c4", "c5") and rank == 0:
+        # the full C5 (1B ratings) spends minutes in host-side generation and in the engine's
+        # per-chunk preparation: a heartbeat keeps the run visibly alive meanwhile
+        import threading
+
+        def beat():
+            while True:
+                time.sleep(45)
+                note("alive")
+        threading.Thread(target=beat, daemon=True).start()
 
     # host-side workload first (no GPU touched yet)
     csr, test, n_items, n_users_global, desc = workload(args, rank, world)
@@ -737,7 +753,8 @@ def main():
     lay = layout_of(eng)
     chain = time_top_chain(eng, torch) if args.shape == "ml-1m" and not args.no_chain_probe \
         else None
-    rl = roofline_of(algo, K, args.dtype, n_train, ms_step, args.shape, phases, lay, chain)
+    rl = roofline_of(algo, K, args.dtype, n_train, ms_step, shape_key(args.shape, args.users),
+                     phases, lay, chain)
     rl.update({
         "kernel": "dominant: %s; step (%s): %s" % (
             (rl.get("dominant_kernel") or {}).get("kernel"), mode,
@@ -781,7 +798,7 @@ def main():
         chain2 = None if args.no_chain_probe else time_top_chain(e32, torch)
         ms2 = el2 / args.steps * 1e3
         leg = {"dtype": other, "value": n_train * args.steps / el2, "ms_per_step": ms2,
-               "roofline": roofline_of(algo, K, other, n_train, ms2, args.shape, ph, lay2,
+               "roofline": roofline_of(algo, K, other, n_train, ms2, shape_key(args.shape, args.users), ph, lay2,
                                        chain2)}
         leg["roofline"]["phases_gpu_ms"] = ph
         if not args.no_rmse:
@@ -949,6 +966,7 @@ def rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch, mak
     se, n, se_mu = sum_over_ranks(ctx, [float(((tr - est) ** 2).sum()), float(len(tr)),
                                         float(((tr - gm) ** 2).sum())], torch)
     out = {"gpu": (se / n) ** .5, "global_mean_baseline": (se_mu / n) ** .5,
+           "below_global_mean": bool(se < se_mu),
            "fit": "%s K=%d E=%d %s (%s) through the bench engine, %d held-out ratings over %d "
                   "rank(s)" % (args.algo.upper(), K, E, eng.tdt, mode, int(n), world)}
     del eng

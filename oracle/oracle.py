@@ -138,6 +138,29 @@ def svdpp_sgd_hotstale(row_ptr, items, ratings, n_items, K, n_epochs, global_mea
     return pu, qi, yj, bu, bi
 
 
+def svdpp_sgd_stalelog(row_ptr, items, ratings, n_items, K, n_epochs, global_mean, hp, pu, qi,
+                       yj, stale, chunk_of_user=None, n_chunks=1, merge=3, bu=None, bi=None):
+    """SVD++ with y deferred per epoch-chunk, q / b live except the items with stale[i] != 0,
+    whose steps are logged against the chunk-start row and folded after the chunk (merge 3:
+    recency weights, 2: count-aware).  Returns (pu, qi, yj, bu, bi)."""
+    row_ptr, items, ratings = _csr_args(row_ptr, items, ratings)
+    n_users = len(row_ptr) - 1
+    pu = np.ascontiguousarray(pu, dtype=np.float64)
+    qi = np.ascontiguousarray(qi, dtype=np.float64)
+    yj = np.ascontiguousarray(yj, dtype=np.float64)
+    bu = np.zeros(n_users) if bu is None else np.ascontiguousarray(bu, dtype=np.float64)
+    bi = np.zeros(n_items) if bi is None else np.ascontiguousarray(bi, dtype=np.float64)
+    stale = np.ascontiguousarray(stale, dtype=np.int32)
+    c = (np.zeros(n_users, np.int32) if chunk_of_user is None
+         else np.ascontiguousarray(chunk_of_user, dtype=np.int32))
+    lib().oracle_svdpp_sgd_stalelog(
+        ctypes.c_int64(n_users), ctypes.c_int64(n_items), _p(row_ptr), _p(items), _p(ratings),
+        ctypes.c_int32(K), ctypes.c_int32(n_epochs), ctypes.c_double(global_mean),
+        ctypes.byref(hp), _p(c), ctypes.c_int32(n_chunks), _p(stale), ctypes.c_int32(merge),
+        _p(pu), _p(qi), _p(yj), _p(bu), _p(bi))
+    return pu, qi, yj, bu, bi
+
+
 def svd_sgd_groups(row_ptr, items, ratings, n_items, K, n_epochs, biased, global_mean, hp,
                    pu, qi, group_of_user, n_groups, chunk_of_user=None, n_chunks=1,
                    bu=None, bi=None):

@@ -8,6 +8,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 tag = sys.argv[1]
 PMC_STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 11  # warmup + timed + phase steps of a --pmc run
 SETUP = ("elementwise", "rocclr", "user_sq_kernel", "fill")  # one-off setup kernels, not in a step
@@ -86,7 +87,12 @@ if fetch and write and bench_line:
                "workload": cfg["workload"]}
     summary["traffic"] = traffic
     dt = cfg.get("dtype", "f32")
-    name = "traffic_%s_k%d_%s%s.json" % (cfg["algo"], cfg["n_factors"], cfg.get("shape", "ml-1m"),
+    import bench
+    U_FULL = {"c4": 2_000_000, "c5": 10_000_000}
+    shp = cfg.get("shape", "ml-1m")
+    users = cfg.get("users_total", 0)
+    key = bench.shape_key(shp, users if users and users < U_FULL.get(shp, 0) else 0)
+    name = "traffic_%s_k%d_%s%s.json" % (cfg["algo"], cfg["n_factors"], key,
                                          "" if dt == "f32" else "_" + dt)
     with open(os.path.join(prof, name), "w") as f:
         json.dump(traffic, f, indent=1)
