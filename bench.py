@@ -113,6 +113,9 @@ def parse():
     p.add_argument("--no-chain-probe", action="store_true",
                    help="skip timing the heaviest user's chain alone (profiling runs: its extra "
                         "epoch-kernel launches would mix into the kernel's statistics)")
+    p.add_argument("--qlog", action="store_true",
+                   help="SVD++: the q log (item rows read-only within a chunk, gradients folded "
+                        "after it; engine option qlog) instead of the float-atomic schedule")
     p.add_argument("--no-c4", action="store_true",
                    help="skip the C4 leg (BASELINE configs[3]'s shape on this GPU)")
     p.add_argument("--users", type=int, default=0,
@@ -704,6 +707,7 @@ def main():
                        **({"helpers": args.hx_helpers} if args.hx_helpers else {}),
                        **({"heavy": args.heavy} if args.heavy >= 0 else {}),
                        **({"hot_rows": args.hot_rows} if args.hot_rows >= 0 else {}),
+                       **({"qlog": True} if args.qlog and a == "svdpp" else {}),
                        **({"replay_rows": args.replay_rows} if args.replay_rows else {}),
                        **({"gram": bool(args.gram)} if args.gram >= 0 else {}),
                        **({"xcd_split": bool(args.xcd_split)} if args.xcd_split >= 0 else {}))
@@ -740,7 +744,9 @@ def main():
         "data": "synthetic planted ratings (surprise_amd.synthetic, seed 0): " + desc,
         "config": {"workload": "%s n_factors=%d %s, one epoch per step over %d training ratings "
                                "per GPU (rank 0), mode=%s, chunks/epoch=%d, %s scaling over %d "
-                               "GPU(s)" % (algo.upper(), K, args.dtype, n_train, mode,
+                               "GPU(s)" % (algo.upper(), K, args.dtype, n_train,
+                                           mode + ("+qlog" if getattr(eng, "qlog_pp", False)
+                                                   else ""),
                                            eng.n_chunks, args.scaling, world),
                    "shape": args.shape, "algo": algo, "n_factors": K, "dtype": args.dtype,
                    "train_ratings_rank0": n_train, "users_total": n_users_global,

@@ -151,6 +151,25 @@ int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, v
                    int32_t flags, int32_t *status, const uint8_t *hot, int32_t dtype,
                    void *stream);
 
+/*
+ * One epoch-chunk of SVD++ SGD (matrix_factorization.pyx:463-498) with the item rows READ-ONLY
+ * for the chunk (the q log): the per-user affine form of mf_svdpp_epoch with y deferred (ycbuf,
+ * as MF_MODE_ATOMIC with ycbuf: mf_svdpp_y_fold afterwards), and instead of float atomics on
+ * q_i / b_i each rating's gradient err_k [p_k + m_k | 1] (m_k: u_impl before rating k; the bias
+ * column K holds err_k) is stored as row log_row0[u] + j of qlog ([rows][ldq], j = the rating's
+ * index in the user's CSR row; log_row0: int64 per user, valid for the scheduled users).  Fold
+ * with mf_log_reduce (perm = the chunk's log rows grouped by item, recency weights) and
+ * mf_log_apply, as the SVD gradient log: q_i += lr (S_i - W reg q_i), i.e. the reference's
+ * steps on the row to first order (oracle_svdpp_sgd_stalelog, every item stale).  Rows of
+ * <= 1 KiB, no repeated items; flags: MF_EPOCH_DUP_ITEMS must be clear, XCD mask bits allowed.
+ * n_waves <= 0: one wave per user up to the launch's cap.  A user's log segment must stay below
+ * 1 GiB.  Replaces matrix_factorization.pyx:487 / :494-495 (the item-side updates).
+ */
+int mf_svdpp_epoch_qlog(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
+                        void *bu, int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
+                        const mf_hyper_t *hp, void *qlog, const int64_t *log_row0, void *ycbuf,
+                        int32_t n_waves, int32_t flags, int32_t dtype, void *stream);
+
 /* After mf_svdpp_epoch with hot rows: row i += row n_items + i and the replica row zeroed, for
  * i in hot_items[0 .. n_hot). */
 int mf_svdpp_hot_fold(void *qb, int32_t ldq, int32_t n_items, const int32_t *hot_items,

@@ -41,7 +41,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
                     int hx, double *psq, int err_col, int ck_ld, int32_t *status,
-                    const uint8_t *hot, void *stream);
+                    const uint8_t *hot, const int64_t *urow, void *stream);
 }  // namespace mf_ext
 
 namespace {
@@ -273,6 +273,10 @@ struct Buf<float> {
     __device__ static __forceinline__ float lds(rsrc_t r, uint32_t voff, uint32_t soff) {
         return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX));
     }
+    template <int AUX>
+    __device__ static __forceinline__ void sts(rsrc_t r, uint32_t voff, uint32_t soff, float v) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, AUX);
+    }
 };
 
 template <>
@@ -295,6 +299,12 @@ struct Buf<double> {
     template <int AUX>
     __device__ static __forceinline__ double lds(rsrc_t r, uint32_t voff, uint32_t soff) {
         return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, AUX));
+    }
+    template <int AUX>
+    __device__ static __forceinline__ void sts(rsrc_t r, uint32_t voff, uint32_t soff, double v) {
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v), r,
+            voff, soff, AUX);
     }
 };
 
@@ -1324,14 +1334,23 @@ __device__ void pp_ring_helper(PPRing<T, G, H> *ring, int h, T *qb, int ldq, int
 // replica at row n_items + i of qb: the chains of odd workgroups add its deltas there, the
 // others to the row itself, and every read of the row adds the replica (the value one row would
 // hold: no staleness added); mf_svdpp_hot_fold folds the replicas back after the chunk.
-template <typename T, int G, bool HX, bool HOT = false, bool SB = false, int H = kHxHelpers>
+//
+// q log (LQ, mf_svdpp_epoch_qlog): the item rows are a read-only chunk-start snapshot; each
+// rating's q / b gradient g_k = err_k [s_k | 1] is stored (plain stores) as row urow[u] + k of the
+// chunk's log instead of being added to the row, and mf_log_reduce / mf_log_apply fold the log
+// after the chunk with the recency weights, as the SVD gradient log (oracle:
+// oracle_svdpp_sgd_stalelog with every item stale).  No float atomic, no helper wave.
+template <typename T, int G, bool HX, bool HOT = false, bool SB = false, int H = kHxHelpers,
+          bool LQ = false>
 __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *ycbuf, int K,
     Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, PPRing<T, G, H> *ring,
-    int32_t *status, const uint8_t *__restrict__ hot = nullptr)
+    int32_t *status, const uint8_t *__restrict__ hot = nullptr, T *qlog = nullptr,
+    const int64_t *__restrict__ urow = nullptr)
 {
+    static_assert(!(LQ && (HX || HOT)), "the q log: no helper waves, no hot replicas");
     using L = Lane8<T>;
     using vec = typename L::vec;
     constexpr int W = L::W;
@@ -1362,6 +1381,10 @@ __device__ __forceinline__ void epoch_body_pp_la(
     uint32_t cq[G], cu[G], cq1[U], cy1[U];
     vec one[G], lrp[G], ap[G], lry[G], lrpy[G], lrq[G], nrq[G];
     const T dc = T(1) - hp.lr_yj * hp.reg_yj;
+    // a lane past the row: its column offset is past the item table AND past any user's log
+    // segment (< 2^30 bytes) -- both ranges dropped (voffset + soffset, no 32-bit wrap)
+    constexpr uint32_t kColOob = 0x7FFFF000u;
+    const uint32_t col_oob = LQ ? kColOob : q_oob;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int c = lane + kWave * u;
@@ -1372,7 +1395,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
     for (int v = 0; v < G; ++v) {
         const int c0 = (lane + kWave * v) * W;
         const uint32_t b = (uint32_t)c0 * sizeof(T);
-        cq[v] = c0 < ldq ? b : q_oob;
+        cq[v] = c0 < ldq ? b : col_oob;
         cu[v] = c0 < ldu ? b : y_oob;  // >= the pu / ycbuf records (K elements) too: dropped
 #pragma unroll
         for (int e = 0; e < W; ++e) {
@@ -1407,6 +1430,8 @@ __device__ __forceinline__ void epoch_body_pp_la(
         const T *__restrict__ rt = ratings + s;
         const rsrc_t p_rs = make_rsrc(pu + (int64_t)u * ldu, (uint32_t)K * sizeof(T));
         const rsrc_t b_rs = make_rsrc(bu + u, sizeof(T));
+        // LQ: the user's rows of the chunk's log (row k = its k-th rating)
+        const rsrc_t l_rs = LQ ? make_rsrc(qlog + urow[u] * ldq, (uint32_t)n * qrow) : q_rs;
         const T rs_n = T(1) / sqrt(T(n));  // mf.pyx:470-476
 
         vec p0[G];
@@ -1495,6 +1520,16 @@ __device__ __forceinline__ void epoch_body_pp_la(
             }
         };
         auto flush = [&]() {  // the float atomics of the previous bank's ratings
+            if constexpr (LQ) {  // ... or (the q log) the bank's gradient rows, plain stores
+#pragma unroll
+                for (int d = 0; d < kB; ++d) {
+#pragma unroll
+                    for (int v = 0; v < G; ++v) L::template sts<0>(l_rs, cq[v], dlo[d], dl[d][v]);
+                    if constexpr (SB)
+                        Buf<T>::template sts<0>(l_rs, lane == 0 ? kbo : kColOob, dlo[d], dlb[d]);
+                }
+                return;
+            }
             if constexpr (HX) {  // ... handed to the helper waves through the ring
                 constexpr int R = PPRing<T, G, H>::R;
                 bool room = false;
@@ -1593,11 +1628,18 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 Dm[v] = lry[v] * q;
                 px += qn[v] * (P[v] + M[v]);
                 py += qn[v] * (lrpy[v] * q);
-                dl[d][v] = err * (lrq[v] * sk) + nrq[v] * q;  // mf.pyx:489, :492
+                if constexpr (LQ) dl[d][v] = err * sk;  // the gradient (the fold applies lr, reg)
+                else dl[d][v] = err * (lrq[v] * sk) + nrq[v] * q;  // mf.pyx:489, :492
             }
-            if constexpr (SB) dlb[d] = hp.lr_bi * (err - hp.reg_bi * bb[bk][d]);  // mf.pyx:489
+            if constexpr (SB) {
+                if constexpr (LQ) dlb[d] = err;
+                else dlb[d] = hp.lr_bi * (err - hp.reg_bi * bb[bk][d]);  // mf.pyx:489
+            }
             const bool hot_d = HOT && to_rep && ((hm[bk] >> d) & 1u);
-            dlo[d] = valid ? (hot_d ? bo[bk][d] + rep_shift : bo[bk][d]) : bo[bk][d] + q_oob;
+            if constexpr (LQ)  // (past the user's segment: dropped)
+                dlo[d] = (uint32_t)(valid ? k : n) * qrow;
+            else
+                dlo[d] = valid ? (hot_d ? bo[bk][d] + rep_shift : bo[bk][d]) : bo[bk][d] + q_oob;
             T Xn, Yn;
             wave_sum2_u(L::hsum(px), L::hsum(py), Xn, Yn);  // X_{k+1}, Y_{k+1}
             if constexpr (SB) Xn += bb[bn][dn];  // (the next item's bias: s_k's column K is 1)
@@ -1752,6 +1794,17 @@ __global__ __launch_bounds__(kWave * (1 + H)) void mf_svdpp_hx_kernel(MF_EPOCH_P
     }
 }
 
+// SVD++ with the q log (mf_svdpp_epoch_qlog): every wave a user chain, the item rows read-only,
+// each rating's gradient row stored to the chunk's log (urow[u]: the user's first log row)
+template <typename T, int G, bool SB>
+__global__ __launch_bounds__(kBlock) void mf_svdpp_qlog_kernel(MF_EPOCH_PARAMS,
+                                                              const int64_t *urow)
+{
+    epoch_body_pp_la<T, G, false, false, SB, 1, true>(
+        row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, elog, K, hp, n_items,
+        n_waves_req, xmask, (PPRing<T, G, 1> *)nullptr, nullptr, nullptr, qlog, urow);
+}
+
 }  // namespace
 
 #ifdef MF_TU_EPOCH
@@ -1761,7 +1814,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
                     int hx, double *psq, int err_col, int ck_ld, int32_t *status,
-                    const uint8_t *hot, void *stream)
+                    const uint8_t *hot, const int64_t *urow, void *stream)
 {
     if ((psq || err_col) && (PP || M != kLog || !elog))
         return set_err(MF_E_UNSUPPORTED, "user_sq / errors in rows: the SVD checkpoint log only");
@@ -1774,8 +1827,11 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
         return set_err(MF_E_UNSUPPORTED, "checkpoint log: SVD, MF_MODE_LOG, ldq * size <= 1 KiB only");
     // (with the kLog snapshot the error stays stale for the whole chunk and the undamped sum of a
     // popular item's c_u diverges: measured held-out RMSE 1.82 on ML-1M)
-    if (elog && PP && M != kAtomic)
-        return set_err(MF_E_UNSUPPORTED, "deferred y: MF_MODE_ATOMIC only");
+    // ... unless the q log's chunks are small (mf_svdpp_epoch_qlog: urow given)
+    if (elog && PP && !(M == kAtomic || (M == kLog && urow)))
+        return set_err(MF_E_UNSUPPORTED, "deferred y: MF_MODE_ATOMIC, or the q log");
+    if (urow && !(PP && M == kLog && elog && qlog && !dups && !hx && !hot))
+        return set_err(MF_E_UNSUPPORTED, "the q log: SVD++, deferred y, no repeated items");
     if (hx && !(PP && M == kAtomic && elog && !dups))
         return set_err(MF_E_UNSUPPORTED, "helper waves: SVD++, MF_MODE_ATOMIC, deferred y, no repeated items");
     if (hot && !hx) return set_err(MF_E_ARG, "hot-row replicas: the helper-wave launch only");
@@ -1786,7 +1842,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     const bool sb = hx && !hot && whole;
     // ... and the SVD checkpoint epoch with narrow rows (the rows hold the factor columns only)
     const bool sbk = !PP && M == kLog && elog && ck_ld < ldq && err_col <= 0 && whole;
-    return dispatch_g<T>(sb || sbk ? K : ldq, [&](auto gc) -> int {
+    return dispatch_g<T>(sb || sbk || (urow && whole) ? K : ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         if constexpr (PP && M == kAtomic && V <= kLaMaxG) {
             if (hx) {  // one workgroup per chain: wave 0 trains, waves 1..hx issue the q atomics
@@ -1806,6 +1862,20 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
             }
         } else {
             if (hx) return set_err(MF_E_UNSUPPORTED, "helper waves: rows of <= 1 KiB");
+        }
+        if constexpr (PP && M == kLog && V <= kLaMaxG) {
+            if (urow) {  // the q log: a user chain per wave, gradient rows to the chunk's log
+                auto kern = whole ? mf_svdpp_qlog_kernel<T, V, true> : mf_svdpp_qlog_kernel<T, V, false>;
+                hipLaunchKernelGGL(kern, dim3(grid_for_waves_x(waves, xmask)), dim3(kBlock), 0,
+                                   (hipStream_t)stream, csr->row_ptr, csr->items,
+                                   (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
+                                   (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
+                                   cast_hyper<T>(hp), csr->n_items, waves, xmask, nullptr, 0, ldq,
+                                   urow);
+                return check_launch("mf_svdpp_qlog_kernel");
+            }
+        } else {
+            if (urow) return set_err(MF_E_UNSUPPORTED, "the q log: rows of <= 1 KiB");
         }
         if constexpr (M == kLog && !PP && V <= kLaMaxG && MF_LA) {
             if (elog) {  // the checkpoint log
@@ -1836,7 +1906,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
 template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
     void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, int, double *,
-    int, int, int32_t *, const uint8_t *, void *);
+    int, int, int32_t *, const uint8_t *, const int64_t *, void *);
 }  // namespace mf_ext
 #else  // the main translation unit
 
@@ -3867,7 +3937,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
                  int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                  int32_t biased, const mf_hyper_t *hp, int32_t mode, int32_t n_waves, int32_t flags,
                  int32_t dtype, void *stream, double *psq = nullptr, int32_t *status = nullptr,
-                 const uint8_t *hot = nullptr)
+                 const uint8_t *hot = nullptr, const int64_t *urow = nullptr)
 {
     const bool dups = flags & MF_EPOCH_DUP_ITEMS;
     // helper waves per chain: 3, or 1 (MF_EPOCH_SVDPP_ONE_HELPER); 0 = no helper-wave launch
@@ -3907,7 +3977,8 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         constexpr int M = decltype(mode_c)::value;
         return mf_ext::launch_epoch_tm<T, M, PP>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj,
                                                   qlog, elog, K, biased, hp, waves, dups, xmask,
-                                                  hx, psq, err_col, ck_ld, status, hot, stream);
+                                                  hx, psq, err_col, ck_ld, status, hot, urow,
+                                                  stream);
     };
     auto by_mode = [&](auto tag_t) -> int {
         switch (mode) {
@@ -4079,6 +4150,19 @@ int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, v
     return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, ycbuf,
                               n_factors, 1, hp, mode, n_waves, flags, dtype, stream, nullptr,
                               status, hot);
+}
+
+int mf_svdpp_epoch_qlog(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
+                        void *bu, int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
+                        const mf_hyper_t *hp, void *qlog, const int64_t *log_row0, void *ycbuf,
+                        int32_t n_waves, int32_t flags, int32_t dtype, void *stream)
+{
+    if (!qlog || !log_row0 || !ycbuf) return set_err(MF_E_ARG, "the q log needs qlog, log_row0, ycbuf");
+    if (flags & ~(MF_EPOCH_DUP_ITEMS | (0xFF << MF_EPOCH_XCD_SHIFT)))
+        return set_err(MF_E_ARG, "mf_svdpp_epoch_qlog: flags MF_EPOCH_DUP_ITEMS / XCD mask only");
+    return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, ycbuf,
+                              n_factors, 1, hp, MF_MODE_LOG, n_waves, flags, dtype, stream,
+                              nullptr, nullptr, nullptr, log_row0);
 }
 
 int mf_svdpp_hot_fold(void *qb, int32_t ldq, int32_t n_items, const int32_t *hot_items,

@@ -108,12 +108,14 @@ def position_users(row_ptr):
     return np.repeat(np.arange(len(row_ptr) - 1, dtype=np.int32), np.diff(row_ptr))
 
 
-def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS):
+def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS, local=False):
     """Item grouping of one epoch-chunk's delta-log rows (MF_MODE_LOG).
 
     Returns (perm, piece_beg, item_piece_ptr, counts): perm = CSR positions of the ratings of
     `users`, grouped by item, increasing position within an item (the reference's user order);
-    an item's rows are cut into pieces of <= piece_rows; counts[i] = ratings of item i."""
+    an item's rows are cut into pieces of <= piece_rows; counts[i] = ratings of item i.
+    local=True: perm holds chunk-local log rows instead -- the users' ratings numbered in
+    ascending user order (chunk_log_rows: the SVD++ q log's per-chunk buffer)."""
     row_ptr = np.asarray(row_ptr, np.int64)
     users = np.sort(np.asarray(users, np.int64))
     starts, ends = row_ptr[users], row_ptr[users + 1]
@@ -121,11 +123,21 @@ def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS):
     tot = int(lens.sum())
     ks = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(tot)
     it = np.asarray(items)[ks]
-    perm = ks[stable_argsort(it)].astype(np.int32)
+    order = stable_argsort(it)
+    perm = (order if local else ks[order]).astype(np.int32)
     counts = np.bincount(it, minlength=n_items).astype(np.int64)
     offs = np.concatenate([[0], np.cumsum(counts)])
     item_piece_ptr, piece_beg = piece_bounds(offs, counts, piece_rows)
     return perm, piece_beg.astype(np.int32), item_piece_ptr, counts.astype(np.int32)
+
+
+def chunk_log_rows(row_ptr, users):
+    """First chunk-local log row of each of `users` (the SVD++ q log: a chunk's ratings numbered
+    in ascending user order, as log_layout(local=True)): (sorted users, int64 rows)."""
+    row_ptr = np.asarray(row_ptr, np.int64)
+    users = np.sort(np.asarray(users, np.int64))
+    lens = row_ptr[users + 1] - row_ptr[users]
+    return users, np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
 
 
 def item_positions(row_ptr, items, users, n_items):
@@ -360,7 +372,7 @@ class MFEngine(ItemSync, Predictor):
                  ckpt=True, heavy=None, err_in_row=True, narrow=None, events="native",
                  join="event",
                  helpers=None, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
-                 replay_rows=None, gram=None, xcd_split=None):
+                 replay_rows=None, gram=None, xcd_split=None, qlog=None):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -393,7 +405,11 @@ class MFEngine(ItemSync, Predictor):
           gram        checkpoint log, split chunk: the heavy users by the blocked solve
                       (mf_svd_epoch_gram, where the rows carry their errors); None / False: the
                       lookahead chain (mf_svd_epoch_sq)
-          xcd_split   the heavy launch on XCD 0, the rest on XCDs 1-7 (None: without gram)"""
+          xcd_split   the heavy launch on XCD 0, the rest on XCDs 1-7 (None: without gram)
+          qlog        SVD++: the item rows read-only within an epoch-chunk, each rating's q / b
+                      gradient logged (mf_svdpp_epoch_qlog) and folded after the chunk with the
+                      recency weights, y deferred -- no float atomics (oracle:
+                      oracle_svdpp_sgd_stalelog); None / False: the atomic schedule"""
         torch = _lib.require_gpu()
         self.torch = torch
         self.algo = algo
@@ -416,6 +432,12 @@ class MFEngine(ItemSync, Predictor):
         if self.deterministic:
             mode, n_chunks, n_waves = "plain", 1, 1
         self.mode = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
+        # SVD++ q log: MF_MODE_LOG's log / fold machinery with the deferred-y lookahead chain
+        esz0 = 8 if self.dtype == _lib.MF_F64 else 4
+        self.qlog_pp = (algo == "svdpp" and not self.deterministic and bool(qlog)
+                        and default_ldq(n_factors, self.dtype) * esz0 <= 1024)
+        if self.qlog_pp:
+            self.mode = _lib.MF_MODE_LOG
         # (the user-bias column of the SVD log's lookahead body: that schedule's rows only)
         self.ldq = default_ldq(self.K, self.dtype,
                                user_bias_col=algo == "svd" and self.mode == _lib.MF_MODE_LOG)
@@ -430,7 +452,8 @@ class MFEngine(ItemSync, Predictor):
         if events not in ("native", "torch") or join not in ("event", "kernel"):
             raise ValueError("events must be 'native' or 'torch', join 'event' or 'kernel'")
         self.n_waves = int(n_waves)
-        if self.n_waves <= 0 and algo == "svdpp" and not self.deterministic:
+        # (the q log reads the chunk-start rows whatever the users in flight: the launch default)
+        if self.n_waves <= 0 and algo == "svdpp" and not self.deterministic and not self.qlog_pp:
             # SVD++ with shared item rows: at most SVDPP_WAVES_PER_CU users in flight per CU.
             # Users that start later then see the q rows (float atomics) of the users before
             # them, as the reference's sequential order does; with every ML-1M user in flight at
@@ -490,6 +513,9 @@ class MFEngine(ItemSync, Predictor):
                             and bool(err_in_row))
         # (a user listing an item twice: the kernels forward rows in registers)
         self.dup_items = int(_has_duplicate_items(row_ptr, items, self.n_items, torch, dev))
+        if self.qlog_pp and self.dup_items:
+            raise ValueError("qlog: a user lists an item twice (the q log reads each item row "
+                             "once per rating from the chunk-start table)")
         # gram=True: the heaviest users by the blocked solve (mf_svd_epoch_gram: one workgroup
         # per user, the block's errors from its item-row Gram matrix) instead of the lookahead
         # body's chain, where the checkpoint rows carry their errors.  Off by default: equal to
@@ -554,7 +580,8 @@ class MFEngine(ItemSync, Predictor):
                 if self.ckpt:
                     rows = replay_piece_rows(row_ptr, us) if replay_rows is None else \
                         max(1, int(replay_rows))
-                perm, pb, ipp, cnt = log_layout(row_ptr, items, us, self.n_items, rows)
+                perm, pb, ipp, cnt = log_layout(row_ptr, items, us, self.n_items, rows,
+                                                local=self.qlog_pp)
                 lg = dict(sched=to_dev(us), perm=to_dev(perm), pb=to_dev(pb), ipp=to_dev(ipp),
                           n_pieces=len(pb) - 1, cnt=cnt)
                 if self.ckpt:
@@ -575,13 +602,13 @@ class MFEngine(ItemSync, Predictor):
         self.counts = [to_dev(t) for t in self._totals_local]  # this rank's n_r per chunk
         # SVD++ in atomic mode: the end-of-user y update deferred to a per-item fold after each
         # chunk (mf_svdpp_y_fold; ydefer=False: float atomics at each user's end)
-        self.ydefer = (algo == "svdpp" and self.mode == _lib.MF_MODE_ATOMIC
-                       and not self.deterministic and bool(ydefer))
+        self.ydefer = (algo == "svdpp" and (self.mode == _lib.MF_MODE_ATOMIC or self.qlog_pp)
+                       and not self.deterministic and (bool(ydefer) or self.qlog_pp))
         # ... with helper waves (rows <= 1 KiB, no repeated items): one user chain per CU whose
         # q atomics the workgroup's other three waves issue (mf_svdpp_epoch flag
         # MF_EPOCH_SVDPP_HELPERS); the chains take users in a longest-first balanced layout
         self.hx = self.ydefer and self.ldq * esz <= 1024 and not self.dup_items and \
-            (helpers is None or bool(helpers))
+            (helpers is None or bool(helpers)) and not self.qlog_pp
         # helper waves per chain: 3 (helpers=True) or 1 (helpers=1: MF_EPOCH_SVDPP_ONE_HELPER);
         # None: by the users per epoch-chunk (HX_ONE_HELPER_MIN_USERS)
         if helpers is None:
@@ -669,6 +696,14 @@ class MFEngine(ItemSync, Predictor):
                 if rows >= (1 << 30):
                     raise _lib.SurpriseAMDError("checkpoint log too large for 32-bit positions")
                 self.qlog = z(max(rows, 1), self.ldc)
+                self._qlog_base = self.qlog.data_ptr()
+            elif self.qlog_pp:  # SVD++ q log: one chunk's rows (urow: each user's first row)
+                urow = np.zeros(max(self.n_users, 1), np.int64)
+                for us in self._chunk_users:
+                    su, r0 = chunk_log_rows(row_ptr, us)
+                    urow[su] = r0
+                self.urow = to_dev(urow)
+                self.qlog = z(max(max(int(t.sum()) for t in self._totals_local), 1), ldq)
                 self._qlog_base = self.qlog.data_ptr()
             else:  # the gradient log: the kernels index it by absolute CSR position k
                 self.qlog = z(max(k_hi - k_lo, 1), ldq)
@@ -826,6 +861,11 @@ class MFEngine(ItemSync, Predictor):
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
                       self.ldq, self.K, int(self.biased), ctypes.byref(self._hyper), self.mode,
                       qlog, elog, n_waves, flags, self.dtype, st)
+        elif self.qlog_pp:
+            _lib.call("mf_svdpp_epoch_qlog", ctypes.byref(self._csr), self._ptr(sched), n_sched,
+                      self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
+                      self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper), qlog,
+                      self._ptr(self.urow), self._ptr(self.ycbuf), n_waves, flags, self.dtype, st)
         else:
             _lib.call("mf_svdpp_epoch", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),

@@ -157,3 +157,24 @@ def test_two_rank_gloo_equals_group_sum_schedule(tmp_path, n_chunks):
     np.testing.assert_array_equal(res[0]["bu"], ebu)
     np.testing.assert_allclose(res[0]["qi"], eqi, rtol=0, atol=1e-15)
     np.testing.assert_allclose(res[0]["bi"], ebi, rtol=0, atol=1e-15)
+
+
+def test_chunk_users_groups_long_chains():
+    """A few users whose chains outlast a chunk (> 1/256 of its ratings) all land in chunk 0
+    (the full C5's 9 users of 200k-600k ratings); many such users, or one, leave the
+    round-robin dealing unchanged."""
+    rng = np.random.RandomState(2)
+    deg = rng.randint(1, 100, size=100_000)
+    deg[[5, 77, 900, 4242]] = [60_000, 50_000, 40_000, 30_000]
+    row_ptr = np.concatenate([[0], np.cumsum(deg)])
+    chunks = chunk_users(np.arange(len(deg)), row_ptr, 8)
+    assert set(chunks[0][:4].tolist()) == {5, 77, 900, 4242}
+    assert all(not ({5, 77, 900, 4242} & set(c.tolist())) for c in chunks[1:])
+    np.testing.assert_array_equal(np.sort(np.concatenate(chunks)), np.arange(len(deg)))
+    for c in chunks:
+        assert np.all(np.diff(deg[c]) <= 0)
+    deg[[5, 77, 900, 4242]] = 50  # no long chain: plain round-robin
+    row_ptr = np.concatenate([[0], np.cumsum(deg)])
+    srt = np.argsort(-deg, kind="stable")
+    for c, us in enumerate(chunk_users(np.arange(len(deg)), row_ptr, 8)):
+        np.testing.assert_array_equal(us, srt[c::8])

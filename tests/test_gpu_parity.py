@@ -23,7 +23,8 @@ import pytest
 
 import oracle as orc
 from conftest import GOLDEN
-from test_oracle_golden import _oracle_test_rmse, run_oracle, run_oracle_log
+from test_oracle_golden import (_oracle_test_rmse, run_oracle, run_oracle_log,
+                                run_oracle_stalelog)
 
 pytestmark = pytest.mark.gpu
 
@@ -451,6 +452,55 @@ def test_svdpp_item_bias_beside_lane_groups_rmse(torch, u1, K, dtype):
         assert algo._engine.hx
         got = _rmse(algo.test(test))
         assert abs(got - ref) < RMSE_TOL, (opt, got, ref)
+
+
+@pytest.mark.parametrize("K,chunks", [(10, 1), (10, 3), (64, 2)])
+def test_svdpp_qlog_fp64_matches_stalelog_oracle(torch, u1, K, chunks):
+    """SVD++ with the q log (mf_svdpp_epoch_qlog: item rows read-only within a chunk, gradient
+    rows folded by mf_log_reduce / mf_log_apply with recency weights, y deferred) in fp64
+    against oracle_svdpp_sgd_stalelog with every item stale, same chunking, to 1e-9 -- K=64 is
+    the layout with the item bias beside the lane group (fp64 K * 8 = 512 B)."""
+    from surprise_amd import SVDpp
+    from surprise_amd.dist import chunk_users
+    ts, test = u1
+    row_ptr, items, ratings = ts.csr()
+    params = dict(n_factors=K, n_epochs=3, random_state=0)
+    cou = np.zeros(ts.n_users, np.int32)
+    for c, us in enumerate(chunk_users(np.arange(ts.n_users), row_ptr, chunks)):
+        cou[us] = c
+    P, f = run_oracle_stalelog(params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
+                               cou, chunks)
+    algo = SVDpp(**params, dtype="float64", chunks_per_epoch=chunks)
+    algo._engine_options = {"qlog": True}
+    algo.fit(ts)
+    assert algo._engine.qlog_pp and not algo._engine.hx
+    for k in ("pu", "qi", "yj", "bu", "bi"):
+        np.testing.assert_allclose(getattr(algo, k), f[k], rtol=0, atol=1e-9, err_msg=k)
+    ref = _oracle_test_rmse(P, f, "SVDpp", ts, list(test))[1]
+    assert abs(_rmse(algo.test(test)) - ref) < 1e-9
+
+
+def test_svdpp_qlog_fp32_k128_tracks_stalelog_oracle(torch, u1):
+    """The q log at C5's layout (fp32 K=128: one lane group, the item bias beside it) over 4
+    chunks: held-out RMSE within 1e-4 of its fp64 oracle, and within 1e-3 of the exact
+    per-user reference form."""
+    from surprise_amd import SVDpp
+    from surprise_amd.dist import chunk_users
+    ts, test = u1
+    row_ptr, items, ratings = ts.csr()
+    params = dict(n_factors=128, n_epochs=10, random_state=0)
+    cou = np.zeros(ts.n_users, np.int32)
+    for c, us in enumerate(chunk_users(np.arange(ts.n_users), row_ptr, 4)):
+        cou[us] = c
+    P, f = run_oracle_stalelog(params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
+                               cou, 4)
+    ref = _oracle_test_rmse(P, f, "SVDpp", ts, list(test))[1]
+    algo = SVDpp(**params, chunks_per_epoch=4)
+    algo._engine_options = {"qlog": True}
+    got = _rmse(algo.fit(ts).test(test))
+    assert abs(got - ref) < 1e-4, (got, ref)
+    exact = _oracle_rmse("SVDpp", params, ts, test, affine=True)
+    assert abs(got - exact) < RMSE_TOL, (got, exact)
 
 
 @pytest.mark.parametrize("K", [1, 3, 17, 64, 65, 100, 128, 200, 256, 300, 512])

@@ -96,9 +96,11 @@ def test_c5_at_8_ranks_schedule_within_1e3_of_committed_oracle(torch):
     per epoch -- 625k users (78k per rank) per chunk, the users per chunk of C5@8 at its 16
     chunks over 10M users -- q / b carried through the later ranks' steps
     (MF_MERGE_RECENCY), y composed in rank order; 20 epochs within 1e-3 of the sequential
-    reference loop's held-out RMSE (scale_golden.json c5shard; the same rule restated on the CPU
-    is c5at8_c2 there)."""
+    reference loop's held-out RMSE (scale_golden.json c5shard), and within 1e-3 of the same
+    schedule restated on the CPU (c5at8_c2_m3: oracle_svdpp_sgd_groups_merge(merge=3), final
+    0.95164 vs the sequential 0.95182; the round-3 merge rule, c5at8_c2_m2, ends at -2.1e-3)."""
     g = _golden("c5shard")
+    gm3 = _golden("c5at8_c2_m3")
     r = _bench("--shape", "c5", "--users", "1250000", "--gpus", "8", "--backend", "gloo",
                "--chunks", "2", "--rmse-epochs", "20", "--steps", "1", "--warmup", "0",
                timeout=1100)
@@ -106,6 +108,8 @@ def test_c5_at_8_ranks_schedule_within_1e3_of_committed_oracle(torch):
     assert "chunks/epoch=2" in r["config"]["workload"]
     assert r["rmse"]["reference_oracle_fp64"] == g["rmse_by_epoch"][19]
     assert abs(r["rmse"]["delta"]) < 1e-3, r["rmse"]
+    assert abs(r["rmse"]["gpu"] - gm3["rmse_by_epoch"][19]) < 1e-3, (r["rmse"], gm3["rmse_by_epoch"][19])
+    assert abs(gm3["rmse_by_epoch"][19] - g["rmse_by_epoch"][19]) < 1e-3
     ph = r["roofline"]["phases_gpu_ms"]
     assert ph["allreduce_bytes_per_chunk"] > 0 and ph["allreduce_ms_per_chunk"] > 0
 

@@ -482,3 +482,47 @@ def test_svdpp_cpu_baseline_leg_on_a_user_prefix(u1, monkeypatch):
     assert cb["value"] > 0 and cb["single_core"]["value"] > 0
     assert cb["affine_form_single_core"]["value"] > cb["single_core"]["value"]
     assert "mf.pyx:463-498" in cb["sample"]
+
+
+def run_oracle_stalelog(params, row_ptr, items, ratings, n_items, global_mean,
+                        chunk_of_user=None, n_chunks=1, stale=None, merge=3):
+    """SVD++ with the q log (the GPU's qlog option): oracle_svdpp_sgd_stalelog, every item
+    stale unless `stale` says otherwise."""
+    P = _Params("SVDpp", params)
+    rng = get_rng(P.random_state)
+    n_users = len(row_ptr) - 1
+    pu, qi, yj = orc.init_factors(rng, n_users, n_items, P.n_factors, P.init_mean,
+                                  P.init_std_dev, with_yj=True)
+    hp = orc.svd_hyper(P)
+    st = np.ones(n_items, np.int32) if stale is None else stale
+    pu, qi, yj, bu, bi = orc.svdpp_sgd_stalelog(row_ptr, items, ratings, n_items, P.n_factors,
+                                                P.n_epochs, global_mean, hp, pu, qi, yj, st,
+                                                chunk_of_user, n_chunks, merge)
+    return P, dict(pu=pu, qi=qi, yj=yj, bu=bu, bi=bi)
+
+
+@pytest.mark.parametrize("merge", [2, 3])
+def test_stalelog_svdpp_one_user_per_chunk_is_the_affine_form(u1, merge):
+    """Pins the q-log oracle (oracle_svdpp_sgd_stalelog) to the reference's per-user form: with
+    one user per chunk every stale row is read once (no repeated items) and folded with weight
+    1, so it is oracle_svdpp_sgd_affine (itself pinned to the reference arrays) bit-for-bit; and
+    with nothing stale it is the atomic schedule's deferred-y form at any chunking."""
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    params = dict(n_factors=6, n_epochs=2, random_state=0)
+    _, a = run_oracle("SVDpp", params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
+                      affine=True)
+    _, b = run_oracle_stalelog(params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
+                               np.arange(ts.n_users, dtype=np.int32), ts.n_users, merge=merge)
+    for k in a:
+        np.testing.assert_allclose(b[k], a[k], rtol=0, atol=1e-13, err_msg=k)
+    # nothing stale, one chunk: the helper-wave schedule's oracle (hotstale with no hot item)
+    P = _Params("SVDpp", params)
+    pu, qi, yj = orc.init_factors(get_rng(0), ts.n_users, ts.n_items, 6, P.init_mean,
+                                  P.init_std_dev, with_yj=True)
+    c = orc.svdpp_sgd_hotstale(row_ptr, items, ratings, ts.n_items, 6, 2, ts.global_mean,
+                               orc.svd_hyper(P), pu, qi, yj, np.zeros(ts.n_items, np.int32))
+    _, d = run_oracle_stalelog(params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
+                               stale=np.zeros(ts.n_items, np.int32), merge=merge)
+    for k, x in zip(("pu", "qi", "yj", "bu", "bi"), c):
+        np.testing.assert_array_equal(d[k], x, err_msg=k)
