@@ -163,12 +163,16 @@ int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, v
  * steps on the row to first order (oracle_svdpp_sgd_stalelog, every item stale).  Rows of
  * <= 1 KiB, no repeated items; flags: MF_EPOCH_DUP_ITEMS must be clear, XCD mask bits allowed.
  * n_waves <= 0: one wave per user up to the launch's cap.  A user's log segment must stay below
- * 1 GiB.  Replaces matrix_factorization.pyx:487 / :494-495 (the item-side updates).
+ * 1 GiB.  user_sq (nullable, fp64 [n_users]): each trained user's |p_u|^2 over the factor
+ * columns is stored there (as mf_svd_epoch_sq), so the next chunk's <p^2> is
+ * mf_user_sq_reduce's sum instead of an mf_sumsq pass over every user row.
+ * Replaces matrix_factorization.pyx:487 / :494-495 (the item-side updates).
  */
 int mf_svdpp_epoch_qlog(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
                         void *bu, int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
                         const mf_hyper_t *hp, void *qlog, const int64_t *log_row0, void *ycbuf,
-                        int32_t n_waves, int32_t flags, int32_t dtype, void *stream);
+                        double *user_sq, int32_t n_waves, int32_t flags, int32_t dtype,
+                        void *stream);
 
 /* After mf_svdpp_epoch with hot rows: row i += row n_items + i and the replica row zeroed, for
  * i in hot_items[0 .. n_hot). */

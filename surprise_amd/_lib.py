@@ -64,7 +64,8 @@ SIGNATURES = {
                        ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _vp, _vp, _i32,
                        _vp],
     "mf_svdpp_epoch_qlog": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp,
-                            _i32, ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i32, _i32, _i32, _vp],
+                            _i32, ctypes.POINTER(MfHyper), _vp, _vp, _vp, _vp, _i32, _i32, _i32,
+                            _vp],
     "mf_svdpp_hot_fold": [_vp, _i32, _i32, _vp, _i32, _i32, _vp],
     "mf_svdpp_y_fold": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32,
                         _vp],

@@ -1348,7 +1348,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *ycbuf, int K,
     Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, PPRing<T, G, H> *ring,
     int32_t *status, const uint8_t *__restrict__ hot = nullptr, T *qlog = nullptr,
-    const int64_t *__restrict__ urow = nullptr)
+    const int64_t *__restrict__ urow = nullptr, double *__restrict__ psq = nullptr)
 {
     static_assert(!(LQ && (HX || HOT)), "the q log: no helper waves, no hot replicas");
     using L = Lane8<T>;
@@ -1699,10 +1699,23 @@ __device__ __forceinline__ void epoch_body_pp_la(
         // after rating n-1: p_n, m_n (u_impl), c_n
         vec cacc[G];
         const T A = pow_int(dc, n);
+        double sq = 0;  // LQ with psq: |p_n|^2 over the factor columns (the fold's <p^2>)
 #pragma unroll
         for (int v = 0; v < G; ++v) {
-            L::template st<0>(p_rs, cu[v], Pp[v] + err_p * Dpp[v]);
+            const vec pn = Pp[v] + err_p * Dpp[v];
+            L::template st<0>(p_rs, cu[v], pn);
             cacc[v] = ((Mp[v] + err_p * Dmp[v]) - A * m0[v]) * rs_n;
+            if constexpr (LQ) {
+#pragma unroll
+                for (int e = 0; e < W; ++e) {
+                    const double x = (double)L::get(pn, e);
+                    sq += (lane + kWave * v) * W + e < K ? x * x : 0.0;
+                }
+            }
+        }
+        if (LQ && psq) {
+            sq = wave_sum(sq);
+            if (lane == 0) psq[u] = sq;
         }
         const T bu_u = lr_bu * err_p + c0_p - hp.gm;
         Buf<T>::template st<0>(b_rs, lane == 0 ? 0u : (uint32_t)sizeof(T), bu_u);
@@ -1802,7 +1815,7 @@ __global__ __launch_bounds__(kBlock) void mf_svdpp_qlog_kernel(MF_EPOCH_PARAMS,
 {
     epoch_body_pp_la<T, G, false, false, SB, 1, true>(
         row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, elog, K, hp, n_items,
-        n_waves_req, xmask, (PPRing<T, G, 1> *)nullptr, nullptr, nullptr, qlog, urow);
+        n_waves_req, xmask, (PPRing<T, G, 1> *)nullptr, nullptr, nullptr, qlog, urow, psq);
 }
 
 }  // namespace
@@ -1816,8 +1829,8 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                     int hx, double *psq, int err_col, int ck_ld, int32_t *status,
                     const uint8_t *hot, const int64_t *urow, void *stream)
 {
-    if ((psq || err_col) && (PP || M != kLog || !elog))
-        return set_err(MF_E_UNSUPPORTED, "user_sq / errors in rows: the SVD checkpoint log only");
+    if ((psq || err_col) && (PP || M != kLog || !elog) && !(psq && urow && !err_col))
+        return set_err(MF_E_UNSUPPORTED, "user_sq / errors in rows: the SVD checkpoint log or the SVD++ q log only");
     // the lookahead body (SVD, MF_MODE_LOG, rows <= 1 KiB) carries the user bias in column K + 1
     if (!PP && M == kLog && MF_LA && (int64_t)ldq * sizeof(T) <= 512 * kLaMaxG && ldq < K + 2)
         return set_err(MF_E_ARG, "MF_MODE_LOG: ldq >= n_factors + 2 (the user-bias column)");
@@ -1870,7 +1883,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
                                    (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
-                                   cast_hyper<T>(hp), csr->n_items, waves, xmask, nullptr, 0, ldq,
+                                   cast_hyper<T>(hp), csr->n_items, waves, xmask, psq, 0, ldq,
                                    urow);
                 return check_launch("mf_svdpp_qlog_kernel");
             }
@@ -2189,10 +2202,13 @@ __device__ __forceinline__ void bias_selector(int c_bias, typename Lane8<T>::vec
             L::set(bsel[v], e, (lane + kWave * v) * L::W + e == c_bias ? T(1) : T(0));
 }
 
-// One wave per piece (<= 64 rows): the piece's log-row indices arrive with ONE vector load
-// (lane l holds perm[beg + l]) and are broadcast with v_readlane, so the row gathers carry no
-// scalar-load round trips; rows are read 16 at a time in the 8-byte lane layout of the epoch
-// kernel (one dwordx2 per lane per 512 B of row).  REC: each row weighted by its recency weight.
+// One wave per TWO pieces (<= 64 rows each) at a time: each piece's log-row indices arrive with
+// ONE vector load (lane l holds perm[beg + l]) and are broadcast with v_readlane, so the row
+// gathers carry no scalar-load round trips; rows are read 8 per piece at a time (16 in flight) in
+// the 8-byte lane layout of the epoch kernel (one dwordx2 per lane per 512 B of row).  Two pieces
+// per iteration: most pieces are short (the C5 shard's chunks hold ~8 ratings per item), so a
+// piece costs its chain of dependent loads (bounds -> rows, item -> N), which the second piece's
+// overlap.  REC: each row weighted by its recency weight.
 template <typename T, int G, bool REC>
 __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
     const T *__restrict__ qlog, int ld, int n_cols, const int32_t *__restrict__ perm,
@@ -2213,52 +2229,78 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
         recency_logs(rc, l_q, l_b);
         bias_selector<T, G>(bias_col, bsel);
     }
-    for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
-        const int beg = piece_beg[pc], cnt = piece_beg[pc + 1] - beg;  // 1 <= cnt <= 64
-        const int xr = beg + (lane < cnt ? lane : cnt - 1);
-        const int myk = perm[xr];
-        T wf_l = T(1), wb_l = T(1);
-        if constexpr (REC) {
-            const int item = piece_item ? piece_item[pc] : items[readlane(myk, 0)];
-            recency_weights(rc, l_q, l_b, item, xr, wf_l, wb_l);
+    constexpr int kP = 2;   // pieces per iteration
+    constexpr int kU = 8;   // rows in flight per piece
+    for (int64_t pc0 = wave; pc0 < n_pieces; pc0 += kP * n_waves) {
+        int cnt[kP], myk[kP];
+        T wf_l[kP], wb_l[kP];
+#pragma unroll
+        for (int q = 0; q < kP; ++q) {
+            const int64_t pc = pc0 + q * n_waves;
+            const bool ok = pc < n_pieces;  // (uniform)
+            const int64_t pcc = ok ? pc : pc0;
+            const int beg = piece_beg[pcc];
+            cnt[q] = ok ? piece_beg[pcc + 1] - beg : 0;  // 1 <= cnt <= 64 for a real piece
+            const int c1 = cnt[q] > 0 ? cnt[q] : 1;
+            const int xr = beg + (lane < c1 ? lane : c1 - 1);
+            myk[q] = perm[xr];
+            wf_l[q] = T(1);
+            wb_l[q] = T(1);
+            if constexpr (REC) {
+                const int item = piece_item ? piece_item[pcc] : items[readlane(myk[q], 0)];
+                recency_weights(rc, l_q, l_b, item, xr, wf_l[q], wb_l[q]);
+            }
         }
-        vec acc[G];
+        vec acc[kP][G];
 #pragma unroll
-        for (int v = 0; v < G; ++v) acc[v] = L::splat(T(0));
-        constexpr int kU = 16;  // rows in flight
-        for (int x = 0; x < cnt; x += kU) {
-            vec g[kU][G];
+        for (int q = 0; q < kP; ++q)
 #pragma unroll
-            for (int a = 0; a < kU; ++a) {
-                const int k = readlane(myk, x + a < cnt ? x + a : cnt - 1);
-                const T *row = qlog + (int64_t)k * ld;
+            for (int v = 0; v < G; ++v) acc[q][v] = L::splat(T(0));
+        const int cmax = cnt[0] > cnt[1] ? cnt[0] : cnt[1];
+        for (int x = 0; x < cmax; x += kU) {
+            vec g[kP][kU][G];
 #pragma unroll
-                for (int v = 0; v < G; ++v) {  // (lanes past the row re-read column 0: no branch)
-                    const int c0 = (lane + kWave * v) * W;
-                    g[a][v] = *(const vec *)(row + (c0 < ld ? c0 : 0));
+            for (int q = 0; q < kP; ++q) {
+                const int cq = cnt[q] > 0 ? cnt[q] : 1;
+#pragma unroll
+                for (int a = 0; a < kU; ++a) {
+                    const int k = readlane(myk[q], x + a < cq ? x + a : cq - 1);
+                    const T *row = qlog + (int64_t)k * ld;
+#pragma unroll
+                    for (int v = 0; v < G; ++v) {  // (lanes past the row re-read column 0)
+                        const int c0 = (lane + kWave * v) * W;
+                        g[q][a][v] = *(const vec *)(row + (c0 < ld ? c0 : 0));
+                    }
                 }
             }
 #pragma unroll
-            for (int a = 0; a < kU; ++a)
-                if (x + a < cnt) {
-                    if constexpr (REC) {
-                        const int xa = x + a < kWave ? x + a : kWave - 1;
-                        const T wf = readlane(wf_l, xa), wb = readlane(wb_l, xa);
+            for (int q = 0; q < kP; ++q)
 #pragma unroll
-                        for (int v = 0; v < G; ++v)
-                            acc[v] += (L::splat(wf) + (wb - wf) * bsel[v]) * g[a][v];
-                    } else {
+                for (int a = 0; a < kU; ++a)
+                    if (x + a < cnt[q]) {
+                        if constexpr (REC) {
+                            const int xa = x + a < kWave ? x + a : kWave - 1;
+                            const T wf = readlane(wf_l[q], xa), wb = readlane(wb_l[q], xa);
 #pragma unroll
-                        for (int v = 0; v < G; ++v) acc[v] += g[a][v];
+                            for (int v = 0; v < G; ++v)
+                                acc[q][v] += (L::splat(wf) + (wb - wf) * bsel[v]) * g[q][a][v];
+                        } else {
+#pragma unroll
+                            for (int v = 0; v < G; ++v) acc[q][v] += g[q][a][v];
+                        }
                     }
-                }
         }
 #pragma unroll
-        for (int v = 0; v < G; ++v) {
-            const int c0 = (lane + kWave * v) * W;
+        for (int q = 0; q < kP; ++q) {
+            if (cnt[q] <= 0) continue;
+            const int64_t pc = pc0 + q * n_waves;
 #pragma unroll
-            for (int e = 0; e < W; ++e)
-                if (c0 + e < ld) sums[pc * ld + c0 + e] = c0 + e < n_cols ? L::get(acc[v], e) : T(0);
+            for (int v = 0; v < G; ++v) {
+                const int c0 = (lane + kWave * v) * W;
+#pragma unroll
+                for (int e = 0; e < W; ++e)
+                    if (c0 + e < ld) sums[pc * ld + c0 + e] = c0 + e < n_cols ? L::get(acc[q][v], e) : T(0);
+            }
         }
     }
 }
@@ -4155,14 +4197,15 @@ int mf_svdpp_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, v
 int mf_svdpp_epoch_qlog(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
                         void *bu, int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
                         const mf_hyper_t *hp, void *qlog, const int64_t *log_row0, void *ycbuf,
-                        int32_t n_waves, int32_t flags, int32_t dtype, void *stream)
+                        double *user_sq, int32_t n_waves, int32_t flags, int32_t dtype,
+                        void *stream)
 {
     if (!qlog || !log_row0 || !ycbuf) return set_err(MF_E_ARG, "the q log needs qlog, log_row0, ycbuf");
     if (flags & ~(MF_EPOCH_DUP_ITEMS | (0xFF << MF_EPOCH_XCD_SHIFT)))
         return set_err(MF_E_ARG, "mf_svdpp_epoch_qlog: flags MF_EPOCH_DUP_ITEMS / XCD mask only");
     return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, ycbuf,
                               n_factors, 1, hp, MF_MODE_LOG, n_waves, flags, dtype, stream,
-                              nullptr, nullptr, nullptr, log_row0);
+                              user_sq, nullptr, nullptr, log_row0);
 }
 
 int mf_svdpp_hot_fold(void *qb, int32_t ldq, int32_t n_items, const int32_t *hot_items,

@@ -662,8 +662,9 @@ class MFEngine(ItemSync, Predictor):
         # checkpoint log: the epoch kernel keeps user_sq[u] = |p_u|^2 (factor columns) current, and
         # the next chunk's <pu^2> is its fixed-order sum, taken right after this chunk's epoch
         # kernels (mf_user_sq_reduce, off the step's critical path; no mf_sumsq pass)
+        # (the SVD++ q log too: its kernel stores |p_u|^2 of the users it trains)
         self.user_sq = (torch.zeros(max(self.n_users, 1), dtype=torch.float64, device=dev)
-                        if self.ckpt else None)
+                        if self.ckpt or self.qlog_pp else None)
         self._sq_valid = self._sq_pending = False
         # several ranks, checkpoint log: the next chunk's <p^2> rode in this chunk's exchange
         # buffer (already every rank's sum: no collective of its own at the chunk start)
@@ -865,7 +866,8 @@ class MFEngine(ItemSync, Predictor):
             _lib.call("mf_svdpp_epoch_qlog", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
                       self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper), qlog,
-                      self._ptr(self.urow), self._ptr(self.ycbuf), n_waves, flags, self.dtype, st)
+                      self._ptr(self.urow), self._ptr(self.ycbuf), self._ptr(self.user_sq),
+                      n_waves, flags, self.dtype, st)
         else:
             _lib.call("mf_svdpp_epoch", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
@@ -894,7 +896,9 @@ class MFEngine(ItemSync, Predictor):
         if self.ckpt:
             self._run_chunk_ckpt(c, ev)
             return
-        if self.is_log:
+        if self.qlog_pp:  # <p^2> of the chunk start from user_sq (as the checkpoint log)
+            self._sq_prologue(st)
+        elif self.is_log:
             self.work = self._works[self._wt % 2]
             self._wt += 1
             if not self._work_cleared:  # (the last chunk was not folded through mf_log_apply)
@@ -984,25 +988,8 @@ class MFEngine(ItemSync, Predictor):
         main stream; the main stream joins the side stream at the end."""
         torch = self.torch
         st = self._st()
-        cur = self._works[self._wt % 2]
-        self._wt += 1
-        self.work = cur
-        self._work_cleared = True  # (written, never accumulated: nothing to clear)
-        launched = True  # (a kernel on the main stream after the last mf_log_apply)
-        if not self._sq_valid:
-            _lib.call("mf_user_sq", self._ptr(self.pu), self.n_users, self.K, self.ld,
-                      self._ptr(self.user_sq), self.dtype, st)
-            self._sq_reduce(cur, st)
-            self._sq_valid = True
-            self._stat_global = False  # (a local partial again: _global_stat sums it)
-        elif self._sq_pending:  # (the previous chunk was not folded by mf_log_apply)
-            self._sq_reduce(cur, st)
-            self._stat_global = False
-        else:
-            launched = False
-        launched = self._global_stat() or launched  # (several ranks: every rank's <p^2>)
+        launched = self._sq_prologue(st)
         fork_bound, self._fork_bound = self._fork_bound and not launched, False
-        self._sq_pending = True
         if "start" in ev:
             ev["start"].record(self.stream)
         lg = self.logs[c]
@@ -1054,6 +1041,30 @@ class MFEngine(ItemSync, Predictor):
                 _lib.call("mf_stream_wait_event", st, self._nev["join"])
         if "end_r" in ev:
             ev["end_r"].record(self.stream)
+
+    def _sq_prologue(self, st):
+        """The chunk-start <p^2> into work slot t % 2 from user_sq (kept current by the epoch
+        kernels): summed by the previous chunk's mf_log_apply, or here at the first chunk after
+        set_factors / after a chunk that was not folded.  True if it launched a kernel."""
+        cur = self._works[self._wt % 2]
+        self._wt += 1
+        self.work = cur
+        self._work_cleared = True  # (written, never accumulated: nothing to clear)
+        launched = True  # (a kernel on the main stream after the last mf_log_apply)
+        if not self._sq_valid:
+            _lib.call("mf_user_sq", self._ptr(self.pu), self.n_users, self.K, self.ld,
+                      self._ptr(self.user_sq), self.dtype, st)
+            self._sq_reduce(cur, st)
+            self._sq_valid = True
+            self._stat_global = False  # (a local partial again: _global_stat sums it)
+        elif self._sq_pending:  # (the previous chunk was not folded by mf_log_apply)
+            self._sq_reduce(cur, st)
+            self._stat_global = False
+        else:
+            launched = False
+        launched = self._global_stat() or launched  # (several ranks: every rank's <p^2>)
+        self._sq_pending = True
+        return launched
 
     def _ev_record(self, name, stream):
         """Record the engine's cross-stream event `name` on stream."""
@@ -1203,7 +1214,7 @@ class MFEngine(ItemSync, Predictor):
         from user_sq inside the launch (checkpoint log) or cleared for mf_sumsq."""
         if not apply:
             return None, None, 0
-        if self.ckpt:
+        if self.user_sq is not None:
             self._sq_pending = False
             return self._ptr(self._works[self._wt % 2]), self._ptr(self.user_sq), self.n_users
         return self._next_work(), None, 0
@@ -1260,7 +1271,7 @@ class MFEngine(ItemSync, Predictor):
         """Several ranks, checkpoint log: the next chunk's <p^2> is summed from user_sq by this
         chunk's first mf_log_apply (apply = 0, before the all-reduce) and rides in the exchange
         buffer's last two elements -- one collective per chunk instead of two."""
-        return self.ckpt and self.world > 1
+        return self.user_sq is not None and self.world > 1
 
     def _delta_buffer(self):
         """(flat, views): one device buffer holding [log sums (log mode)] + [one delta per
