@@ -187,11 +187,14 @@ int mf_svdpp_hot_fold(void *qb, int32_t ldq, int32_t n_items, const int32_t *hot
  * [item_piece_ptr[j], item_piece_ptr[j+1]); users in CSR order), applying them to y_j one user
  * after the other.  uA [n_users] = A_u = (1 - lr_yj reg_yj)^{|I_u|}; piece_c [n_pieces][ldu] and
  * piece_A [n_pieces] are scratch.  Race-free and deterministic (a fixed two-level tree).
+ * piece_item (nullable, [n_pieces]: each piece's item): an item with ONE piece gets its map
+ * applied by the piece's own wave (no scratch round trip, the same arithmetic), the per-item pass
+ * then composes only the items of several pieces.
  */
 int mf_svdpp_y_fold(void *yj, int32_t ldu, int32_t n_factors, const void *ycbuf, const void *uA,
                     const int32_t *item_users, const int32_t *piece_beg, int64_t n_pieces,
                     const int32_t *item_piece_ptr, int32_t n_items, void *piece_c,
-                    void *piece_A, int32_t dtype, void *stream);
+                    void *piece_A, const int32_t *piece_item, int32_t dtype, void *stream);
 
 /* stat[0] += sum of x[r][c]^2 over r < n_rows, c < n_cols, stat[1] += n_rows * n_cols (x is
  * [n_rows][ld]; stat is two device doubles; both parts add up across ranks).  <pu^2> =

@@ -67,8 +67,8 @@ SIGNATURES = {
                             _i32, ctypes.POINTER(MfHyper), _vp, _vp, _vp, _vp, _i32, _i32, _i32,
                             _vp],
     "mf_svdpp_hot_fold": [_vp, _i32, _i32, _vp, _i32, _i32, _vp],
-    "mf_svdpp_y_fold": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32,
-                        _vp],
+    "mf_svdpp_y_fold": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp,
+                        _i32, _vp],
     "mf_svd_epoch_sq": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32,
                         _i32, ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_svd_epoch_gram": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32,

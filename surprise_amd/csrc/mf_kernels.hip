@@ -3631,7 +3631,9 @@ template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void y_piece_kernel(
     int ldu, int K, const T *__restrict__ ycbuf, const T *__restrict__ uA,
     const int32_t *__restrict__ item_users, const int32_t *__restrict__ piece_beg,
-    int64_t n_pieces, T *__restrict__ pc_c, T *__restrict__ pc_A)
+    int64_t n_pieces, T *__restrict__ pc_c, T *__restrict__ pc_A,
+    const int32_t *__restrict__ piece_item, const int32_t *__restrict__ item_piece_ptr,
+    T *__restrict__ yj)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
@@ -3675,6 +3677,17 @@ __global__ __launch_bounds__(kBlock) void y_piece_kernel(
             if (x + 2 * kU < n) load(x + 2 * kU, gA, AA);
             comp(gB, AB);
         }
+        if (piece_item) {  // the item's only piece: its map applied to y_j here (y_apply skips it)
+            const int j = piece_item[pc];
+            if (item_piece_ptr[j + 1] - item_piece_ptr[j] == 1) {
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    const int c = lane + kWave * v;
+                    if (c < K) yj[(int64_t)j * ldu + c] = Aacc * yj[(int64_t)j * ldu + c] + cacc[v];
+                }
+                continue;
+            }
+        }
 #pragma unroll
         for (int v = 0; v < V; ++v) {
             const int c = lane + kWave * v;
@@ -3687,7 +3700,7 @@ __global__ __launch_bounds__(kBlock) void y_piece_kernel(
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void y_apply_kernel(
     T *__restrict__ yj, int ldu, int K, const int32_t *__restrict__ item_piece_ptr, int n_items,
-    const T *__restrict__ pc_c, const T *__restrict__ pc_A)
+    const T *__restrict__ pc_c, const T *__restrict__ pc_A, int min_pieces)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) +
@@ -3695,7 +3708,7 @@ __global__ __launch_bounds__(kBlock) void y_apply_kernel(
     const int64_t n_waves = ((int64_t)gridDim.x * kBlock) / kWave;
     for (int64_t j = wave; j < n_items; j += n_waves) {
         const int p0 = item_piece_ptr[j], p1 = item_piece_ptr[j + 1];
-        if (p0 == p1) continue;
+        if (p1 - p0 < min_pieces) continue;  // (none, or -- fused -- the one y_piece applied)
         T y[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -4363,7 +4376,7 @@ int mf_ckpt_interval(void) { return kCkpt; }
 int mf_svdpp_y_fold(void *yj, int32_t ldu, int32_t n_factors, const void *ycbuf, const void *uA,
                     const int32_t *item_users, const int32_t *piece_beg, int64_t n_pieces,
                     const int32_t *item_piece_ptr, int32_t n_items, void *piece_c,
-                    void *piece_A, int32_t dtype, void *stream)
+                    void *piece_A, const int32_t *piece_item, int32_t dtype, void *stream)
 {
     if (n_items < 0 || n_pieces < 0 || ldu < n_factors || n_factors < 0)
         return set_err(MF_E_ARG, "bad shape");
@@ -4380,11 +4393,12 @@ int mf_svdpp_y_fold(void *yj, int32_t ldu, int32_t n_factors, const void *ycbuf,
             constexpr int V = decltype(vc)::value;
             hipLaunchKernelGGL((y_piece_kernel<T, V>), dim3(gp), dim3(kBlock), 0, st, ldu,
                                n_factors, (const T *)ycbuf, (const T *)uA, item_users, piece_beg,
-                               n_pieces, (T *)piece_c, (T *)piece_A);
+                               n_pieces, (T *)piece_c, (T *)piece_A, piece_item, item_piece_ptr,
+                               (T *)yj);
             if (int rc = check_launch("y_piece_kernel")) return rc;
             hipLaunchKernelGGL((y_apply_kernel<T, V>), dim3(gi), dim3(kBlock), 0, st, (T *)yj,
                                ldu, n_factors, item_piece_ptr, n_items, (const T *)piece_c,
-                               (const T *)piece_A);
+                               (const T *)piece_A, piece_item ? 2 : 1);
             return check_launch("y_apply_kernel");
         });
     };

@@ -646,7 +646,10 @@ class MFEngine(ItemSync, Predictor):
                 perm, pb, ipp, _ = log_layout(row_ptr, items, us.cpu().numpy(), self.n_items)
                 iusr = pos_user()[perm]
                 self.ycsc.append(dict(users=to_dev(iusr), pb=to_dev(pb), ipp=to_dev(ipp),
-                                      n_pieces=len(pb) - 1))
+                                      n_pieces=len(pb) - 1,
+                                      pitem=to_dev(np.repeat(np.arange(self.n_items,
+                                                                       dtype=np.int32),
+                                                             np.diff(ipp)))))
             h = dict(hyper or {})
             decay = 1.0 - h.get("lr_yj", 0.0) * h.get("reg_yj", 0.0)
             # A_u = decay^{|I_u|} (the epoch kernel's per-user factor), fp64 on the host
@@ -942,7 +945,8 @@ class MFEngine(ItemSync, Predictor):
             _lib.call("mf_svdpp_y_fold", self._ptr(self.yj), self.ld, self.K,
                       self._ptr(self.ycbuf), self._ptr(self.uA), self._ptr(y["users"]),
                       self._ptr(y["pb"]), y["n_pieces"], self._ptr(y["ipp"]), self.n_items,
-                      self._ptr(self.ypc_c), self._ptr(self.ypc_A), self.dtype, st)
+                      self._ptr(self.ypc_c), self._ptr(self.ypc_A), self._ptr(y["pitem"]),
+                      self.dtype, st)
         if lg is not None:
             self._reduce_log(lg, self.sums.data_ptr(), st, lx)
         if hv is not None:

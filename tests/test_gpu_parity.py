@@ -769,10 +769,12 @@ def test_user_sq_statistic_equals_sumsq(torch, u1):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("K", [20, 100, 130])
-def test_svdpp_y_fold_equals_sequential_composition(torch, K):
+@pytest.mark.parametrize("fused", [False, True])
+def test_svdpp_y_fold_equals_sequential_composition(torch, K, fused):
     """mf_svdpp_y_fold (per-piece composition, then each item's pieces in order) equals applying
     y_j <- A_u y_j + c_u for the item's users one after the other (fp64), on a CSR with items
-    of 0, 1, 64, 65 and ~300 users (several pieces) and K across the lane layouts."""
+    of 0, 1, 64, 65 and ~300 users (several pieces) and K across the lane layouts; fused (with
+    piece_item): single-piece items applied by their piece's wave."""
     import ctypes
     from surprise_amd import _lib
     from surprise_amd.engine import log_layout, position_users
@@ -801,8 +803,9 @@ def test_svdpp_y_fold_equals_sequential_composition(torch, K):
     n_pc = len(pb) - 1
     sc, sa = torch.zeros(n_pc, ld, dtype=torch.float64, device=dev), torch.zeros(n_pc, dtype=torch.float64, device=dev)
     p = lambda z: ctypes.c_void_p(z.data_ptr())
+    pitem = i32(np.repeat(np.arange(n_items, dtype=np.int32), np.diff(ipp)))
     _lib.call("mf_svdpp_y_fold", p(y), ld, K, p(cb), p(Ab), p(users), p(pbd), n_pc, p(ippd),
-              n_items, p(sc), p(sa), _lib.MF_F64, None)
+              n_items, p(sc), p(sa), p(pitem) if fused else None, _lib.MF_F64, None)
     torch.cuda.synchronize()
     got = y.cpu().numpy()
     np.testing.assert_allclose(got[:, :K], want[:, :K], rtol=0, atol=1e-12)

@@ -515,3 +515,23 @@ def test_default_chunks_counts_users_per_rank():
     for users, world in ((10_000_000, 8), (1_250_000, 1), (999_999, 3)):
         c = default_chunks("svdpp", "atomic", users, world)
         assert -(-users // world) <= c * SVDPP_USERS_PER_CHUNK
+
+
+def test_default_ldq_reserves_the_user_bias_column_only_for_the_svd_log():
+    """column K+1 (the SVD log lookahead body's constant user-bias column) only where
+    that body reads it -- rows stay within 1 KiB at fp64 K=126 / fp32 K=254 for the SVD log and
+    at fp64 K=127 / fp32 K=255 elsewhere (SVD++ keeps its helper-wave launch); fp64 K=63
+    without the column keeps one lane group (64 * 8 = 512 B)."""
+    from surprise_amd import _lib
+    from surprise_amd.engine import default_ldq
+    F32, F64 = _lib.MF_F32, _lib.MF_F64
+    assert default_ldq(127, F64) * 8 == 1024 and default_ldq(255, F32) * 4 == 1024
+    assert default_ldq(126, F64, user_bias_col=True) * 8 == 1024
+    assert default_ldq(254, F32, user_bias_col=True) * 4 == 1024
+    assert default_ldq(127, F64, user_bias_col=True) * 8 > 1024  # (K + 2 columns do not fit)
+    assert default_ldq(63, F64) * 8 == 512
+    for K in (1, 10, 100, 128):
+        for dt, s in ((F32, 4), (F64, 8)):
+            for col in (False, True):
+                ldq = default_ldq(K, dt, user_bias_col=col)
+                assert ldq >= K + 1 + int(col) and (ldq * s) % 64 == 0
