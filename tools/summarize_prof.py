@@ -11,7 +11,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 tag = sys.argv[1]
 PMC_STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 11  # warmup + timed + phase steps of a --pmc run
-SETUP = ("elementwise", "rocclr", "user_sq_kernel", "fill")  # one-off setup kernels, not in a step
+# one-off setup kernels, not in a step (torch's sort / scan / reduce: the engine's duplicate-item
+# check at construction)
+SETUP = ("elementwise", "rocclr", "user_sq_kernel", "fill", "mergepath", "radix_sort",
+         "lookback", "scan_state", "onesweep")
+SETUP_EXACT = ("compute_cuda_kernel", "reduce_kernel")
 out = os.path.join(ROOT, "gpurun_out")
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
@@ -75,12 +79,14 @@ if fetch and write and bench_line:
         wb = write[k]["mean_per_dispatch"] * 1024 * d
         row = {"dispatches_per_step": d, "read_bytes": fb, "write_bytes": wb,
                "bytes_per_step": fb + wb}
-        (setup if any(x in k for x in SETUP) else per)[k] = row
+        (setup if any(x in k for x in SETUP) or k in SETUP_EXACT else per)[k] = row
     total = sum(v["bytes_per_step"] for v in per.values())
     cfg = bench_line["config"]
-    n_up = bench_line["roofline"]["updates_per_step"]
+    rl = bench_line["roofline"]
+    n_up = cfg["train_ratings_rank0"]  # one epoch per step: every training rating once
     traffic = {"bytes_per_step": total, "bytes_per_update": total / n_up,
-               "algorithmic_bytes_per_update": bench_line["roofline"]["algorithmic_bytes_per_update"],
+               "algorithmic_bytes_per_update": rl["survey_8d"]["bytes_per_update"],
+               "executed_bytes_per_update": rl["step"]["executed_bytes"] / n_up,
                "per_kernel": per, "setup_kernels_excluded": setup,
                "source": "profiles/%s_summary.json (2 x FETCH_SIZE + WRITE_SIZE, separate --pmc "
                          "passes of %d epochs, every kernel of the step)" % (tag, PMC_STEPS),
