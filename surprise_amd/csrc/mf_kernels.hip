@@ -3885,7 +3885,8 @@ int n_cus() {
     return n_cu;
 }
 
-// The dispatch layout the XCD masks assume (wave_slot): 8 XCDs, workgroup b on XCD b mod 8.
+// The dispatch layout the XCD masks assume (wave_slot): 8 XCDs, workgroup b on XCD
+// (x0 + b) mod 8 for some x0 of the launch.
 // Checked once per device with the XCC_ID register (xcc_selftest_kernel); a launch with an XCD
 // mask is refused where it does not hold (e.g. a partitioned device): its waves would otherwise
 // exit or share user slots, silently training some users twice and others never.
@@ -3901,10 +3902,22 @@ int xcd_layout_ok()
         int32_t *d = nullptr, h[kN];
         bool ok = n_cus() % 8 == 0 && hipMalloc((void **)&d, sizeof(h)) == hipSuccess;
         if (ok) {
-            hipLaunchKernelGGL(xcc_selftest_kernel, dim3(kN), dim3(kWave), 0, (hipStream_t)0, d, kN);
-            ok = hipGetLastError() == hipSuccess &&
-                 hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess;
-            for (int b = 0; ok && b < kN; ++b) ok = h[b] == b % 8;
+            // on an idle device (work of other streams drained first), twice: a layout that is
+            // not round-robin fails both times, a transient one once
+            (void)hipDeviceSynchronize();
+            bool seen = false;
+            for (int attempt = 0; attempt < 2 && !seen; ++attempt) {
+                hipLaunchKernelGGL(xcc_selftest_kernel, dim3(kN), dim3(kWave), 0,
+                                   (hipStream_t)0, d, kN);
+                bool run = hipGetLastError() == hipSuccess &&
+                           hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess;
+                // (round-robin from whichever XCD the dispatcher's pointer is at: measured
+                // starting at XCD 5 after earlier launches -- wave_slot only needs every 8
+                // consecutive workgroups on 8 distinct XCDs)
+                seen = run && h[0] >= 0 && h[0] < 8;
+                for (int b = 0; seen && b < kN; ++b) seen = h[b] == (h[0] + b) % 8;
+            }
+            ok = seen;
             (void)hipFree(d);
         }
         state[dev] = ok ? 1 : -1;

@@ -203,6 +203,18 @@ def split_heavy(users, row_ptr, heavy):
     return [users[~h], users[h]]
 
 
+def split_groups(users, row_ptr, heavy, top=0):
+    """The launch groups of a split chunk: [light, heavy] (split_heavy), or with top > 0
+    [light, top, rest]: the `top` heaviest of the heavy users (main stream) and the rest of
+    them (a third stream), each in schedule order."""
+    parts = split_heavy(users, row_ptr, heavy)
+    if top and len(parts) == 2:
+        rest_top = split_heavy(parts[1], row_ptr, top)
+        if len(rest_top) == 2:
+            return [parts[0], rest_top[1], rest_top[0]]
+    return parts
+
+
 def chain_schedule(users, row_ptr, n_chains, user_cost=16):
     """The users laid out for n_chains user chains taking entries c, c + n_chains, ... (the
     helper-wave SVD++ launch): longest-processing-time-first, each user (heaviest first) to the
@@ -372,7 +384,7 @@ class MFEngine(ItemSync, Predictor):
                  ckpt=True, heavy=None, err_in_row=True, narrow=None, events="native",
                  join="event",
                  helpers=None, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
-                 replay_rows=None, gram=None, xcd_split=None, qlog=None):
+                 replay_rows=None, gram=None, xcd_split=None, qlog=None, top=None):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -406,6 +418,10 @@ class MFEngine(ItemSync, Predictor):
                       (mf_svd_epoch_gram, where the rows carry their errors); None / False: the
                       lookahead chain (mf_svd_epoch_sq)
           xcd_split   the heavy launch on XCD 0, the rest on XCDs 1-7 (None: without gram)
+          top         split chunk: the heaviest `top` of the heavy users keep the main stream
+                      (XCD 0) and the rest of the heavy launch runs beside them on a third stream
+                      (XCD 1), so that its log replay and a first fold of the light + rest sums
+                      overlap the top chains (None: HEAVY_TOP_USERS = off; measured slower)
           qlog        SVD++: the item rows read-only within an epoch-chunk, each rating's q / b
                       gradient logged (mf_svdpp_epoch_qlog) and folded after the chunk with the
                       recency weights, y deferred -- no float atomics (oracle:
@@ -540,12 +556,19 @@ class MFEngine(ItemSync, Predictor):
         _pu = []
         pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
         self.side = torch.cuda.Stream(device=dev) if self.ckpt and heavy > 0 else None
+        # the top users of the heavy launch on the main stream, the rest of it on a third stream
+        # (its replay and the pre-fold then overlap the top chains)
+        if top is None:
+            top = self.HEAVY_TOP_USERS
+        self.top = (int(top) if self.side is not None and heavy >= 1 and int(top) > 0
+                    and int(top) < heavy and not self.gram and join == "event" else 0)
+        self.side2 = torch.cuda.Stream(device=dev) if self.top else None
         # the fork / join between the two streams as native events bound to the kernels that
         # complete them (mf_launch_event: no marker packet in the main stream's queue);
         # events="torch": torch.cuda.Event record / wait_event
         self._nev = None
         if self.side is not None and events == "native":
-            self._nev = {k: _new_event() for k in ("fork", "join")}
+            self._nev = {k: _new_event() for k in ("fork", "join", "mid")}
             weakref.finalize(self, _free_events, list(self._nev.values()))
         self._fork_bound = False  # the last mf_log_apply on the main stream completes "fork"
         # the join as an event the main stream waits for; join="kernel": inside the two replays
@@ -566,7 +589,7 @@ class MFEngine(ItemSync, Predictor):
                 self._totals_local.append(
                     item_counts(c, row_ptr, items, self.n_items).astype(np.int32))
                 continue
-            parts = split_heavy(c, row_ptr, heavy) if self.side is not None else [c]
+            parts = split_groups(c, row_ptr, heavy, self.top) if self.side is not None else [c]
             # (recency, a split chunk: each rating's position among the chunk's ratings of its
             # item, indexed by CSR position; one group: its perm is already in that order)
             kpos = None
@@ -596,6 +619,7 @@ class MFEngine(ItemSync, Predictor):
                 lgs.append(lg)
             main = lgs[0]
             main["heavy"] = lgs[1] if len(lgs) > 1 else None
+            main["mid"] = lgs[2] if len(lgs) > 2 else None  # (the heavy launch's rest, side2)
             self.sched.append(main["sched"])
             self.logs.append(main)
             self._totals_local.append(sum(lg.pop("cnt") for lg in lgs).astype(np.int32))
@@ -713,8 +737,11 @@ class MFEngine(ItemSync, Predictor):
                 self.qlog = z(max(k_hi - k_lo, 1), ldq)
                 self._qlog_base = self.qlog.data_ptr() - k_lo * ldq * esz
             # per chunk: the main group's piece sums, then the heavy group's
-            self.sums = z(max(lg["n_pieces"] + (lg["heavy"]["n_pieces"] if lg["heavy"] else 0)
+            self.sums = z(max(lg["n_pieces"] + sum(lg[g]["n_pieces"] for g in ("heavy", "mid")
+                                                   if lg.get(g))
                               for lg in self.logs), ldq)
+            # three groups: the light + rest sums pre-folded per item while the top chains run
+            self.sbuf = z(I, ldq) if any(lg.get("mid") for lg in self.logs) else None
             if self.ckpt:  # (errors in the rows: elog is never read or written)
                 self.elog = z(64 if self.err_in_row else k_hi - k_lo + 64)
                 self._elog_base = self.elog.data_ptr() - (0 if self.err_in_row else k_lo * esz)
@@ -730,7 +757,10 @@ class MFEngine(ItemSync, Predictor):
         """Ratings each epoch-kernel launch of chunk c trains, in launch order (checkpoint log,
         split chunk: the heavy users' launch, then the light users'; else one launch)."""
         if self.ckpt and self.logs[c]["heavy"] is not None:
-            return [int(self.logs[c]["heavy"]["perm"].numel()), int(self.logs[c]["perm"].numel())]
+            out = [int(self.logs[c]["heavy"]["perm"].numel()), int(self.logs[c]["perm"].numel())]
+            if self.logs[c].get("mid") is not None:
+                out.append(int(self.logs[c]["mid"]["perm"].numel()))
+            return out
         return [int(self._totals_local[c].sum())]
 
     @property
@@ -739,6 +769,10 @@ class MFEngine(ItemSync, Predictor):
         return self._err_in_row
 
     HEAVY_USERS = 128     # users in the heavy launch (measured: 64 0.231, 128 0.224, 256 0.232 ms)
+    # `top` default: off.  Measured (profiles/r4m_*, r4n_*, r4o_*): the light users' epoch +
+    # replay on the other XCDs take about as long as the top chain, so the pre-fold lands on the
+    # critical path -- 0.35 ms/epoch fp64 with top = 16 / 32 / 64 against 0.29 without
+    HEAVY_TOP_USERS = 0
     HEAVY_USERS_GRAM = 256  # ... with the blocked solve (one workgroup per user)
     HEAVY_MAX_NNZ = 8_000_000
 
@@ -1005,6 +1039,8 @@ class MFEngine(ItemSync, Predictor):
             if "end" in ev:
                 ev["end"].record(self.stream)
             self._reduce_log(lg, self.sums.data_ptr(), st)
+        elif lg.get("mid") is not None:
+            self._run_chunk_three(lg, ev, st, fork_bound)
         else:
             side = self.side
             sh = ctypes.c_void_p(side.cuda_stream)
@@ -1045,6 +1081,72 @@ class MFEngine(ItemSync, Predictor):
                 _lib.call("mf_stream_wait_event", st, self._nev["join"])
         if "end_r" in ev:
             ev["end_r"].record(self.stream)
+
+    def _run_chunk_three(self, lg, ev, st, fork_bound):
+        """A chunk split in three (top): main stream = the top heavy users' epoch (XCD 0), then
+        their replay; side2 = the rest of the heavy users' epoch and replay (XCD 1); side = the
+        light users' epoch and replay (XCDs 2-7), then -- after side2's replay -- a first fold of
+        the light + rest piece sums into sbuf (mf_log_apply, apply=0).  The main stream joins
+        the side stream before the chunk's fold, which then adds only the top users' pieces."""
+        side, side2 = self.side, self.side2
+        sh, sh2 = ctypes.c_void_p(side.cuda_stream), ctypes.c_void_p(side2.cuda_stream)
+        # XCD 0: the top chains alone; XCD 1: the rest of the heavy users (sharing XCD 0 put
+        # two chains on a SIMD: the top launch 239 -> 367 us); XCDs 2-7: the light users
+        mx = 0x02 if self.heavy_xcd else 0
+        lx = (~(self.heavy_xcd | mx) & 0xFF) if self.heavy_xcd else 0
+        hv, md = lg["heavy"], lg["mid"]
+        esz = self.sums.element_size()
+        sums_l = self.sums.data_ptr()
+        sums_h = sums_l + lg["n_pieces"] * self.ldq * esz
+        sums_m = sums_h + hv["n_pieces"] * self.ldq * esz
+        native = self._nev is not None
+        if not native:
+            self._ev_record("fork", self.stream)
+            self._ev_wait(side, "fork")
+            self._ev_wait(side2, "fork")
+        else:  # (bound to the previous chunk's mf_log_apply unless a kernel followed it)
+            if not fork_bound:
+                _lib.call("mf_event_record", self._nev["fork"], st)
+            _lib.call("mf_stream_wait_event", sh, self._nev["fork"])
+            _lib.call("mf_stream_wait_event", sh2, self._nev["fork"])
+        self._epoch_sq(hv["sched"], hv["sched"].numel(), hv["sched"].numel(), st, self.heavy_xcd)
+        if "end" in ev:
+            ev["end"].record(self.stream)
+        if "m_start" in ev:
+            ev["m_start"].record(side2)
+        self._epoch_sq(md["sched"], md["sched"].numel(), md["sched"].numel(), sh2, mx)
+        if "m_end" in ev:
+            ev["m_end"].record(side2)
+        if native:
+            _lib.call("mf_launch_event", self._nev["mid"])  # completed by the rest's replay
+        self._reduce_log(md, sums_m, sh2, lx | mx)  # (XCDs 1-7: by then the light epoch is done)
+        if not native:
+            self._ev_record("mid", side2)
+        if "l_start" in ev:
+            ev["l_start"].record(side)
+        ls = lg["sched"]
+        self._epoch_sq(ls, ls.numel(), self.n_waves, sh, lx)
+        if "l_end" in ev:
+            ev["l_end"].record(side)
+        self._reduce_log(lg, sums_l, sh, lx)
+        if native:
+            _lib.call("mf_stream_wait_event", sh, self._nev["mid"])
+            _lib.call("mf_launch_event", self._nev["join"])  # completed by the pre-fold
+        else:
+            self._ev_wait(side, "mid")
+        _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K,
+                  self._bias_col, ctypes.c_void_p(sums_l), self._ptr(lg["ipp"]),
+                  ctypes.c_void_p(sums_m), self._ptr(md["ipp"]),
+                  self._ptr(self._totals()[self._chunk]), ctypes.byref(self._hyper),
+                  self._ptr(self.work), self._log_rule(), self._ptr(self.sbuf), 0, None, None, 0,
+                  self.dtype, sh)
+        if not native:
+            self._ev_record("join", side)
+        self._reduce_log(hv, sums_h, st)  # (the top users' replay: every XCD)
+        if native:
+            _lib.call("mf_stream_wait_event", st, self._nev["join"])
+        else:
+            self._ev_wait(self.stream, "join")
 
     def _sq_prologue(self, st):
         """The chunk-start <p^2> into work slot t % 2 from user_sq (kept current by the epoch
@@ -1198,8 +1300,10 @@ class MFEngine(ItemSync, Predictor):
                                  self.sums.element_size()) if hv is not None else None)
         if apply:
             self._bind_fork()
+        three = lg.get("mid") is not None  # (the light + rest sums already folded into sbuf)
         _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K,
-                  self._bias_col, self._ptr(self.sums), self._ptr(lg["ipp"]), sums2,
+                  self._bias_col, self._ptr(self.sbuf if three else self.sums),
+                  None if three else self._ptr(lg["ipp"]), sums2,
                   self._ptr(hv["ipp"]) if hv is not None else None,
                   self._ptr(self._totals()[c]), ctypes.byref(self._hyper),
                   self._ptr(self.work), self._log_rule(),

@@ -391,21 +391,43 @@ def test_c2_ml1m_svd_k100_e20_rmse_within_1e3(torch, ml1m, mode):
 
 
 @pytest.mark.slow
-def test_headline_configuration_fp64_matches_deltalog_oracle(torch, ml1m):
+@pytest.mark.parametrize("top", [None, 16])
+def test_headline_configuration_fp64_matches_deltalog_oracle(torch, ml1m, top):
     """The bench headline's own kernel configuration at factor level: SVD K=100 in fp64 on the
     ML-1M-shape fold through the default path, which at this size splits every epoch into the
-    128 heaviest users' launch on XCD 0 beside the other users' on XCDs 1-7, each group with
-    its own checkpoint replay, both groups' piece sums folded by one mf_log_apply (the split u1
-    is too small to take).  pu, qi, bu, bi after 3 epochs equal oracle_svd_sgd_deltalog(merge=3) -- the
-    schedule restated on the CPU, pinned to the reference by the u1 goldens -- to 1e-9."""
+    128 heaviest users' launch on XCD 0 beside the other users' launch on XCDs 1-7 (top=None,
+    the default) -- or with the engine option top=16 the 16 heaviest on XCD 0 and the other
+    112 on XCD 1 on a third stream, the light + rest sums pre-folded and the top users' added by
+    the last mf_log_apply -- each group with its own checkpoint replay (the split u1 is too
+    small to take).  pu, qi, bu, bi after 3 epochs equal
+    oracle_svd_sgd_deltalog(merge=3) -- the schedule restated on the CPU, pinned to the
+    reference by the u1 goldens -- to 1e-9."""
     from surprise_amd import SVD
     ts, test = ml1m
     params = dict(n_factors=100, n_epochs=3, random_state=0)
-    algo = SVD(**params, dtype="float64").fit(ts)
+    algo = SVD(**params, dtype="float64")
+    if top is not None:
+        algo._engine_options = {"top": top}
+    algo.fit(ts)
     eng = algo._engine
     assert eng.ckpt and eng.logs[0]["heavy"] is not None, "the heavy/light split is off"
-    assert eng.logs[0]["heavy"]["sched"].numel() == eng.HEAVY_USERS
-    assert eng.heavy_xcd == 1, "the XCD-masked launches are off"
+    if top:
+        assert eng.logs[0]["heavy"]["sched"].numel() == top
+        assert eng.logs[0]["mid"]["sched"].numel() == eng.HEAVY_USERS - top
+    else:
+        assert eng.logs[0]["heavy"]["sched"].numel() == eng.HEAVY_USERS
+        assert eng.logs[0].get("mid") is None
+    from surprise_amd import _lib
+    if _lib.xcd_layout_ok():  # (the XCD masks need the 8-XCD round-robin dispatch)
+        assert eng.heavy_xcd == 1, "the XCD-masked launches are off"
+    else:  # (report what the device showed: a partitioned or non-round-robin dispatch)
+        import ctypes
+        ids = torch.zeros(64, dtype=torch.int32, device="cuda")
+        _lib.call("mf_selftest_xcc", ctypes.c_void_p(ids.data_ptr()), 64, None)
+        torch.cuda.synchronize()
+        import warnings
+        warnings.warn("XCD layout check failed; XCC_ID of blocks 0..63: %s" % ids.tolist())
+        assert eng.heavy_xcd == 0
     row_ptr, items, ratings = ts.csr()
     P, f = run_oracle_log("SVD", params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
                           merge=3)
@@ -607,13 +629,16 @@ def test_heavy_user_split_matches_single_launch(torch, u1):
 
 
 @pytest.mark.parametrize("which,chunks", [("u1", 1), ("u1", 3), ("ml1m", 1)])
+@pytest.mark.parametrize("top", [0, 16])
 def test_native_fork_and_kernel_join_equal_torch_events(torch, request, monkeypatch, which,
-                                                          chunks):
+                                                          chunks, top):
     """The split chunk's fork as a native event bound to the previous chunk's mf_log_apply
     (mf_launch_event) and its join inside the two replays (mf_launch_join: the heavy replay's
     last block waits for the light replay's) against torch.cuda.Event record / wait_event: the
     same kernels on the same data, so the fits are bit-identical -- with main-stream work (a
-    batched predict) between epochs, after which the fork must be recorded again."""
+    batched predict) between epochs, after which the fork must be recorded again.  top=16
+    (ML-1M: the heavy launch split in two on two streams, the light + rest sums pre-folded):
+    native events against torch events, both with the event join."""
     from surprise_amd.engine import MFEngine
     ts, _ = request.getfixturevalue(which)
     row_ptr, items, ratings = ts.csr()
@@ -627,12 +652,15 @@ def test_native_fork_and_kernel_join_equal_torch_events(torch, request, monkeypa
     ii = np.arange(ts.n_users, dtype=np.int32) % ts.n_items
     out = []
     for native in ("1", "0"):
+        kjoin = native == "1" and top == 0
         eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype="float32",
                        mode="log", n_chunks=chunks, heavy=heavy,
                        events="native" if native == "1" else "torch",
-                       join="kernel" if native == "1" else "event")
+                       join="kernel" if kjoin else "event", top=top)
         assert eng.logs[0]["heavy"] is not None and (eng._nev is not None) == (native == "1")
-        assert (eng._join_words is not None) == (native == "1")
+        assert (eng._join_words is not None) == kjoin
+        if top and which == "ml1m":
+            assert eng.logs[0]["mid"] is not None
         eng.set_factors(pu0, qi0)
         ests = []
         eng.run_epochs(2)

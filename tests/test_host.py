@@ -535,3 +535,24 @@ def test_default_ldq_reserves_the_user_bias_column_only_for_the_svd_log():
             for col in (False, True):
                 ldq = default_ldq(K, dt, user_bias_col=col)
                 assert ldq >= K + 1 + int(col) and (ldq * s) % 64 == 0
+
+
+def test_split_groups_light_top_rest():
+    """A split chunk's launch groups (engine `heavy`, `top`): [light, heavy], or [light, top,
+    rest] -- a partition of the chunk, schedule order kept inside each group, the top users the
+    heaviest of the heavy ones."""
+    from surprise_amd.engine import split_groups
+    rng = np.random.RandomState(3)
+    deg = rng.randint(1, 2000, size=3000)
+    row_ptr = np.concatenate([[0], np.cumsum(deg)])
+    users = np.argsort(-deg, kind="stable").astype(np.int32)  # heaviest-first, as chunks are
+    two = split_groups(users, row_ptr, 128)
+    three = split_groups(users, row_ptr, 128, top=16)
+    assert [len(p) for p in two] == [3000 - 128, 128]
+    assert [len(p) for p in three] == [3000 - 128, 16, 112]
+    np.testing.assert_array_equal(np.sort(np.concatenate(three)), np.arange(3000))
+    np.testing.assert_array_equal(np.sort(np.concatenate(three[1:])), np.sort(two[1]))
+    assert deg[three[1]].min() >= deg[three[2]].max()
+    for p in three:  # (schedule order kept: heaviest first)
+        assert np.all(np.diff(deg[p]) <= 0)
+    assert len(split_groups(users, row_ptr, 128, top=200)) == 2  # (top >= heavy: no third)
