@@ -52,6 +52,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); 6.3 TB/s achievable copy
+# no-return float atomics (global_atomic_add_f32, one dword per lane) execute at the memory side:
+# chip-wide ~1.3 TB/s of added bytes (MI355X_MICROARCH.md, "Global float atomics": 1.26-1.36)
+ATOMIC_F32_GBS = 1300.0
 PHASE_STEPS = 5  # epochs with HIP events around each phase, after the timed region
 BOX_CPU_SHARE = 16  # host cores of one GPU's share on the GPU box (os.cpu_count() shows the host)
 SHAPE_DEFAULTS = {  # shape -> (algo, n_factors, scaling)
@@ -638,6 +641,20 @@ def roofline_of(algo, K, dtype, n_train, ms_step, shape, phases=None, lay=None, 
             chain["frac"] = chain["alone_us"] / crit["avg_us"]
         out["critical_path_bound"] = "chain latency: the heaviest user's ratings are sequential"
         out["chain_latency"] = chain
+    if lay.get("hx"):
+        # the SVD++ helper-wave launch adds each rating's q row (ldq columns: factors, b_i,
+        # padding) by memory-side float atomics: its own roof is the chip's atomic rate
+        # (factor columns filling whole 512-B lane groups: the bias rides beside them, K + 1
+        # columns added; otherwise the whole padded row, ldq columns)
+        cols = lay["K"] + 1 if (lay["K"] * s) % 512 == 0 else lay["ldq"]
+        added = tot_r * cols * s
+        a_at = gbs(added, span)
+        out["atomic_roof"] = {
+            "added_bytes_per_step": added, "achieved": a_at,
+            "peak": ATOMIC_F32_GBS if s == 4 else None,
+            "frac": a_at / ATOMIC_F32_GBS if s == 4 else None,
+            "note": "float atomics' chip-wide added-byte rate (MI355X_MICROARCH.md, fp32 "
+                    "global_atomic_add_f32); fp64 adds have no guide figure (null)"}
     out["traffic_breakdown"] = tinfo.get("per_kernel") if tinfo else None
     out["traffic_source"] = tinfo.get("source") if tinfo else None
     return out
