@@ -140,7 +140,7 @@ def test_two_ranks_union_of_populations_equals_one_gpu(torch, tmp_path):
     res = _ranks(tmp_path, algo="SVD", mode="log", data="pop2", factors=100, epochs=20,
                  dtype="float32")
     ts, test = dataset("pop2")
-    a = SVD(n_factors=100, n_epochs=20, random_state=0, mode="log").fit(ts)
+    a = SVD(n_factors=100, n_epochs=20, random_state=0, mode="log", dtype="float32").fit(ts)
     rmse = accuracy.rmse(a.test(test), verbose=False)
     assert abs(float(res[0]["rmse"]) - rmse) < 2e-5, (float(res[0]["rmse"]), rmse)
     np.testing.assert_allclose(res[0]["qi"], a.qi, rtol=0, atol=2e-3)

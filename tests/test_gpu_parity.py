@@ -131,7 +131,7 @@ def test_log_mode_long_runs_track_deltalog_oracle(torch, golden, u1, name):
                           ts.global_mean, merge=3)
     ref = _oracle_test_rmse(P, f, "SVD", ts, list(test))[1]
     got64 = _rmse(SVD(**case["params"], dtype="float64").fit(ts).test(test))
-    got32 = _rmse(SVD(**case["params"]).fit(ts).test(test))
+    got32 = _rmse(SVD(**case["params"], dtype="float32").fit(ts).test(test))
     assert abs(got64 - ref) < 1e-6, (got64, ref)
     assert abs(got32 - ref) < 1e-4, (got32, ref)
 
@@ -517,9 +517,10 @@ def test_svdpp_qlog_fp32_k128_tracks_stalelog_oracle(torch, u1):
     P, f = run_oracle_stalelog(params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
                                cou, 4)
     ref = _oracle_test_rmse(P, f, "SVDpp", ts, list(test))[1]
-    algo = SVDpp(**params, chunks_per_epoch=4)
+    algo = SVDpp(**params, chunks_per_epoch=4, dtype="float32")
     algo._engine_options = {"qlog": True}
     got = _rmse(algo.fit(ts).test(test))
+    assert algo._engine.qlog_pp
     assert abs(got - ref) < 1e-4, (got, ref)
     exact = _oracle_rmse("SVDpp", params, ts, test, affine=True)
     assert abs(got - exact) < RMSE_TOL, (got, exact)
