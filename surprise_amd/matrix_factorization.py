@@ -11,9 +11,11 @@ in that order, fp64); same attributes after fit (``pu``, ``qi``, ``bu``, ``bi``
 libsurprise_amd.so and raises if the library or the GPU is missing -- there is
 no CPU fallback.  Extra, keyword-only device options:
 
-  dtype              "float64" (default: the reference's arithmetic, mf.pyx's double
-                     arrays) or "float32" (about 1.7x the fp64 rate at ML-1M, held within
-                     1e-3 of the fp64 reference's held-out RMSE by the parity tests)
+  dtype              "float64" (the reference's arithmetic, mf.pyx's double arrays) or
+                     "float32" (about 1.7x the fp64 rate at ML-1M, held within 1e-3 of the
+                     fp64 reference's held-out RMSE by the parity tests); None (default):
+                     float64 up to 256 factors (the fp64 row limit of the device kernels),
+                     float32 above it (up to 512)
   mode               item-side schedule: "log" (default; item rows read from the chunk-start
                      snapshot, per-rating item deltas logged and folded in once per
                      epoch-chunk -- race-free, bit-reproducible), "atomic" (shared rows,
@@ -50,6 +52,9 @@ class _MFBase(AlgoBase):
                         distributed):
         if mode not in ("auto",) + tuple(_lib.MODES):
             raise ValueError(f"mode must be 'auto' or one of {sorted(_lib.MODES)}, got {mode!r}")
+        if dtype is None:  # fp64 where the device rows allow it (<= 256 factors), else fp32
+            dtype = "float64" if getattr(self, "n_factors", 0) <= \
+                _lib.MAX_FACTORS[_lib.MF_F64] else "float32"
         self.dtype = dtype
         self.mode = mode
         self.chunks_per_epoch = chunks_per_epoch
@@ -309,7 +314,7 @@ class SVD(_MFBase):
     def __init__(self, n_factors=100, n_epochs=20, biased=True, init_mean=0, init_std_dev=.1,
                  lr_all=.005, reg_all=.02, lr_bu=None, lr_bi=None, lr_pu=None, lr_qi=None,
                  reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, random_state=None,
-                 verbose=False, *, dtype="float64", mode="auto",
+                 verbose=False, *, dtype=None, mode="auto",
                  chunks_per_epoch="auto", deterministic=False, n_waves=0, distributed=False):
         self.n_factors = n_factors
         self.n_epochs = n_epochs
@@ -365,7 +370,7 @@ class SVDpp(_MFBase):
     def __init__(self, n_factors=20, n_epochs=20, init_mean=0, init_std_dev=.1, lr_all=.007,
                  reg_all=.02, lr_bu=None, lr_bi=None, lr_pu=None, lr_qi=None, lr_yj=None,
                  reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, reg_yj=None,
-                 random_state=None, verbose=False, *, dtype="float64", mode="auto",
+                 random_state=None, verbose=False, *, dtype=None, mode="auto",
                  chunks_per_epoch="auto", deterministic=False, n_waves=0,
                  distributed=False):
         self.n_factors = n_factors
@@ -437,7 +442,7 @@ class NMF(_MFBase):
 
     def __init__(self, n_factors=15, n_epochs=50, biased=False, reg_pu=.06, reg_qi=.06,
                  reg_bu=.02, reg_bi=.02, lr_bu=.005, lr_bi=.005, init_low=0, init_high=1,
-                 random_state=None, verbose=False, *, dtype="float64"):
+                 random_state=None, verbose=False, *, dtype=None):
         self.n_factors = n_factors
         self.n_epochs = n_epochs
         self.biased = biased

@@ -534,7 +534,7 @@ def test_factor_counts_deterministic_fp32(torch, u1, K):
     params = dict(n_factors=K, n_epochs=2, random_state=0)
     row_ptr, items, ratings = ts.csr()
     P, f = run_oracle("SVD", params, row_ptr, items, ratings, ts.n_items, ts.global_mean)
-    algo = SVD(**params, deterministic=True).fit(ts)
+    algo = SVD(**params, deterministic=True, dtype="float32").fit(ts)
     for k in ("pu", "qi", "bu", "bi"):
         np.testing.assert_allclose(getattr(algo, k), f[k], rtol=0, atol=2e-4)
 

@@ -556,3 +556,13 @@ def test_split_groups_light_top_rest():
     for p in three:  # (schedule order kept: heaviest first)
         assert np.all(np.diff(deg[p]) <= 0)
     assert len(split_groups(users, row_ptr, 128, top=200)) == 2  # (top >= heavy: no third)
+
+
+def test_default_dtype_is_fp64_up_to_the_fp64_row_limit():
+    """The drop-in classes compute in the reference's fp64 by default; above the fp64 kernels'
+    256-factor rows they fall back to fp32 (up to 512) instead of refusing the model."""
+    from surprise_amd import NMF, SVD, SVDpp
+    assert SVD().dtype == "float64" and SVDpp().dtype == "float64" and NMF().dtype == "float64"
+    assert SVD(n_factors=256).dtype == "float64"
+    assert SVD(n_factors=300).dtype == "float32"
+    assert SVD(n_factors=10, dtype="float32").dtype == "float32"
