@@ -822,6 +822,9 @@ constexpr int kLaMaxG = MF_LA_MAX_G;
 #ifndef MF_LA_BANK_G2
 #define MF_LA_BANK_G2 8  // the same for two lane groups per row
 #endif
+#ifndef MF_LA_BANK_SB
+#define MF_LA_BANK_SB 16  // ... with the biases beside one lane group (SB: fp32 K=128)
+#endif
 #ifndef MF_LA_BANK
 #define MF_LA_BANK 8  // ratings per bank in the lookahead body (two banks alternate)
 #endif
@@ -903,7 +906,9 @@ __device__ __forceinline__ void epoch_body_la(
     using vec = typename L::vec;
     constexpr int W = L::W;
     // ratings per bank of gathered rows (a power of 2 <= 64)
-    constexpr int kB = G == 1 ? MF_LA_BANK : MF_LA_BANK_G2;
+    // (SB -- narrow checkpoint rows, the C4 layout -- gathers its rows in banks of 16: the epoch
+    // kernel at C4 19.7 -> 18.9 ms, profiles/r4q_bank_sweep.txt; banks of 4: 25.0)
+    constexpr int kB = SB ? MF_LA_BANK_SB : (G == 1 ? MF_LA_BANK : MF_LA_BANK_G2);
     static_assert(!CK || (kB % kCkpt == 0 && kB <= kWave), "checkpoints: whole banks");
     const int lane = threadIdx.x & (kWave - 1);
     int64_t wave, grid_waves;
