@@ -501,6 +501,40 @@ def test_roofline_executed_bytes_and_span_bounds():
     assert abs(rl["chain_latency"]["frac"] - 199 / 246) < 1e-12
 
 
+def test_bench_line_stays_small_and_keeps_the_contract():
+    """round 4's 21.9 KB stdout line went unparsed by the driver.  The line
+    built from a canned full result (round 4's final-tree bench dictionary, every leg present)
+    stays under bench.LINE_LIMIT (< 12 KB, the largest line a driver parsed) and keeps the
+    contract's fields, the roofline's dominant kernel per launch, cpu_baseline and rmse."""
+    import json
+    import bench
+    full = json.load(open(os.path.join(os.path.dirname(bench.__file__), "profiles",
+                                       "r4u_bench.json")))
+    assert len(json.dumps(full)) > 20000
+    line = bench.compact_line(full, "gpurun_out/bench_detail_ml-1m_n1.json")
+    text = json.dumps(line)
+    assert len(text) <= bench.LINE_LIMIT < 12000, len(text)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in line, k
+    assert abs(line["value"] / full["value"] - 1) < 1e-4
+    rl = line["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in rl, k
+    assert set(rl["dominant_kernel"]["launches"]) == {"heavy", "light"}
+    assert "frac" in rl["step"] and "frac" in rl["chain_latency"]
+    cb = line["cpu_baseline"]
+    assert {"value", "unit", "cores", "kind", "sample"} <= set(cb)
+    assert "value" in cb["single_core"] and "cython_equivalent_single_core" in cb
+    assert line["rmse"]["delta"] == full["rmse"]["delta"]  # (full precision)
+    for leg in ("f32_leg", "svdpp_c3", "c4", "predict"):
+        assert leg in line, leg
+    assert line["detail"].endswith(".json")
+    # a pathological result still keeps the headline under the limit
+    fat = dict(full, data="x" * 4000)
+    assert len(json.dumps(bench.compact_line(fat))) <= bench.LINE_LIMIT + 4000
+
+
 def test_default_chunks_counts_users_per_rank():
     """SVD++'s epoch-chunks follow the users of ONE rank (engine.SVDPP_USERS_PER_CHUNK): C5@8
     (10M users, 8 ranks) and the C5 shard on one GPU both run 16 chunks of <= 80k users per rank,
