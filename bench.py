@@ -124,6 +124,9 @@ def parse():
                         "after it; engine option qlog) instead of the float-atomic schedule")
     p.add_argument("--no-c4", action="store_true",
                    help="skip the C4 leg (BASELINE configs[3]'s shape on this GPU)")
+    p.add_argument("--long-chain", type=int, default=-1,
+                   help="epoch-chunk dealing: users of > 1/N of a chunk's ratings all in chunk 0 "
+                        "(engine option long_chain; -1: the engine's 256, 0: round-robin)")
     p.add_argument("--users", type=int, default=0,
                    help="c4 / c5: train only the first N users of the shape (a user-prefix "
                         "subsample that keeps every item; 0 = all)")
@@ -746,7 +749,8 @@ def main():
                        **({"top": args.top} if args.top >= 0 else {}),
                        **({"replay_rows": args.replay_rows} if args.replay_rows else {}),
                        **({"gram": bool(args.gram)} if args.gram >= 0 else {}),
-                       **({"xcd_split": bool(args.xcd_split)} if args.xcd_split >= 0 else {}))
+                       **({"xcd_split": bool(args.xcd_split)} if args.xcd_split >= 0 else {}),
+                       **({"long_chain": args.long_chain} if args.long_chain >= 0 else {}))
         eng.set_factors(pu, qi, yj=yj)
         eng._prepare(ctx)  # global per-item counts (all ranks)
         return eng
@@ -881,8 +885,10 @@ def main():
 
     if small and headline and args.legs and not args.no_c4:
         eng = None
-        result["c4"] = c4_leg(torch)
-        note("c4 leg done")
+        legs = c4_leg(torch)
+        result["c4"] = legs["f32"]
+        result["c4_f64"] = legs.get("f64")
+        note("c4 legs done")
 
     if rank == 0:
         detail = args.detail or os.path.join(
@@ -998,8 +1004,9 @@ def compact_line(result, detail_path=None):
         if pp.get("cpu_baseline"):
             s["cpu_baseline"] = _pick(pp["cpu_baseline"], "value", "cores", "kind")
         out["svdpp_c3"] = s
-    if result.get("c4"):
-        out["c4"] = leg(result["c4"])
+    for k in ("c4", "c4_f64"):
+        if result.get(k):
+            out[k] = leg(result[k])
     if result.get("predict"):
         p = result["predict"]
         out["predict"] = {n: {k: p[n][k]["us_per_prediction"] for k in
@@ -1012,7 +1019,7 @@ def compact_line(result, detail_path=None):
         out["rmse"] = rm  # (full precision: tests compare the committed oracle value exactly)
     text = json.dumps(out)
     if len(text) > LINE_LIMIT:  # never lose the headline: drop the legs first
-        for k in ("predict", "svdpp_c3", "f32_leg", "f64_leg", "c4"):
+        for k in ("predict", "svdpp_c3", "f32_leg", "f64_leg", "c4_f64", "c4"):
             out.pop(k, None)
             if len(json.dumps(out)) <= LINE_LIMIT:
                 break
@@ -1032,11 +1039,13 @@ ROOFLINE_NOTE = (
     "L2-resident; the HBM-bound configuration is the c4 leg")
 
 
-def c4_leg(torch, steps=5, warmup=2):
+def c4_leg(torch, steps=5, warmup=2, dtypes=("f32", "f64")):
     """BASELINE configs[3]'s shape on this one GPU (2M users x 200k items, 99M training ratings,
-    SVD K=128 fp32, the checkpoint log, one epoch per step): the HBM-bound configuration
-    (its tables exceed the caches), with its own roofline and traffic (profiles/
-    traffic_svd_k128_c4.json).  Held-out RMSE at E=20: tests/test_gpu_scale.py."""
+    SVD K=128, the checkpoint log, one epoch per step): the HBM-bound configuration (SURVEY
+    8(d): its tables exceed the caches), with its own roofline and traffic (profiles/
+    traffic_svd_k128_c4[_f64].json), in fp32 and -- the reference's arithmetic, mf.pyx:206-239 --
+    fp64 (rows of 1088 B: the narrow checkpoint rows).  Held-out RMSE at E=20:
+    tests/test_gpu_scale.py.  Returns {dtype: leg}."""
     from types import SimpleNamespace
     from surprise_amd.engine import MFEngine
     a = SimpleNamespace(shape="c4", users=0)
@@ -1046,24 +1055,30 @@ def c4_leg(torch, steps=5, warmup=2):
     gm = float(csr[2].sum()) / n_train
     K = 128
     pu, qi, _ = init_tables("c4", 0, len(csr[0]) - 1, n_items, K, False, 0)
-    eng = MFEngine(csr, n_items, K, algo="svd", hyper=hyper_for("svd", gm), mode="log",
-                   dtype="float32")
-    eng.set_factors(pu, qi)
-    eng._prepare(None)
-    prep = time.perf_counter() - t0
-    el, ph = run_steps(eng, None, steps, warmup, torch)
-    lay = layout_of(eng)
-    ms = el / steps * 1e3
-    del eng
-    torch.cuda.empty_cache()
-    rl = roofline_of("svd", K, "f32", n_train, ms, "c4", ph, lay)
-    rl["phases_gpu_ms"] = ph
-    rl["note"] = ROOFLINE_NOTE
-    return {"config": "BASELINE configs[3]'s shape on one GPU: " + desc + "; SVD K=128 f32, "
-                      "checkpoint log, one epoch per step",
-            "value": n_train * steps / el, "unit": "rating-updates/s", "steps": steps,
-            "warmup": warmup, "ms_per_step": ms, "dtype": "f32", "host_prep_s": prep,
-            "roofline": rl}
+    gen = time.perf_counter() - t0
+    out = {}
+    for dt in dtypes:
+        t1 = time.perf_counter()
+        eng = MFEngine(csr, n_items, K, algo="svd", hyper=hyper_for("svd", gm), mode="log",
+                       dtype=TORCH_DTYPE[dt])
+        eng.set_factors(pu, qi)
+        eng._prepare(None)
+        prep = time.perf_counter() - t1 + gen
+        el, ph = run_steps(eng, None, steps, warmup, torch)
+        lay = layout_of(eng)
+        ms = el / steps * 1e3
+        del eng
+        torch.cuda.empty_cache()
+        rl = roofline_of("svd", K, dt, n_train, ms, "c4", ph, lay)
+        rl["phases_gpu_ms"] = ph
+        rl["note"] = ROOFLINE_NOTE
+        out[dt] = {"config": "BASELINE configs[3]'s shape on one GPU: " + desc + "; SVD K=128 "
+                             "%s, checkpoint log, one epoch per step" % dt,
+                   "value": n_train * steps / el, "unit": "rating-updates/s", "steps": steps,
+                   "warmup": warmup, "ms_per_step": ms, "dtype": dt, "host_prep_s": prep,
+                   "roofline": rl}
+        note("c4 %s leg: %.2f ms/step" % (dt, ms))
+    return out
 
 
 def oracle_rmse(args, csr, test, n_items, K, gm, cache):
@@ -1115,7 +1130,10 @@ def scale_golden(args, E):
     path = os.path.join(ROOT, "tests", "golden", "scale_golden.json")
     if key is None or not os.path.exists(path):
         return None
-    g = json.load(open(path)).get(key)
+    data = json.load(open(path))
+    g = data.get(key)
+    if args.users and (g is None or (g["users"] or 0) != args.users):
+        g = data.get("%s_u%d" % (args.shape, args.users))  # (a user-prefix miniature)
     if g is None or (g["users"] or 0) != (args.users or 0) or E > len(g["rmse_by_epoch"]):
         return None
     return g

@@ -465,6 +465,14 @@ int mf_svdpp_user_implicit(const mf_csr_t *csr, const void *yj, int32_t ldu, voi
  * (MF_E_UNSUPPORTED) where it does not hold. */
 int mf_xcd_layout(int32_t *ok);
 
+/* The dispatch check of the XCD-masked launches: every masked launch settles each
+ * wave's (workgroup's) slot against its grid index in a device-side 64-bit sum that stays 0
+ * exactly when the launch's slots were a permutation -- every user / piece processed once.
+ * *sum = that sum over every code object of the library (synchronous; read after the device's
+ * work).  Nonzero: some masked launch since the library was loaded trained a user twice or
+ * never (the engine raises). */
+int mf_dispatch_check(uint64_t *sum);
+
 /* Self-test of the XCD id register: out[b] = HW_REG_XCC_ID of workgroup b, b < n_blocks. */
 int mf_selftest_xcc(int32_t *out, int32_t n_blocks, void *stream);
 

@@ -102,6 +102,7 @@ SIGNATURES = {
     "mf_selftest_wave_sum": [_vp, _vp, _i32, _i32, _vp],
     "mf_selftest_xcc": [_vp, _i32, _vp],
     "mf_xcd_layout": [ctypes.POINTER(ctypes.c_int32)],
+    "mf_dispatch_check": [ctypes.POINTER(ctypes.c_uint64)],
     "mf_event_create": [ctypes.POINTER(ctypes.c_void_p)],
     "mf_event_destroy": [_vp],
     "mf_event_record": [_vp, _vp],
@@ -171,6 +172,18 @@ def xcd_layout_ok() -> bool:
     ok = ctypes.c_int32(0)
     call("mf_xcd_layout", ctypes.byref(ok))
     return bool(ok.value)
+
+
+def dispatch_check() -> None:
+    """Raise unless every XCD-masked launch since the library was loaded gave each of its slots
+    to exactly one wave (mf_dispatch_check: the device-side sum stays 0).  Synchronous."""
+    s = ctypes.c_uint64(0)
+    call("mf_dispatch_check", ctypes.byref(s))
+    if s.value:
+        raise SurpriseAMDError(
+            "an XCD-masked launch did not deal its workgroups round-robin over the 8 XCDs "
+            "(mf_dispatch_check sum %#x): some users were trained twice and others never; "
+            "train with xcd_split=False" % s.value)
 
 
 def header_symbols(path: str = HEADER_PATH):

@@ -104,8 +104,10 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None, o
 # through SURPRISE_AMD_LIB, after checking their embedded hash against source_hash(extra))
 TEST_VARIANTS = {
     # the SVD++ helper-wave launch's bounded waits give up at once on request (status word bits
-    # 0x100 / 0x200): tests/test_gpu_ext.py forces MF_HX_HELPER_TIMEOUT / MF_HX_CHAIN_FALLBACK
-    "spintest": ("-DMF_HX_SPIN_TEST",),
+    # 0x100 / 0x200): tests/test_gpu_ext.py forces MF_HX_HELPER_TIMEOUT / MF_HX_CHAIN_FALLBACK;
+    # and the XCD-masked launches' slot 1 is mapped onto slot 0 (MF_DISPATCH_FAULT_TEST): the
+    # dispatch check must report it (tests/_spin_worker.py "dispatch")
+    "spintest": ("-DMF_HX_SPIN_TEST", "-DMF_DISPATCH_FAULT_TEST"),
 }
 VARIANT_DIR = os.path.join(_HERE, "variants")
 

@@ -42,6 +42,9 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
                     int hx, double *psq, int err_col, int ck_ld, int32_t *status,
                     const uint8_t *hot, const int64_t *urow, void *stream);
+// this unit's g_dispatch_sum (the dispatch check of the masked launches it holds)
+template <typename T, int M, bool PP>
+int dispatch_sum_tm(unsigned long long *out);
 }  // namespace mf_ext
 
 namespace {
@@ -206,12 +209,69 @@ __device__ __forceinline__ int xcc_id() {
     return (int)(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 0xF);
 }
 
+// ---- the dispatch check of XCD-masked launches (mf_dispatch_check)
+// A masked launch numbers its waves from blockIdx and XCC_ID (wave_slot below), assuming every
+// group of 8 consecutive workgroups lands on 8 distinct XCDs (verified once per device on an
+// idle GPU by xcd_layout_ok).  Every masked launch also proves it as it runs: a wave (workgroup,
+// mf_svd_gram_kernel) owes mix(g) for its own grid index g when g < n_slots -- blockIdx only,
+// whatever XCD it runs on -- and pays back mix(slot) for the slot it took, in ONE no-return
+// 64-bit vector atomic when it exits (SlotSettle), into one of kDispatchShards counters of this
+// code object (each on a 128-B line of its own: no single hot word).  The slots of a launch are a
+// permutation of [0, n_slots) exactly when the assumption held; then the launch leaves the
+// shards' total unchanged, while a slot taken twice or never (users trained twice / never)
+// leaves it nonzero.  The engine reads the total when it copies factors back and reports it.
+constexpr int kDispatchShards = 256;
+__device__ unsigned long long g_dispatch_sum[kDispatchShards * 16];  // (stays 0 in total)
+
+__device__ __forceinline__ unsigned long long dispatch_mix(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ull;  // splitmix64's finalizer
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+// one lane per wave (or workgroup): its debt for grid index g, its payment for slot (-1: none)
+__device__ __forceinline__ void dispatch_settle(int64_t g, int64_t slot, int64_t n_slots) {
+    unsigned long long d = g < n_slots ? 0ull - dispatch_mix((uint64_t)g) : 0ull;
+    if (slot >= 0) d += dispatch_mix((uint64_t)slot);
+    if (d) atomicAdd(&g_dispatch_sum[(g % kDispatchShards) * 16], d);
+}
+
+// A participating wave's settlement, made when it leaves its scope (every return path of the
+// kernel body): at the end, so the atomic never sits in front of the body's counted vmcnt waits.
+// (host) this code object's total over the shards; 0 on success
+int dispatch_sum_here(unsigned long long *out)
+{
+    static unsigned long long h[kDispatchShards * 16];
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dispatch_sum), sizeof(h)) != hipSuccess) return -1;
+    unsigned long long t = 0;
+    for (int i = 0; i < kDispatchShards; ++i) t += h[i * 16];
+    *out = t;
+    return 0;
+}
+
+struct SlotSettle {
+    int64_t g, slot, n;
+    bool on;
+    __device__ SlotSettle(int xmask, int64_t slot_, int64_t n_, int64_t g_)
+        : g(g_), slot(slot_), n(n_), on(xmask != 0) {}
+    __device__ ~SlotSettle() {
+        if (on) dispatch_settle(g, slot, n);
+    }
+};
+
 // The calling wave's slot among the launch's waves on the XCDs of xmask (bit x: XCD x; 0: every
 // XCD), and the number of such slots.  Blocks are dealt round-robin over the 8 XCDs
 // (MI355X_MICROARCH.md, checked by mf_selftest_xcc), so every group of 8 consecutive blocks holds
 // one block per XCD: slot = ((b / 8) * c + rank of the wave's XCD in xmask) * 4 + wave in block,
 // c = popcount(xmask).  Launches with a mask have a multiple of 8 blocks (grid_for_waves_x).
-// Returns false for a wave on an XCD outside the mask (it exits).
+// Returns false for a wave on an XCD outside the mask (it settles its debt and exits); a wave
+// that returns true settles through a SlotSettle(xmask, slot, n_slots, wave_grid_index()).
+__device__ __forceinline__ int64_t wave_grid_index() {
+    return (int64_t)blockIdx.x * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+}
 __device__ __forceinline__ bool wave_slot(int xmask, int64_t &slot, int64_t &n_slots) {
     const int64_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     if (!xmask) {
@@ -220,10 +280,17 @@ __device__ __forceinline__ bool wave_slot(int xmask, int64_t &slot, int64_t &n_s
         return true;
     }
     const int x = __builtin_amdgcn_readfirstlane(xcc_id());
-    if (!((xmask >> x) & 1)) return false;
     const int c = __builtin_popcount(xmask), rank = __builtin_popcount(xmask & ((1 << x) - 1));
-    slot = ((int64_t)(blockIdx.x >> 3) * c + rank) * (kBlock / kWave) + w;
     n_slots = (int64_t)(gridDim.x >> 3) * c * (kBlock / kWave);
+    if (!((xmask >> x) & 1)) {
+        slot = -1;
+        if ((threadIdx.x & (kWave - 1)) == 0) dispatch_settle(wave_grid_index(), -1, n_slots);
+        return false;
+    }
+    slot = ((int64_t)(blockIdx.x >> 3) * c + rank) * (kBlock / kWave) + w;
+#ifdef MF_DISPATCH_FAULT_TEST
+    if (slot == 1) slot = 0;  // (test build: slot 0 taken twice, slot 1 never -- must be reported)
+#endif
     return true;
 }
 
@@ -504,6 +571,8 @@ __device__ __forceinline__ void epoch_body(
     // branches instead of exec-masked ones.
     int64_t wave, grid_waves;
     if (!wave_slot(xmask, wave, grid_waves)) return;
+    SlotSettle settle((threadIdx.x & (kWave - 1)) == 0 ? xmask : 0, wave, grid_waves,
+                      wave_grid_index());
     const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
     if (wave >= n_waves) return;  // whole wave exits (a 1-wave launch still uses a 4-wave block)
 
@@ -913,6 +982,7 @@ __device__ __forceinline__ void epoch_body_la(
     const int lane = threadIdx.x & (kWave - 1);
     int64_t wave, grid_waves;
     if (!wave_slot(xmask, wave, grid_waves)) return;
+    SlotSettle settle(lane == 0 ? xmask : 0, wave, grid_waves, wave_grid_index());
     const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
     if (wave >= n_waves) return;
 
@@ -1370,6 +1440,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
     } else if (!wave_slot(xmask, wave, grid_waves)) {
         return;
     }
+    SlotSettle settle(!HX && lane == 0 ? xmask : 0, wave, grid_waves, wave_grid_index());
     const int64_t n_waves = n_waves_req < grid_waves ? n_waves_req : grid_waves;
     if (wave >= n_waves) return;
 
@@ -1839,10 +1910,18 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     // the lookahead body (SVD, MF_MODE_LOG, rows <= 1 KiB) carries the user bias in column K + 1
     if (!PP && M == kLog && MF_LA && (int64_t)ldq * sizeof(T) <= 512 * kLaMaxG && ldq < K + 2)
         return set_err(MF_E_ARG, "MF_MODE_LOG: ldq >= n_factors + 2 (the user-bias column)");
-    // elog: SVD: the checkpoint log (the lookahead body: kLog, up to two lane groups);
+    // the factor columns fill whole lane groups and the bias column alone would need another
+    const bool whole = ((int64_t)K * sizeof(T)) % 512 == 0 &&
+                       (int64_t)K * sizeof(T) < ((int64_t)ldq * sizeof(T) + 511) / 512 * 512;
+    // elog: SVD: the checkpoint log (the lookahead body: kLog, up to two lane groups -- of the
+    //       whole row, or with narrow rows of whole groups (the biases beside the groups, SB) of
+    //       the factor columns: fp64 K = 128, rows of 1088 B);
     //       SVD++: the deferred y buffer (kAtomic)
-    if (elog && !PP && (M != kLog || !MF_LA || (int64_t)ldq * sizeof(T) > 512 * kLaMaxG))
-        return set_err(MF_E_UNSUPPORTED, "checkpoint log: SVD, MF_MODE_LOG, ldq * size <= 1 KiB only");
+    const bool sb_rows = ck_ld < ldq && err_col <= 0 && whole &&
+                         (int64_t)K * sizeof(T) <= 512 * kLaMaxG;
+    if (elog && !PP && (M != kLog || !MF_LA || ((int64_t)ldq * sizeof(T) > 512 * kLaMaxG && !sb_rows)))
+        return set_err(MF_E_UNSUPPORTED, "checkpoint log: SVD, MF_MODE_LOG, ldq * size <= 1 KiB "
+                                         "(or narrow rows of whole lane groups) only");
     // (with the kLog snapshot the error stays stale for the whole chunk and the undamped sum of a
     // popular item's c_u diverges: measured held-out RMSE 1.82 on ML-1M)
     // ... unless the q log's chunks are small (mf_svdpp_epoch_qlog: urow given)
@@ -1854,12 +1933,10 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
         return set_err(MF_E_UNSUPPORTED, "helper waves: SVD++, MF_MODE_ATOMIC, deferred y, no repeated items");
     if (hot && !hx) return set_err(MF_E_ARG, "hot-row replicas: the helper-wave launch only");
     // the helper-wave launch with the item bias beside the lane groups (SB) where the factor
-    // columns fill whole groups and the bias column alone would need another
-    const bool whole = ((int64_t)K * sizeof(T)) % 512 == 0 &&
-                       (int64_t)K * sizeof(T) < ((int64_t)ldq * sizeof(T) + 511) / 512 * 512;
+    // columns fill whole groups
     const bool sb = hx && !hot && whole;
     // ... and the SVD checkpoint epoch with narrow rows (the rows hold the factor columns only)
-    const bool sbk = !PP && M == kLog && elog && ck_ld < ldq && err_col <= 0 && whole;
+    const bool sbk = !PP && M == kLog && elog && sb_rows;
     return dispatch_g<T>(sb || sbk || (urow && whole) ? K : ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         if constexpr (PP && M == kAtomic && V <= kLaMaxG) {
@@ -1925,6 +2002,12 @@ template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
     void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, int, double *,
     int, int, int32_t *, const uint8_t *, const int64_t *, void *);
+template <typename T, int M, bool PP>
+int dispatch_sum_tm(unsigned long long *out)
+{
+    return dispatch_sum_here(out);
+}
+template int dispatch_sum_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(unsigned long long *);
 }  // namespace mf_ext
 #else  // the main translation unit
 
@@ -2379,6 +2462,9 @@ __device__ __forceinline__ void log_replay_body(
     // narrow rows (MF_EPOCH_CKPT_NARROW): the K factor columns only; the bias column's gradient
     // err_k * 1 is summed from the per-lane errors
     const bool narrow = ldc < ldq;
+    // lane groups the checkpoint rows fill (G = kLaMaxG + 1 only with narrow rows of kLaMaxG
+    // groups -- fp64 K = 128 -- whose last group holds the bias column alone)
+    constexpr int GR = G > kLaMaxG ? kLaMaxG : G;
     for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
         // a piece: >= 1 ratings of ONE item, taken 64 at a time (lane x: rating x of the
         // sub-piece); the undone step's and the bias column's scalar sums accumulate per lane
@@ -2426,7 +2512,7 @@ __device__ __forceinline__ void log_replay_body(
                     const int x = x0 + y < kWave ? x0 + y : kWave - 1;
                     const T *row = ckpt + (int64_t)readlane(c_l, x) * ldc;
 #pragma unroll
-                    for (int v = 0; v < G; ++v) p[y][v] = *(const vec *)(row + cc[v]);
+                    for (int v = 0; v < GR; ++v) p[y][v] = *(const vec *)(row + cc[v]);
                 }
             };
             auto comp_grp = [&](const int x0, vec (&p)[kU][G]) {
@@ -2435,7 +2521,7 @@ __device__ __forceinline__ void log_replay_body(
                     const int x = x0 + y < kWave ? x0 + y : kWave - 1;
                     const T wo = readlane(eo_l, x), we = readlane(ee_l, x);
 #pragma unroll
-                    for (int v = 0; v < G; ++v) {
+                    for (int v = 0; v < GR; ++v) {
                         ao[v] += wo * p[y][v];
                         ae[v] += we * p[y][v];
                     }
@@ -2536,10 +2622,13 @@ __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     uint32_t join_epoch, Recency rc, int ldc)
 {
     int64_t wave, n_waves;
-    if (wave_slot(xmask, wave, n_waves))
+    if (wave_slot(xmask, wave, n_waves)) {
+        SlotSettle settle((threadIdx.x & (kWave - 1)) == 0 ? xmask : 0, wave, n_waves,
+                          wave_grid_index());
         log_replay_body<T, G, REC>(ckpt, elog, ldq, K, items, qb, n_items, lr_pu, inv_ap, perm,
                                    ck_pos, piece_beg, n_pieces, sums, err_col, piece_item, wave,
                                    n_waves, join && join_role == 1, rc, ldc);
+    }
     if (join) join_arrive(join, join_role, join_epoch);
 }
 
@@ -2743,11 +2832,17 @@ __global__ __launch_bounds__(kBlock) void mf_svd_gram_kernel(
     int64_t slot = blockIdx.x, n_slots = gridDim.x;
     if (xmask) {  // this block's slot among the launch's blocks on the XCDs of xmask
         const int x = __builtin_amdgcn_readfirstlane(xcc_id());
-        if (!((xmask >> x) & 1)) return;
+        const bool in = (xmask >> x) & 1;
         const int c = __builtin_popcount(xmask), rank = __builtin_popcount(xmask & ((1 << x) - 1));
-        slot = (int64_t)(blockIdx.x >> 3) * c + rank;
+        slot = in ? (int64_t)(blockIdx.x >> 3) * c + rank : -1;
         n_slots = (int64_t)(gridDim.x >> 3) * c;
+        if (!in) {
+            if (tid == 0) dispatch_settle(blockIdx.x, -1, n_slots);  // (the dispatch check)
+            return;
+        }
     }
+    // (the block's settlement, by thread 0 when the block ends)
+    SlotSettle settle(tid == 0 ? xmask : 0, slot, n_slots, blockIdx.x);
     const T lr_bu = biased ? hp.lr_bu : T(0);
     const T a = T(1) - hp.lr_pu * hp.reg_pu, abu = T(1) - lr_bu * hp.reg_bu;
     const T kb = hp.gm * (T(1) - abu);
@@ -4095,7 +4190,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 931; }
+int mf_version(void) { return 932; }
 
 #ifndef MF_SOURCE_HASH
 #define MF_SOURCE_HASH "unknown"
@@ -4359,8 +4454,12 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
     if ((flags & MF_EPOCH_CKPT_NARROW) && (err_col || n_factors < 1))
         return set_err(MF_E_ARG, "MF_EPOCH_CKPT_NARROW: errors in elog, n_factors >= 1");
     const int ldc = (flags & MF_EPOCH_CKPT_NARROW) ? ckpt_narrow_ld(n_factors, dtype) : ldq;
-    const int64_t rb = (int64_t)ldq * (dtype == MF_F64 ? 8 : 4);
-    if (rb > 512 * kLaMaxG) return set_err(MF_E_UNSUPPORTED, "checkpoint log: ldq * size <= 1 KiB only");
+    const int64_t esz = dtype == MF_F64 ? 8 : 4;
+    // rows of <= 1 KiB; narrow rows: their factor columns in <= 1 KiB, the item row / sums in one
+    // more lane group at most (fp64 K = 128: ldc 128, ldq 136)
+    if ((int64_t)ldc * esz > 512 * kLaMaxG || (ldc == ldq && (int64_t)ldq * esz > 512 * kLaMaxG) ||
+        (int64_t)ldq * esz > 512 * (kLaMaxG + 1))
+        return set_err(MF_E_UNSUPPORTED, "checkpoint log: ldq * size <= 1 KiB (narrow rows: ldc) only");
     Recency rc;
     if (int e = make_recency(rec, hp, rc)) return e;
     const int64_t cap = (int64_t)n_cus() * MF_REPLAY_WPC * (xmask ? __builtin_popcount(xmask) : 8) / 8;
@@ -4370,9 +4469,10 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
         using T = decltype(tag_t);
         return dispatch_g<T>(ldq, [&](auto gc) -> int {
             constexpr int V = decltype(gc)::value;
-            if constexpr (V > kLaMaxG) {
+            if constexpr (V > kLaMaxG + 1) {
                 return set_err(MF_E_UNSUPPORTED, "checkpoint log: row too long");
             } else {
+                // (V = kLaMaxG + 1 only for narrow rows: their groups stop at kLaMaxG)
                 auto kern = rec ? log_replay_kernel<T, V, true> : log_replay_kernel<T, V, false>;
                 launch_ev(stop.take(), kern, dim3(g), dim3(kBlock), st,
                                    (const T *)qlog, (const T *)elog, ldq, n_factors, csr->items,
@@ -4795,6 +4895,30 @@ int mf_xcd_layout(int32_t *ok)
 {
     if (!ok) return set_err(MF_E_ARG, "null argument");
     *ok = xcd_layout_ok();
+    return 0;
+}
+
+int mf_dispatch_check(uint64_t *sum)
+{
+    if (!sum) return set_err(MF_E_ARG, "null sum");
+    // every code object's g_dispatch_sum: the main unit's (log replay, blocked solve) and each
+    // epoch unit's; synchronous, after the device's work (hipMemcpyFromSymbol)
+    unsigned long long total = 0, x = 0;
+    int bad = dispatch_sum_here(&x);
+    total += x;
+    auto add = [&](auto tag_t) {
+        using T = decltype(tag_t);
+        bad |= mf_ext::dispatch_sum_tm<T, kPlain, false>(&x); total += x;
+        bad |= mf_ext::dispatch_sum_tm<T, kPlain, true>(&x); total += x;
+        bad |= mf_ext::dispatch_sum_tm<T, kAtomic, false>(&x); total += x;
+        bad |= mf_ext::dispatch_sum_tm<T, kAtomic, true>(&x); total += x;
+        bad |= mf_ext::dispatch_sum_tm<T, kLog, false>(&x); total += x;
+        bad |= mf_ext::dispatch_sum_tm<T, kLog, true>(&x); total += x;
+    };
+    add(float{});
+    add(double{});
+    if (bad) return set_err((int)hipErrorInvalidSymbol, "mf_dispatch_check: hipMemcpyFromSymbol failed");
+    *sum = total;
     return 0;
 }
 

@@ -64,13 +64,14 @@ def chunk_users(users, row_ptr, n_chunks: int, long_chain: int = 256):
     a chunk -- more than 1 / long_chain of a chunk's ratings -- all go to chunk 0, where their
     chains run side by side instead of one per chunk, when there are at most n_chunks of them
     (else the dealing is unchanged): the full C5's 9 users of 200k-600k ratings take ~112 ms of
-    sequential chain each against ~5 ms for a chunk's other 7.9M ratings."""
+    sequential chain each against ~5 ms for a chunk's other 7.9M ratings.
+    long_chain = 0: plain round-robin dealing."""
     users = np.asarray(users, dtype=np.int64)
     deg = np.diff(np.asarray(row_ptr, dtype=np.int64))[users]
     order = np.argsort(-deg, kind="stable")
     srt = users[order]
     n_long = 0
-    if n_chunks > 1 and len(users):
+    if n_chunks > 1 and len(users) and long_chain > 0:
         thr = deg.sum() / n_chunks / max(1, long_chain)
         n_long = int((deg[order] > thr).sum())
     if n_long <= 1 or n_long > n_chunks:
@@ -114,6 +115,11 @@ def csr_fingerprint(csr, n_items: int):
     crc = zlib.crc32(np.ascontiguousarray(items, np.int32).tobytes(), crc)
     crc = zlib.crc32(np.ascontiguousarray(ratings, np.float64).tobytes(), crc)
     return np.array([len(row_ptr) - 1, n_items, int(row_ptr[-1]), crc], np.int64)
+
+
+class _Done:
+    def wait(self):
+        return True
 
 
 class DistContext:
@@ -164,6 +170,16 @@ class DistContext:
     def all_reduce_sum(self, tensor):
         self._run(lambda t: self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group),
                   tensor)
+
+    def all_reduce_sum_async(self, tensor):
+        """SUM all-reduce enqueued behind the current stream's work; returns a handle whose
+        wait() makes the current stream wait for it (RCCL: its own stream runs the collective
+        meanwhile).  Host-staged (gloo): done at once, wait() is a no-op."""
+        if self.host_staged and tensor.is_cuda:
+            self.all_reduce_sum(tensor)
+            return _Done()
+        return self.dist.all_reduce(tensor, op=self.dist.ReduceOp.SUM, group=self.group,
+                                    async_op=True)
 
     def all_reduce_max(self, tensor):
         self._run(lambda t: self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group),

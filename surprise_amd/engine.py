@@ -384,7 +384,8 @@ class MFEngine(ItemSync, Predictor):
                  ckpt=True, heavy=None, err_in_row=True, narrow=None, events="native",
                  join="event",
                  helpers=None, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
-                 replay_rows=None, gram=None, xcd_split=None, qlog=None, top=None):
+                 replay_rows=None, gram=None, xcd_split=None, qlog=None, top=None,
+                 exchange=None, long_chain=256, overlap_q=True):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -425,7 +426,16 @@ class MFEngine(ItemSync, Predictor):
           qlog        SVD++: the item rows read-only within an epoch-chunk, each rating's q / b
                       gradient logged (mf_svdpp_epoch_qlog) and folded after the chunk with the
                       recency weights, y deferred -- no float atomics (oracle:
-                      oracle_svdpp_sgd_stalelog); None / False: the atomic schedule"""
+                      oracle_svdpp_sgd_stalelog); None / False: the atomic schedule
+          long_chain  epoch-chunk dealing (dist.chunk_users): users of more than 1 / long_chain
+                      of a chunk's ratings all go to chunk 0 (when at most n_chunks of them);
+                      0: plain round-robin dealing (the dealing before round 4)
+          overlap_q   SVD++ atomic schedule on several ranks over RCCL: q's part of the
+                      exchange all-reduced (async) while the y fold runs (False: one buffer)
+          exchange    None: the multi-rank exchange (snapshots, the packed all-reduce buffer,
+                      the <p^2> ride) when world > 1; True: also at world 1 with a context --
+                      TEST ONLY: the device-resident exchange path under RCCL on one GPU
+                      (tests/_rccl_worker.py), which must equal the local fold"""
         torch = _lib.require_gpu()
         self.torch = torch
         self.algo = algo
@@ -478,6 +488,9 @@ class MFEngine(ItemSync, Predictor):
             props = torch.cuda.get_device_properties(torch.cuda.current_device())
             self.n_waves = SVDPP_WAVES_PER_CU * props.multi_processor_count
         self.world = int(world)
+        self.multi = self.world > 1 or bool(exchange)  # (the exchange path's tables and rules)
+        self.overlap_q = bool(overlap_q)
+        self._q_work = None
         if merge not in ("count", "recency", "sum"):
             raise ValueError("merge must be 'count', 'recency' or 'sum', got %r" % (merge,))
         self.merge_rule = merge
@@ -500,7 +513,7 @@ class MFEngine(ItemSync, Predictor):
             order = np.asarray(user_order if user_order is not None else self.users, np.int32)
             chunks = [order]
         else:
-            chunks = chunk_users(self.users, row_ptr, self.n_chunks)
+            chunks = chunk_users(self.users, row_ptr, self.n_chunks, long_chain=int(long_chain))
         to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
         self._row_ptr_h, self._items_h = row_ptr, np.asarray(items, np.int32)
         self._chunk_users = [np.asarray(c, np.int32) for c in chunks]
@@ -511,8 +524,11 @@ class MFEngine(ItemSync, Predictor):
         # from 0, else the gradient log)
         h = dict(hyper or {})
         ap = 1.0 - h.get("lr_pu", 0.0) * h.get("reg_pu", 0.0)
+        # (rows of more than 1 KiB: only in narrow form of whole lane groups -- the factor columns
+        # alone fill one or two 512-B groups, the biases ride beside them: fp64 K = 128)
+        whole_rows = (self.K * esz) % 512 == 0 and self.K * esz <= 1024 and narrow is not False
         self.ckpt = (self.mode == _lib.MF_MODE_LOG and bool(ckpt) and algo == "svd"
-                     and esz_q <= 1024 and abs(ap) >= 0.5)
+                     and (esz_q <= 1024 or whole_rows) and abs(ap) >= 0.5)
         # checkpoint log with MF_EPOCH_ERR_IN_ROW where the row has room: each pair's two errors
         # ride in its checkpoint row's padding (the replay gathers no elog entries)
         e0 = ((self.K + 3) & ~1) if self.dtype == _lib.MF_F32 else self.K + 2
@@ -521,7 +537,7 @@ class MFEngine(ItemSync, Predictor):
         # read), so a 4-byte error gather per rating costs less than the rows' extra line
         lc = _lib.ckpt_narrow_ld(self.K, self.dtype)
         if narrow is None:
-            narrow = lc * esz % 128 == 0
+            narrow = lc * esz % 128 == 0 or esz_q > 1024
         self.narrow = self.ckpt and bool(narrow) and 0 < lc < self.ldq
         self.ldc = lc if self.narrow else self.ldq  # the checkpoint rows' stride
         # (read-only after construction: elog is sized for it)
@@ -745,9 +761,9 @@ class MFEngine(ItemSync, Predictor):
             if self.ckpt:  # (errors in the rows: elog is never read or written)
                 self.elog = z(64 if self.err_in_row else k_hi - k_lo + 64)
                 self._elog_base = self.elog.data_ptr() - (0 if self.err_in_row else k_lo * esz)
-        snap_q = self.world > 1 and self.mode != _lib.MF_MODE_LOG
+        snap_q = self.multi and self.mode != _lib.MF_MODE_LOG
         self.qb_s = z(I, ldq) if snap_q else None
-        self.yj_s = z(I, ld) if (self.world > 1 and self.yj is not None) else None
+        self.yj_s = z(I, ld) if (self.multi and self.yj is not None) else None
         self._delta = None
         self._hyper = _lib.MfHyper(**(hyper or {}))
         if not self.biased:
@@ -849,9 +865,10 @@ class MFEngine(ItemSync, Predictor):
             seen = None
         if seen is None and not block:
             host = t.empty(1, dtype=t.int32, pin_memory=True)
-            host.copy_(self._hx_status, non_blocking=True)
-            ev = t.cuda.Event()
-            ev.record(self.stream)
+            with t.cuda.stream(self.stream):  # (the copy and its event on the engine's stream)
+                host.copy_(self._hx_status, non_blocking=True)
+                ev = t.cuda.Event()
+                ev.record(self.stream)
             self._hx_seen = (host, ev)
 
     def get_factors(self, ctx=None):
@@ -862,6 +879,8 @@ class MFEngine(ItemSync, Predictor):
         if getattr(self, "_join_words", None) is not None and int(self._join_words[608]) != 0:
             raise _lib.SurpriseAMDError("the in-kernel join of the two replays timed out: the "
                                         "item folds since are invalid")
+        if getattr(self, "heavy_xcd", 0):  # (the XCD-masked launches' slot check)
+            _lib.dispatch_check()
         if getattr(self, "_hx_status", None) is not None and \
                 int(self._hx_status[0]) & _lib.MF_HX_HELPER_TIMEOUT:
             raise _lib.SurpriseAMDError("an SVD++ helper wave timed out waiting for q deltas and "
@@ -974,6 +993,8 @@ class MFEngine(ItemSync, Predictor):
             self._epoch(s, s.numel(), self.n_waves, 0, st, lx)
         if "end" in ev:
             ev["end"].record(self.stream)
+        if self._q_early():  # (several ranks: q's part of the exchange overlaps the y fold)
+            self._exchange_q_begin()
         if self.ydefer:
             y = self.ycsc[c]
             _lib.call("mf_svdpp_y_fold", self._ptr(self.yj), self.ld, self.K,
@@ -1216,7 +1237,7 @@ class MFEngine(ItemSync, Predictor):
         the chunk's replay / reduce reads it (the recency weights) -- one 2-double all-reduce on
         the main stream; True if it launched one."""
         ctx = self._ctx
-        if ctx is None or ctx.world == 1 or not self.is_log:
+        if not self._exchanging(ctx) or not self.is_log:
             return False
         if self._stat_global:  # (summed by the previous chunk's exchange)
             self._stat_global = False
@@ -1234,7 +1255,7 @@ class MFEngine(ItemSync, Predictor):
         snap_rec = not self.is_log and self.merge_rule == "recency"
         for t in self._totals_local:
             tt = self.torch.from_numpy(t).to(self.dev)
-            if ctx is not None and ctx.world > 1:
+            if self._exchanging(ctx):
                 if self.recency or snap_rec:
                     # this rank's ratings of an item follow the earlier ranks' and precede the
                     # later ranks'
@@ -1248,7 +1269,7 @@ class MFEngine(ItemSync, Predictor):
                 ctx.all_reduce_sum(tt)
             self.totals.append(tt)
         self._yaff = []
-        if self.yj_s is not None and ctx is not None and ctx.world > 1:
+        if self.yj_s is not None and self._exchanging(ctx):
             from .dist import item_log_decay
             torch = self.torch
             h = self._hyper
@@ -1356,10 +1377,23 @@ class MFEngine(ItemSync, Predictor):
         second, 16-byte collective).
         self._sync_events (dict of "ar_begin" / "ar_end" torch events, set by bench.py's
         instrumented epochs) brackets the collective on the engine's stream."""
-        if ctx is None or ctx.world == 1:
+        if not self._exchanging(ctx):
             self._merge_local()
             return
         flat, bufs = self._delta_buffer()
+        if self._q_work is not None:  # q's part went out after the epoch kernel: y's part now
+            ev = getattr(self, "_sync_events", None)
+            if ev:  # (the exchange's time left on the critical path, after the y fold)
+                ev["ar_begin"].record(self.stream)
+            self._delta_into(bufs, which=(1,))
+            ctx.all_reduce_sum(bufs[1])
+            with self.torch.cuda.stream(self.stream):
+                self._q_work.wait()
+            self._q_work = None
+            if ev:
+                ev["ar_end"].record(self.stream)
+            self._apply(bufs)
+            return
         self._delta_into(bufs)
         ride = self._stat_rides()
         if ride:  # the next chunk's <p^2> partial (summed by _delta_into) rides in the buffer
@@ -1379,7 +1413,28 @@ class MFEngine(ItemSync, Predictor):
         """Several ranks, checkpoint log: the next chunk's <p^2> is summed from user_sq by this
         chunk's first mf_log_apply (apply = 0, before the all-reduce) and rides in the exchange
         buffer's last two elements -- one collective per chunk instead of two."""
-        return self.user_sq is not None and self.world > 1
+        return self.user_sq is not None and self.multi
+
+    def _q_early(self):
+        """SVD++'s atomic schedule on several ranks over a device transport (RCCL): q's snapshot
+        delta is ready when the epoch kernel ends, so its all-reduce (async, RCCL's own stream)
+        runs while mf_svdpp_y_fold runs; y's part follows in sync_items.  The same arithmetic
+        as the one-buffer exchange (two collectives instead of one); host-staged gloo keeps
+        the single buffer."""
+        ctx = self._ctx
+        return (self.overlap_q and self._exchanging(ctx) and not ctx.host_staged
+                and self.qb_s is not None and self.yj_s is not None and self.ydefer)
+
+    def _exchange_q_begin(self):
+        flat, bufs = self._delta_buffer()
+        self._delta_into(bufs, which=(0,))
+        with self.torch.cuda.stream(self.stream):
+            self._q_work = self._ctx.all_reduce_sum_async(bufs[0])
+
+    def _exchanging(self, ctx):
+        """The chunk's item-side updates go through the packed all-reduce (several ranks, or
+        the test-only `exchange=True` at world 1) rather than the local fold."""
+        return ctx is not None and (ctx.world > 1 or self.multi)
 
     def _delta_buffer(self):
         """(flat, views): one device buffer holding [log sums (log mode)] + [one delta per
@@ -1396,14 +1451,19 @@ class MFEngine(ItemSync, Predictor):
             self._delta = (flat, views)
         return self._delta
 
-    def _delta_into(self, bufs):
+    def _delta_into(self, bufs, which=None):
+        """Fill the exchange buffer's parts (which: the indices of the snapshot tables to fill,
+        None = every part)."""
         c = getattr(self, "_chunk", 0)
         st = self._st()
         x = 0
         if self.is_log:  # (self.work already holds every rank's <p^2>: _global_stat)
             self._log_fold(bufs[0], False, stat=self._stat_rides())
             x = 1
-        for tab, snap, ld, bias_col, rule in self._snap_tables():
+        for ti, (tab, snap, ld, bias_col, rule) in enumerate(self._snap_tables()):
+            if which is not None and ti not in which:
+                x += 1
+                continue
             if rule == "affine":
                 ya = self._yaff[c]
                 _lib.call("mf_item_affine", self._ptr(tab), self._ptr(snap), self.n_items, ld,

@@ -52,10 +52,8 @@ class _MFBase(AlgoBase):
                         distributed):
         if mode not in ("auto",) + tuple(_lib.MODES):
             raise ValueError(f"mode must be 'auto' or one of {sorted(_lib.MODES)}, got {mode!r}")
-        if dtype is None:  # fp64 where the device rows allow it (<= 256 factors), else fp32
-            dtype = "float64" if getattr(self, "n_factors", 0) <= \
-                _lib.MAX_FACTORS[_lib.MF_F64] else "float32"
-        self.dtype = dtype
+        self._dtype_auto = dtype is None
+        self.dtype = dtype if dtype is not None else self._auto_dtype()
         self.mode = mode
         self.chunks_per_epoch = chunks_per_epoch
         self.deterministic = deterministic
@@ -63,6 +61,15 @@ class _MFBase(AlgoBase):
         self.distributed = distributed
         self._engine = None
         self._imp = None
+
+    def _auto_dtype(self):
+        """dtype=None: fp64 where the device rows allow it (<= 256 factors), else fp32.  Resolved
+        again at fit time, so a model whose n_factors changed after construction follows it.
+        (fp64 rows of more than 126 factors (SVD; 127 SVD++) exceed 1 KiB: those models train on
+        the slower paths -- the gradient log instead of the checkpoint log, SVD++ without the
+        helper-wave launch -- DESIGN.md 2.)"""
+        return "float64" if getattr(self, "n_factors", 0) <= _lib.MAX_FACTORS[_lib.MF_F64] \
+            else "float32"
 
     def __getstate__(self):
         state = self.__dict__.copy()
@@ -129,6 +136,8 @@ class _MFBase(AlgoBase):
         from .dist import DistContext, csr_fingerprint, local_csr, shard_users
 
         _lib.require_gpu()
+        if getattr(self, "_dtype_auto", False):
+            self.dtype = self._auto_dtype()
         if isinstance(trainset, Trainset):
             csr = trainset.csr()
             user_order = trainset.sched_order()
@@ -471,6 +480,8 @@ class NMF(_MFBase):
         from .engine import NMFEngine
 
         _lib.require_gpu()
+        if getattr(self, "_dtype_auto", False):
+            self.dtype = self._auto_dtype()
         ts = _as_trainset(trainset)
         rng = get_rng(self.random_state)
         n_users, n_items, K = trainset.n_users, trainset.n_items, self.n_factors

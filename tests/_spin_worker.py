@@ -13,8 +13,32 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def dispatch_case(out):
+    """The test build maps the XCD-masked launches' slot 1 onto slot 0 (MF_DISPATCH_FAULT_TEST):
+    an SVD fit with the heavy users' launch on XCD 0 (heavy=16, xcd_split) trains one heavy user
+    twice and another never; get_factors must raise (mf_dispatch_check)."""
+    from surprise_amd import SVD, _lib
+    from surprise_amd.synthetic import shape
+    from surprise_amd.trainset import Trainset
+    u, i, r = shape("ml-100k")
+    ts = Trainset.from_inner_arrays(u, i, r, n_users=int(u.max()) + 1, n_items=int(i.max()) + 1)
+    res = {"case": "dispatch", "layout": _lib.xcd_layout_ok()}
+    algo = SVD(n_factors=20, n_epochs=2, random_state=0)
+    algo._engine_options = {"heavy": 16, "xcd_split": True}
+    try:
+        algo.fit(ts)
+        res["raised"] = None
+    except _lib.SurpriseAMDError as e:
+        res["raised"] = str(e)
+    res["heavy_xcd"] = int(getattr(algo._engine, "heavy_xcd", -1)) if algo._engine else None
+    with open(out, "w") as f:
+        json.dump(res, f)
+
+
 def main():
     case, out = sys.argv[1], sys.argv[2]
+    if case == "dispatch":
+        return dispatch_case(out)
     from surprise_amd import Dataset, Reader, SVDpp, _lib, accuracy, engine
     from surprise_amd.model_selection import PredefinedKFold
     assert _lib.LIB_PATH == os.environ["SURPRISE_AMD_LIB"]

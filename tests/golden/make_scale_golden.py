@@ -6,6 +6,8 @@ on the GPU box).
             SVD K=128, the reference loop restated (oracle_svd_sgd <- mf.pyx:241-262)
   c5shard   the first 1.25M users of configs[4]'s shape (every item: 1M; one of 8 ranks' share),
             SVD++ K=128 in the exact per-user form (oracle_svdpp_sgd_affine <- mf.pyx:463-498)
+  c5_u60000 the first 60k users of configs[4]'s shape, the same oracle: the miniature on which the
+            long-chain dealing of dist.chunk_users fires at 8 epoch-chunks
   c5at8_cN_mM  the same 1.25M users in C5@8's multi-rank schedule: split 8 ways by
             dist.shard_users (bench.py --gpus 8), each rank's users dealt into N epoch-chunks by
             dist.chunk_users, the ranks' q / b deltas merged by rule M (3: carried through the
@@ -19,7 +21,7 @@ Same CSR, held-out triples, initial factors (init_tables), global mean and hyper
 The held-out RMSE is recorded after every epoch up to --epochs, so a GPU test can hold any
 E <= epochs to the reference's value; estimates are clipped to [1, 5] like bench.rmse_leg.
 
-usage: python tests/golden/make_scale_golden.py {c4|c5shard} [--epochs 20]
+usage: python tests/golden/make_scale_golden.py {c4|c5shard|c5_u60000|c5at8_cN_mM} [--epochs 20]
 (each case merges its entry into scale_golden.json; c4 ~25 min, c5shard ~1 h on one core)
 """
 import argparse
@@ -41,7 +43,11 @@ import oracle as orc  # noqa: E402
 
 OUT = os.path.join(HERE, "scale_golden.json")
 CASES = {"c4": dict(shape="c4", users=0, algo="svd", K=128),
-         "c5shard": dict(shape="c5", users=1_250_000, algo="svdpp", K=128)}
+         "c5shard": dict(shape="c5", users=1_250_000, algo="svdpp", K=128),
+         # the C5 miniature on which dist.chunk_users' long-chain dealing fires: the first 60k
+         # users at 8 epoch-chunks put 8 users of > 1/256 of a chunk's ratings into chunk 0
+         # (bench.py --shape c5 --users 60000 --chunks 8), as the full C5's 9 long users at 125
+         "c5_u60000": dict(shape="c5", users=60_000, algo="svdpp", K=128)}
 for _n in (2, 4, 8):
     for _m in (2, 3):  # the q / b merge: 2 count-aware (round 3), 3 rank-order composition
         CASES["c5at8_c%d_m%d" % (_n, _m)] = dict(shape="c5", users=1_250_000, algo="svdpp",

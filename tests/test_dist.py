@@ -178,3 +178,23 @@ def test_chunk_users_groups_long_chains():
     srt = np.argsort(-deg, kind="stable")
     for c, us in enumerate(chunk_users(np.arange(len(deg)), row_ptr, 8)):
         np.testing.assert_array_equal(us, srt[c::8])
+
+
+def test_chunk_users_long_chain_branch_fires_on_the_c5_miniature():
+    """the C5 miniature the GPU test pins (the first 60k users of configs[4]'s
+    shape at 8 epoch-chunks, bench.py --shape c5 --users 60000 --chunks 8) has 8 users above
+    1/256 of a chunk's ratings: the long-chain branch puts all 8 in chunk 0; long_chain=0 (the
+    engine option of the same name) deals them round-robin, one per chunk."""
+    from surprise_amd import synthetic
+    U, I, N = synthetic.SHAPES["c5"]
+    deg = synthetic.sharded_truth(U, I, N)["deg"][:60_000]
+    row_ptr = np.concatenate([[0], np.cumsum(deg)])
+    thr = deg.sum() / 8 / 256
+    long_users = set(np.flatnonzero(deg > thr).tolist())
+    assert len(long_users) == 8
+    chunks = chunk_users(np.arange(len(deg)), row_ptr, 8)
+    assert set(chunks[0][:8].tolist()) == long_users
+    old = chunk_users(np.arange(len(deg)), row_ptr, 8, long_chain=0)
+    assert [len(long_users & set(c.tolist())) for c in old] == [1] * 8
+    for cs in (chunks, old):
+        np.testing.assert_array_equal(np.sort(np.concatenate(cs)), np.arange(len(deg)))

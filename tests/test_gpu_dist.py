@@ -186,3 +186,18 @@ def test_rccl_single_rank_collectives(torch, tmp_path):
     assert r["sum_float32"] and r["sum_float64"]
     assert r["max"] == [3, -7, 11] and r["broadcast"] == [2.5] * 5
     assert r["gather_equal"] and r["agreement"] and r["engine_finite"]
+    # the device-resident exchange (sync_items -> _delta_into -> RCCL
+    # all_reduce_sum -> _apply) forced at world 1: the deterministic schedules equal the local
+    # fold; the float-atomic schedule's exchange leaves each chunk's tables unchanged
+    x = r["exchange"]
+    for name in ("svd_log", "svdpp_qlog", "svdpp_atomic", "svdpp_one_buffer"):
+        assert x[name + "_equal"], (name, x[name + "_max_abs_diff"])
+        # one collective per chunk and epoch (+ the SVD log's first-chunk <p^2> sum)
+        assert x[name + "_allreduce_calls"] >= 3 * x[name + "_chunks"], x
+        assert x[name + "_buffer_elems"] > 0
+    assert x["svdpp_qlog_qlog"] and x["svdpp_atomic_finite"]
+    # the overlapped exchange (q's part async beside the y fold, then y's part): two
+    # collectives per chunk; overlap_q=False and the logs: one buffer
+    assert x["svdpp_atomic_overlap"] and not x["svdpp_one_buffer_overlap"]
+    assert not x["svd_log_overlap"] and not x["svdpp_qlog_overlap"]
+    assert x["svdpp_atomic_allreduce_calls"] >= 2 * 3 * x["svdpp_atomic_chunks"], x

@@ -68,6 +68,79 @@ def test_wave_sum_selftest(torch, dtype):
     assert torch.allclose(out.double(), ref, atol=tol)
 
 
+# ------------------------------------------------------- BASELINE configs[0] at its own size
+
+@pytest.fixture(scope="module")
+def synth_ml100k(golden, tmp_path_factory):
+    """BASELINE configs[0]'s data: the ML-100k-shape synthetic ratings written to a file and read
+    back through Reader / Dataset / KFold(5, random_state=0) -- the path make_golden.py ran the
+    reference on (tests/golden/make_golden.py: synth_ml100k); the fold's CSR equals the
+    reference's (sha)."""
+    from surprise_amd import Dataset, Reader, synthetic
+    from surprise_amd.model_selection import KFold
+    from test_oracle_golden import _sha
+    g = golden[0]["synth_ml100k"]
+    u, i, r = synthetic.shape("ml-100k")
+    path = tmp_path_factory.mktemp("ml100k") / "synth.tsv"
+    with open(path, "w") as fh:
+        for a, b, c in zip(u.tolist(), i.tolist(), r.tolist()):
+            fh.write("%d\t%d\t%d\n" % (a, b, int(c)))
+    data = Dataset.load_from_file(str(path), Reader(line_format="user item rating", sep="\t"))
+    ts, test = next(KFold(5, random_state=0).split(data))
+    assert (ts.n_users, ts.n_items, ts.n_ratings, len(test)) == \
+        (g["n_users"], g["n_items"], g["n_ratings"], g["n_test"])
+    assert _sha(*ts.csr()) == g["sha_csr"]
+    return g, data, ts, test
+
+
+def test_configs0_ml100k_svd_k20_e5_deterministic_fp64_equals_reference(torch, synth_ml100k):
+    """BASELINE configs[0] (SVD n_factors=20 n_epochs=5, ML-100k shape, KFold(5, rs=0) fold 0)
+    on the GPU at its own size, the reference's order (one wave) in fp64: factors within 1e-9
+    of the oracle's, which are the reference's bit-for-bit (sha pinned in
+    test_oracle_golden.test_synthetic_fold_matches_reference), and the held-out RMSE within
+    1e-9 of the reference's own (golden.json synth_ml100k.svd_k20_e5)."""
+    from surprise_amd import SVD
+    g, _, ts, test = synth_ml100k
+    params = dict(n_factors=20, n_epochs=5, random_state=0)
+    row_ptr, items, ratings = ts.csr()
+    _, f = run_oracle("SVD", params, row_ptr, items, ratings, ts.n_items, ts.global_mean)
+    algo = SVD(**params, dtype="float64", deterministic=True).fit(ts)
+    for k in ("pu", "qi", "bu", "bi"):
+        np.testing.assert_allclose(getattr(algo, k), f[k], rtol=0, atol=1e-9, err_msg=k)
+    assert abs(_rmse(algo.test(test)) - g["svd_k20_e5"]["rmse"]) < 1e-9
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_configs0_ml100k_default_schedule_within_1e3(torch, synth_ml100k, dtype):
+    """configs[0] on the default parallel schedule (the checkpoint log): held-out RMSE within
+    1e-3 of the reference's (mf.pyx:241-262 run by make_golden.py)."""
+    from surprise_amd import SVD
+    g, _, ts, test = synth_ml100k
+    from surprise_amd import _lib
+    algo = SVD(n_factors=20, n_epochs=5, random_state=0, dtype=dtype).fit(ts)
+    assert algo._engine.mode == _lib.MF_MODE_LOG
+    got = _rmse(algo.test(test))
+    assert abs(got - g["svd_k20_e5"]["rmse"]) < RMSE_TOL, (got, g["svd_k20_e5"]["rmse"])
+
+
+def test_configs0_ml100k_cross_validate_through_the_mirror(torch, synth_ml100k):
+    """configs[0] driven the reference's way: cross_validate(SVD(...), data, cv=KFold(5, rs=0))
+    (validation.py:29-142, split.py:86-122).  Fold 0 is the golden's fold: within 1e-3 of the
+    reference's RMSE; every fold trains (RMSE below the fold's global-mean predictor)."""
+    from surprise_amd import SVD
+    from surprise_amd.model_selection import KFold, cross_validate
+    g, data, _, _ = synth_ml100k
+    res = cross_validate(SVD(n_factors=20, n_epochs=5, random_state=0), data,
+                         measures=["rmse", "mae"], cv=KFold(5, random_state=0))
+    assert len(res["test_rmse"]) == 5 and len(res["fit_time"]) == 5
+    assert abs(res["test_rmse"][0] - g["svd_k20_e5"]["rmse"]) < RMSE_TOL, res["test_rmse"]
+    for k, (tr, te) in enumerate(KFold(5, random_state=0).split(data)):
+        r = np.array([x[2] for x in te])
+        base = float(np.sqrt(np.mean((r - tr.global_mean) ** 2)))
+        assert res["test_rmse"][k] < base, (k, res["test_rmse"][k], base)
+        assert 0 < res["test_mae"][k] < res["test_rmse"][k]
+
+
 # ----------------------------------------------------------------------------- u1 fixture
 
 @pytest.mark.parametrize("name", ["svd_k20_e5", "svd_k10_e3_hyper", "svd_k5_e2_unbiased"])
@@ -732,6 +805,34 @@ def test_narrow_checkpoint_rows_match_padded_rows(torch, u1, K, dtype, heavy, au
     tol = 1e-12 if dtype == "float64" else 1e-5
     for k in ("pu", "qi", "bu", "bi"):
         np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=tol, err_msg=k)
+
+
+@pytest.mark.parametrize("heavy", [0.0, 16])
+def test_fp64_k128_checkpoint_rows_match_deltalog_oracle(torch, golden, u1, heavy):
+    """fp64 K=128 (the C4 factor count at the reference's precision, mf.pyx:206-239): item rows
+    of 1088 B, so the checkpoint log runs in narrow form -- rows of the 128 factor columns (two
+    whole lane groups), both biases beside the groups in the epoch kernel, the replay's third
+    lane group holding the bias column alone.  Factors equal oracle_svd_sgd_deltalog (merge=3)
+    to 1e-9, with and without the heavy users' split."""
+    from surprise_amd.engine import MFEngine
+    ts, test = u1
+    K = 128
+    row_ptr, items, ratings = ts.csr()
+    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
+                 reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    rng = np.random.RandomState(8)
+    pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
+    eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype="float64",
+                   mode="log", heavy=heavy)
+    assert eng.ckpt and eng.narrow and eng.ldq * 8 > 1024 and eng.ldc == K
+    eng.set_factors(pu0, qi0)
+    eng.run_epochs(3)
+    got = eng.get_factors()
+    hp = orc.hyper(**{k: v for k, v in hyper.items() if k != "global_mean"})
+    pu, qi, bu, bi = orc.svd_sgd_deltalog(row_ptr, items, ratings, ts.n_items, K, 3, True,
+                                          ts.global_mean, hp, pu0.copy(), qi0.copy(), merge=3)
+    for k, ref in (("pu", pu), ("qi", qi), ("bu", bu), ("bi", bi)):
+        np.testing.assert_allclose(got[k], ref, rtol=0, atol=1e-9, err_msg=k)
 
 
 @pytest.mark.parametrize("rows,dtype,narrow,heavy", [(256, "float64", False, 0.0),

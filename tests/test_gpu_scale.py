@@ -66,6 +66,19 @@ def test_c4_svd_k128_e20_within_1e3_of_committed_oracle(c4_one):
     assert r["rmse"]["gpu"] < r["rmse"]["global_mean_baseline"]
 
 
+def test_c4_fp64_svd_k128_e20_within_1e3_of_committed_oracle(torch):
+    """C4 at the reference's precision (fp64 arrays, mf.pyx:206-239): SVD K=128 in fp64 -- item
+    rows of 1088 B, the narrow checkpoint log -- 20 epochs within 1e-3 of the committed fp64
+    sequential oracle's held-out RMSE (scale_golden.json c4)."""
+    g = _golden("c4")
+    r = _bench("--shape", "c4", "--dtype", "f64", "--rmse-epochs", "20")
+    assert r["dtype"] == "f64" and r["config"]["n_factors"] == 128
+    assert r["config"]["train_ratings_rank0"] == g["train_ratings"]
+    assert r["rmse"]["reference_oracle_fp64"] == g["rmse_by_epoch"][19]
+    assert abs(r["rmse"]["delta"]) < 1e-3, r["rmse"]
+    assert r["device_bytes_per_rank_max"] < 90e9, r["device_bytes_per_rank_max"]
+
+
 def test_c4_device_memory_within_35gb(c4_one):
     """The packed checkpoint log (one row per pair of ratings) keeps C4 on one GPU under 35 GB."""
     assert c4_one["device_bytes_per_rank_max"] < 35e9, c4_one["device_bytes_per_rank_max"]
@@ -115,6 +128,26 @@ def test_c5_at_8_ranks_schedule_within_1e3_of_committed_oracle(torch):
 
 
 C5_USERS = "60000"
+
+
+def test_c5_miniature_long_chain_dealing_within_1e3_of_committed_oracle(torch):
+    """dist.chunk_users' long-chain dealing (every user of > 1/256 of a
+    chunk's ratings into chunk 0) pinned on a miniature where it fires: the first
+    60k users of C5 at 8 epoch-chunks (8 such users, tests/test_dist.py), SVD++ K=128, 20 epochs,
+    against the exact per-user oracle's held-out RMSE committed in scale_golden.json (c5_u60000,
+    mf.pyx:463-498).  The round-robin dealing (long_chain=0, one long user per chunk) on the
+    same data is held to the same bar; both deltas are printed for the record."""
+    g = _golden("c5_u60000")
+    r = _bench("--shape", "c5", "--users", C5_USERS, "--chunks", "8", "--rmse-epochs", "20")
+    r0 = _bench("--shape", "c5", "--users", C5_USERS, "--chunks", "8", "--rmse-epochs", "20",
+                "--long-chain", "0")
+    print("c5_u60000 E=20: long-chain dealing %+.3e, round-robin %+.3e (oracle %.6f)"
+          % (r["rmse"]["delta"], r0["rmse"]["delta"], g["rmse_by_epoch"][19]))
+    for x in (r, r0):
+        assert "chunks/epoch=8" in x["config"]["workload"]
+        assert x["config"]["train_ratings_rank0"] == g["train_ratings"]
+        assert x["rmse"]["reference_oracle_fp64"] == g["rmse_by_epoch"][19]
+        assert abs(x["rmse"]["delta"]) < 1e-3, x["rmse"]
 
 
 @pytest.fixture(scope="module")

@@ -600,3 +600,10 @@ def test_default_dtype_is_fp64_up_to_the_fp64_row_limit():
     assert SVD(n_factors=256).dtype == "float64"
     assert SVD(n_factors=300).dtype == "float32"
     assert SVD(n_factors=10, dtype="float32").dtype == "float32"
+    # the default follows n_factors set after construction (resolved again at fit)
+    a = SVD(n_factors=10)
+    a.n_factors = 300
+    assert a._dtype_auto and a._auto_dtype() == "float32"
+    b = SVD(n_factors=10, dtype="float64")
+    b.n_factors = 300
+    assert not b._dtype_auto  # (an explicit dtype stays: fit then refuses 300 fp64 factors)
