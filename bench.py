@@ -124,6 +124,9 @@ def parse():
                         "after it; engine option qlog) instead of the float-atomic schedule")
     p.add_argument("--no-c4", action="store_true",
                    help="skip the C4 leg (BASELINE configs[3]'s shape on this GPU)")
+    p.add_argument("--stagger", type=int, default=-1,
+                   help="checkpoint log: the chunk's users in two staggered halves (engine option "
+                        "stagger; -1: the engine's policy, 0 off, 1 on)")
     p.add_argument("--long-chain", type=int, default=-1,
                    help="epoch-chunk dealing: users of > 1/N of a chunk's ratings all in chunk 0 "
                         "(engine option long_chain; -1: the engine's 256, 0: round-robin)")
@@ -750,7 +753,8 @@ def main():
                        **({"replay_rows": args.replay_rows} if args.replay_rows else {}),
                        **({"gram": bool(args.gram)} if args.gram >= 0 else {}),
                        **({"xcd_split": bool(args.xcd_split)} if args.xcd_split >= 0 else {}),
-                       **({"long_chain": args.long_chain} if args.long_chain >= 0 else {}))
+                       **({"long_chain": args.long_chain} if args.long_chain >= 0 else {}),
+                       **({"stagger": bool(args.stagger)} if args.stagger >= 0 else {}))
         eng.set_factors(pu, qi, yj=yj)
         eng._prepare(ctx)  # global per-item counts (all ranks)
         return eng

@@ -294,6 +294,23 @@ int mf_user_sq_reduce(const double *user_sq, int64_t n_rows, int32_t n_cols, dou
 /* Checkpoint interval of the checkpoint log (ratings per stored user row). */
 int mf_ckpt_interval(void);
 
+/* One rank's fold of an SVD++ q-log epoch-chunk in ONE pass over the items (replaces
+ * mf_log_reduce + mf_log_apply + mf_svdpp_y_fold for mf_svdpp_epoch_qlog's chunks; SVDpp.sgd's
+ * item and implicit-factor steps, matrix_factorization.pyx:486-498, in the q log's schedule).
+ * Per item i touched by the chunk, one wavefront:
+ *   S_i = sum over the item's logged rows x in perm[item_row_beg[i] .. item_row_beg[i+1]) of
+ *         (1 - eta)^(N_i - 1 - rpos[x]) qlog[perm[x]] (eta of the bias column in column n_factors),
+ *   qb[i] += lr o (S_i - W reg o qb[i])      (MF_MERGE_RECENCY of mf_log_apply; N_i = totals[i]),
+ *   yj[i] <- A_u yj[i] + ycbuf[u] for u = item_users[item_user_beg[i] ..] in order (A_u = uA[u]).
+ * rec: rpos / totals / p2stat (pos0 must be NULL: one rank).  stat_next / user_sq / n_users: as
+ * mf_log_apply's.  Rows: qb, qlog [.][ldq], yj, ycbuf [.][ldu]. */
+int mf_svdpp_qlog_fold(void *qb, int32_t ldq, int32_t n_factors, void *yj, int32_t ldu,
+                       const void *qlog, const int32_t *perm, const int32_t *item_row_beg,
+                       const int32_t *totals, const mf_recency_t *rec, const mf_hyper_t *hp,
+                       const void *ycbuf, const void *uA, const int32_t *item_users,
+                       const int32_t *item_user_beg, int32_t n_items, double *stat_next,
+                       const double *user_sq, int64_t n_users, int32_t dtype, void *stream);
+
 /*
  * Delta-log merge, step 2: S_i = sum of sums[p] over p in [item_piece_ptr[i], item_piece_ptr[i+1])
  * (item_piece_ptr NULL: S_i = sums[i], e.g. after an all-reduce), plus -- when sums2 is not NULL

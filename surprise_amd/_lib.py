@@ -82,6 +82,9 @@ SIGNATURES = {
                       ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _vp,
                       ctypes.POINTER(MfRecency), _i32, _i32, _vp],
     "mf_ckpt_interval": [],
+    "mf_svdpp_qlog_fold": [_vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp,
+                           ctypes.POINTER(MfRecency), ctypes.POINTER(MfHyper), _vp, _vp, _vp,
+                           _vp, _i32, _vp, _vp, _i64, _i32, _vp],
     "mf_log_apply": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
                      ctypes.POINTER(MfHyper), _vp, _i32, _vp, _i32, _vp, _vp, _i64, _i32, _vp],
     "mf_item_merge": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,

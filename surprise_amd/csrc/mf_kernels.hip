@@ -3841,6 +3841,139 @@ __global__ __launch_bounds__(kBlock) void y_apply_kernel(
     }
 }
 
+// ---------------------------------------------------------------- SVD++ q log: the fused fold
+//
+// One rank's fold of an SVD++ q-log chunk (mf_svdpp_qlog_fold) in ONE pass over the items, each
+// item by one wave: (1) its logged q / b gradient rows (the chunk's rows of the item: positions
+// item_row_beg[i] .. item_row_beg[i+1] of perm, users in order) summed with their recency weights
+// (1 - eta)^(N - 1 - pos) (log_reduce_kernel's weights), then q += lr (S - w N reg q) -- what
+// mf_log_reduce + mf_log_apply compute; (2) its y row composed with the chunk's users' affine
+// maps y <- A_u y + c_u in CSR order (positions item_user_beg[i] .. of item_users) -- what
+// mf_svdpp_y_fold computes.  Nothing round-trips through piece sums; every load is a row gather
+// whose indices come from ONE coalesced vector load per 64 rows, so a wave keeps kF rows in
+// flight per part and the launch's occupancy (kFoldWPC waves per CU) hides the rest of the
+// latency.  Items the chunk did not touch are skipped (their rows do not change).  Block 0: the
+// next chunk's {sum |p_u|^2, count} from user_sq, like mf_log_apply's.
+constexpr int kFoldF = 8;      // rows of one part in flight per wave
+constexpr int kFoldWPC = 32;   // waves per CU
+template <typename T, int VQ, int VY>
+__global__ __launch_bounds__(kBlock) void qlog_fold_kernel(
+    T *__restrict__ qb, int ldq, int K, T *__restrict__ yj, int ldu, const T *__restrict__ qlog,
+    const int32_t *__restrict__ perm, const int32_t *__restrict__ item_row_beg,
+    const int32_t *__restrict__ totals, Recency rc, double lr_f, double reg_f, double lr_b,
+    double reg_b, const T *__restrict__ ycbuf, const T *__restrict__ uA,
+    const int32_t *__restrict__ item_users, const int32_t *__restrict__ item_user_beg,
+    int n_items, double *__restrict__ stat_next, const double *__restrict__ user_sq,
+    int64_t n_sq, int sq_cols)
+{
+    if (stat_next && blockIdx.x == 0) {
+        if (user_sq) block_sum_sq(user_sq, n_sq, sq_cols, stat_next);
+        else if (threadIdx.x < 2) stat_next[threadIdx.x] = 0.0;
+        return;
+    }
+    const int lane = threadIdx.x & (kWave - 1);
+    const int blk0 = stat_next ? 1 : 0;
+    const int64_t wave = (int64_t)(blockIdx.x - blk0) * (kBlock / kWave) +
+                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t n_waves = ((int64_t)(gridDim.x - blk0) * kBlock) / kWave;
+    double l_q, l_b;
+    recency_logs(rc, l_q, l_b);
+    const double n_p2 = rc.p2stat[1];
+    const double eta_f = rc.lr_qi * ((n_p2 > 0 ? rc.p2stat[0] / n_p2 : 0.0) + rc.reg_qi);
+    const double eta_b = rc.eta_b;
+    for (int64_t i = wave; i < n_items; i += n_waves) {
+        const int r0 = item_row_beg[i], r1 = item_row_beg[i + 1];
+        const int u0 = item_user_beg[i], u1 = item_user_beg[i + 1];
+        if (r0 == r1 && u0 == u1) continue;  // (untouched this chunk)
+        const int N = totals[i];
+        T q[VQ], y[VY], acc[VQ];
+#pragma unroll
+        for (int v = 0; v < VQ; ++v) {
+            const int c = lane + kWave * v;
+            q[v] = c < ldq ? qb[i * ldq + c] : T(0);
+            acc[v] = T(0);
+        }
+#pragma unroll
+        for (int v = 0; v < VY; ++v) {
+            const int c = lane + kWave * v;
+            y[v] = c < K ? yj[i * ldu + c] : T(0);
+        }
+        // (1) the weighted sum of the item's gradient rows, 64 row indices per vector load
+        for (int x0 = r0; x0 < r1; x0 += kWave) {
+            const int cnt = r1 - x0 < kWave ? r1 - x0 : kWave;
+            const int xl = x0 + (lane < cnt ? lane : cnt - 1);
+            const int k_l = perm[xl];
+            const double back = (double)(N - 1 - rc.rpos[xl] - (rc.pos0 ? rc.pos0[i] : 0));
+            const T wf_l = lane < cnt ? (T)exp(back * l_q) : T(0);
+            const T wb_l = lane < cnt ? (T)exp(back * l_b) : T(0);
+            for (int a0 = 0; a0 < cnt; a0 += kFoldF) {
+                T g[kFoldF][VQ];
+#pragma unroll
+                for (int a = 0; a < kFoldF; ++a) {
+                    const int x = a0 + a < cnt ? a0 + a : cnt - 1;
+                    const T *row = qlog + (int64_t)readlane(k_l, x) * ldq;
+#pragma unroll
+                    for (int v = 0; v < VQ; ++v) {
+                        const int c = lane + kWave * v;
+                        g[a][v] = c <= K ? row[c] : T(0);
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < kFoldF; ++a) {
+                    const int x = a0 + a < kWave ? a0 + a : kWave - 1;
+                    const T wf = readlane(wf_l, x), wb = readlane(wb_l, x);  // (0 past cnt)
+#pragma unroll
+                    for (int v = 0; v < VQ; ++v)
+                        acc[v] += (lane + kWave * v == K ? wb : wf) * g[a][v];
+                }
+            }
+        }
+        // (2) y: the chunk's users' maps in CSR order, 64 users per vector load
+        for (int x0 = u0; x0 < u1; x0 += kWave) {
+            const int cnt = u1 - x0 < kWave ? u1 - x0 : kWave;
+            const int u_l = item_users[x0 + (lane < cnt ? lane : cnt - 1)];
+            const T A_l = uA[u_l];
+            for (int a0 = 0; a0 < cnt; a0 += kFoldF) {
+                T g[kFoldF][VY];
+#pragma unroll
+                for (int a = 0; a < kFoldF; ++a) {
+                    const int x = a0 + a < cnt ? a0 + a : cnt - 1;
+                    const T *row = ycbuf + (int64_t)readlane(u_l, x) * ldu;
+#pragma unroll
+                    for (int v = 0; v < VY; ++v) {
+                        const int c = lane + kWave * v;
+                        g[a][v] = c < K ? row[c] : T(0);
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < kFoldF; ++a) {
+                    if (a0 + a >= cnt) break;  // (uniform)
+                    const T A = readlane(A_l, a0 + a);
+#pragma unroll
+                    for (int v = 0; v < VY; ++v) y[v] = A * y[v] + g[a][v];
+                }
+            }
+        }
+        // q += lr (S - w N reg q), w N = sum_k (1 - eta)^(N-1-k) (mf_log_apply's recency rule)
+        const double wn_f = N > 1 ? -expm1(N * l_q) / eta_f : (double)N;
+        const double wn_b = N > 1 ? -expm1(N * l_b) / eta_b : (double)N;
+#pragma unroll
+        for (int v = 0; v < VQ; ++v) {
+            const int c = lane + kWave * v;
+            if (c <= K) {
+                const bool b = c == K;
+                qb[i * ldq + c] = q[v] + (T)(b ? lr_b : lr_f) *
+                                             (acc[v] - (T)(b ? wn_b : wn_f) * (T)(b ? reg_b : reg_f) * q[v]);
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < VY; ++v) {
+            const int c = lane + kWave * v;
+            if (c < K) yj[i * ldu + c] = y[v];
+        }
+    }
+}
+
 // accuracy.rmse / mae over the batched estimates (algo_base.py:148-169 finishing, accuracy.py:
 // 22-90): est -> fallback where impossible, minus the reader offset, clipped to the rating scale,
 // against r - offset; out[0] += sum err^2, out[1] += sum |err|, out[2] += count (fp64).
@@ -4518,6 +4651,52 @@ int mf_svdpp_y_fold(void *yj, int32_t ldu, int32_t n_factors, const void *ycbuf,
                                ldu, n_factors, item_piece_ptr, n_items, (const T *)piece_c,
                                (const T *)piece_A, piece_item ? 2 : 1);
             return check_launch("y_apply_kernel");
+        });
+    };
+    if (dtype == MF_F32) return run(float{});
+    if (dtype == MF_F64) return run(double{});
+    return set_err(MF_E_ARG, "bad dtype");
+}
+
+int mf_svdpp_qlog_fold(void *qb, int32_t ldq, int32_t n_factors, void *yj, int32_t ldu,
+                       const void *qlog, const int32_t *perm, const int32_t *item_row_beg,
+                       const int32_t *totals, const mf_recency_t *rec, const mf_hyper_t *hp,
+                       const void *ycbuf, const void *uA, const int32_t *item_users,
+                       const int32_t *item_user_beg, int32_t n_items, double *stat_next,
+                       const double *user_sq, int64_t n_users, int32_t dtype, void *stream)
+{
+    if (n_items < 0 || n_factors < 1 || ldq < n_factors + 1 || ldu < n_factors)
+        return set_err(MF_E_ARG, "bad shape");
+    if (!qb || !yj || !qlog || !perm || !item_row_beg || !totals || !rec || !hp || !ycbuf ||
+        !uA || !item_users || !item_user_beg)
+        return set_err(MF_E_ARG, "null argument");
+    if (rec->pos0) return set_err(MF_E_UNSUPPORTED, "the fused fold is one rank's (pos0 = 0)");
+    if (user_sq && (!stat_next || n_users < 0)) return set_err(MF_E_ARG, "user_sq needs stat_next");
+    if (stat_next && stat_next == rec->p2stat) return set_err(MF_E_ARG, "stat_next aliases p2stat");
+    if (n_items == 0) return 0;
+    Recency rc;
+    if (int e = make_recency(rec, hp, rc)) return e;
+    const int64_t cap = (int64_t)n_cus() * kFoldWPC;
+    const int g = grid_for_waves(n_items < cap ? n_items : cap) + (stat_next ? 1 : 0);
+    hipStream_t st = (hipStream_t)stream;
+    auto run = [&](auto tag_t) -> int {
+        using T = decltype(tag_t);
+        return dispatch_v<T>(ldq, [&](auto vq) -> int {
+            constexpr int VQ = decltype(vq)::value;
+            return dispatch_v<T>(ldu, [&](auto vy) -> int {
+                constexpr int VY = decltype(vy)::value;
+                if constexpr (VQ > 5 || VY > VQ || VQ - VY > 1) {
+                    return set_err(MF_E_UNSUPPORTED, "the fused fold: rows of <= 320 columns");
+                } else {
+                    hipLaunchKernelGGL((qlog_fold_kernel<T, VQ, VY>), dim3(g), dim3(kBlock), 0, st,
+                                       (T *)qb, ldq, n_factors, (T *)yj, ldu, (const T *)qlog, perm,
+                                       item_row_beg, totals, rc, hp->lr_qi, hp->reg_qi, hp->lr_bi,
+                                       hp->reg_bi, (const T *)ycbuf, (const T *)uA, item_users,
+                                       item_user_beg, n_items, stat_next, user_sq, n_users,
+                                       n_factors);
+                    return check_launch("qlog_fold_kernel");
+                }
+            });
         });
     };
     if (dtype == MF_F32) return run(float{});

@@ -385,7 +385,7 @@ class MFEngine(ItemSync, Predictor):
                  join="event",
                  helpers=None, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
                  replay_rows=None, gram=None, xcd_split=None, qlog=None, top=None,
-                 exchange=None, long_chain=256, overlap_q=True):
+                 exchange=None, long_chain=256, overlap_q=True, fused=True, stagger=None):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -430,6 +430,15 @@ class MFEngine(ItemSync, Predictor):
           long_chain  epoch-chunk dealing (dist.chunk_users): users of more than 1 / long_chain
                       of a chunk's ratings all go to chunk 0 (when at most n_chunks of them);
                       0: plain round-robin dealing (the dealing before round 4)
+          stagger     checkpoint log, large chunks: the chunk's users in two halves (every
+                      other user in schedule order), half A's epoch kernel first on the main
+                      stream, then half B's epoch on the side stream beside A's log replay, then
+                      B's replay -- the same arithmetic (the fold adds both halves' piece sums);
+                      None: on where a chunk holds >= STAGGER_MIN_NNZ ratings and no heavy split
+          fused       SVD++ q log on one rank: the chunk's fold in one pass over the items
+                      (mf_svdpp_qlog_fold: the q gradients' weighted sums, the q step and the y
+                      maps' composition together); False: mf_log_reduce + mf_log_apply +
+                      mf_svdpp_y_fold (the several-rank exchange always takes that path)
           overlap_q   SVD++ atomic schedule on several ranks over RCCL: q's part of the
                       exchange all-reduced (async) while the y fold runs (False: one buffer)
           exchange    None: the multi-rank exchange (snapshots, the packed all-reduce buffer,
@@ -489,6 +498,7 @@ class MFEngine(ItemSync, Predictor):
             self.n_waves = SVDPP_WAVES_PER_CU * props.multi_processor_count
         self.world = int(world)
         self.multi = self.world > 1 or bool(exchange)  # (the exchange path's tables and rules)
+        self.fused = bool(fused)
         self.overlap_q = bool(overlap_q)
         self._q_work = None
         if merge not in ("count", "recency", "sum"):
@@ -571,7 +581,13 @@ class MFEngine(ItemSync, Predictor):
         C = _lib.load().mf_ckpt_interval() if self.ckpt else 0
         _pu = []
         pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
-        self.side = torch.cuda.Stream(device=dev) if self.ckpt and heavy > 0 else None
+        # stagger (large chunks): two halves, B's epoch beside A's replay
+        if stagger is None:
+            stagger = (self.ckpt and heavy <= 0 and not self.deterministic and
+                       int(row_ptr[-1] - row_ptr[0]) >= self.n_chunks * self.STAGGER_MIN_NNZ)
+        self.stagger = bool(stagger) and self.ckpt and heavy <= 0
+        self.side = torch.cuda.Stream(device=dev) if self.ckpt and (heavy > 0 or self.stagger) \
+            else None
         # the top users of the heavy launch on the main stream, the rest of it on a third stream
         # (its replay and the pre-fold then overlap the top chains)
         if top is None:
@@ -605,7 +621,11 @@ class MFEngine(ItemSync, Predictor):
                 self._totals_local.append(
                     item_counts(c, row_ptr, items, self.n_items).astype(np.int32))
                 continue
-            parts = split_groups(c, row_ptr, heavy, self.top) if self.side is not None else [c]
+            if self.stagger:  # [B, A]: A (every other user from the first) runs first
+                parts = [c[1::2], c[0::2]] if len(c) > 1 else [c]
+            else:
+                parts = split_groups(c, row_ptr, heavy, self.top) if self.side is not None \
+                    else [c]
             # (recency, a split chunk: each rating's position among the chunk's ratings of its
             # item, indexed by CSR position; one group: its perm is already in that order)
             kpos = None
@@ -632,6 +652,8 @@ class MFEngine(ItemSync, Predictor):
                     rp = kpos[perm] if kpos is not None else \
                         np.arange(len(perm), dtype=np.int64) - np.repeat(pb[ipp[:-1]], cnt)
                     lg["rpos"] = to_dev(rp.astype(np.int32))
+                if self.qlog_pp:  # (the fused fold: each item's range of perm)
+                    lg["irb"] = to_dev(pb[ipp].astype(np.int32))
                 lgs.append(lg)
             main = lgs[0]
             main["heavy"] = lgs[1] if len(lgs) > 1 else None
@@ -686,7 +708,7 @@ class MFEngine(ItemSync, Predictor):
                 perm, pb, ipp, _ = log_layout(row_ptr, items, us.cpu().numpy(), self.n_items)
                 iusr = pos_user()[perm]
                 self.ycsc.append(dict(users=to_dev(iusr), pb=to_dev(pb), ipp=to_dev(ipp),
-                                      n_pieces=len(pb) - 1,
+                                      n_pieces=len(pb) - 1, iub=to_dev(pb[ipp].astype(np.int32)),
                                       pitem=to_dev(np.repeat(np.arange(self.n_items,
                                                                        dtype=np.int32),
                                                              np.diff(ipp)))))
@@ -791,6 +813,7 @@ class MFEngine(ItemSync, Predictor):
     HEAVY_TOP_USERS = 0
     HEAVY_USERS_GRAM = 256  # ... with the blocked solve (one workgroup per user)
     HEAVY_MAX_NNZ = 8_000_000
+    STAGGER_MIN_NNZ = 8_000_000  # (chunks at least this large: two staggered halves)
 
     def _auto_heavy(self, row_ptr):
         """The heavy/light XCD split pays where the epoch is bound by its longest user chains:
@@ -995,6 +1018,10 @@ class MFEngine(ItemSync, Predictor):
             ev["end"].record(self.stream)
         if self._q_early():  # (several ranks: q's part of the exchange overlaps the y fold)
             self._exchange_q_begin()
+        if self._fused_fold():  # (q log, one rank: the whole fold in _merge_local)
+            if "end_r" in ev:
+                ev["end_r"].record(self.stream)
+            return
         if self.ydefer:
             y = self.ycsc[c]
             _lib.call("mf_svdpp_y_fold", self._ptr(self.yj), self.ld, self.K,
@@ -1060,6 +1087,27 @@ class MFEngine(ItemSync, Predictor):
             if "end" in ev:
                 ev["end"].record(self.stream)
             self._reduce_log(lg, self.sums.data_ptr(), st)
+        elif self.stagger:
+            # main: A's epoch, then A's replay; side (after A's epoch): B's epoch, B's replay --
+            # B's epoch kernel runs beside A's replay; main joins side before the fold
+            side = self.side
+            sh = ctypes.c_void_p(side.cuda_stream)
+            self._epoch_sq(hv["sched"], hv["sched"].numel(), lw, st)
+            if "end" in ev:
+                ev["end"].record(self.stream)
+            a_done = torch.cuda.Event()
+            a_done.record(self.stream)
+            side.wait_event(a_done)
+            if "l_start" in ev:
+                ev["l_start"].record(side)
+            self._epoch_sq(ls, ln, lw, sh)
+            if "l_end" in ev:
+                ev["l_end"].record(side)
+            self._reduce_log(lg, self.sums.data_ptr(), sh)
+            b_done = torch.cuda.Event()
+            b_done.record(side)
+            self._reduce_log(hv, sums_h, st)
+            self.stream.wait_event(b_done)
         elif lg.get("mid") is not None:
             self._run_chunk_three(lg, ev, st, fork_bound)
         else:
@@ -1365,7 +1413,23 @@ class MFEngine(ItemSync, Predictor):
             tabs.append((self.yj, self.yj_s, self.ld, -1, "affine"))
         return tabs
 
+    def _fused_fold(self):
+        """SVD++ q log on one rank: reduce + apply + y composition in one launch."""
+        return self.qlog_pp and self.fused and self.recency and not self._exchanging(self._ctx)
+
     def _merge_local(self):
+        if self._fused_fold():
+            c = getattr(self, "_chunk", 0)
+            lg, y = self.logs[c], self.ycsc[c]
+            rec = _lib.MfRecency(lg["rpos"].data_ptr(), None, self._totals()[c].data_ptr(),
+                                 self.work.data_ptr())
+            _lib.call("mf_svdpp_qlog_fold", self._ptr(self.qb), self.ldq, self.K,
+                      self._ptr(self.yj), self.ld, ctypes.c_void_p(self._qlog_base),
+                      self._ptr(lg["perm"]), self._ptr(lg["irb"]), self._ptr(self._totals()[c]),
+                      ctypes.byref(rec), ctypes.byref(self._hyper), self._ptr(self.ycbuf),
+                      self._ptr(self.uA), self._ptr(y["users"]), self._ptr(y["iub"]),
+                      self.n_items, *self._stat_args(True), self.dtype, self._st())
+            return
         if self.is_log:
             self._log_fold(None, True)
 

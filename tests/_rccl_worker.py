@@ -130,7 +130,10 @@ def forced_exchange(ctx, np, torch):
             def run(eng=eng, box=box):
                 eng.run_epochs(3, ctx)
                 box["f"] = eng.get_factors(ctx)
-            n_calls, n_async = counting(run) if forced else (0, 0)
+            if forced:
+                n_calls, n_async = counting(run)
+            else:
+                run()
             got[forced] = box["f"]
             if forced:
                 out[name + "_allreduce_calls"] = n_calls

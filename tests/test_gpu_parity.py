@@ -550,11 +550,13 @@ def test_svdpp_item_bias_beside_lane_groups_rmse(torch, u1, K, dtype):
 
 
 @pytest.mark.parametrize("K,chunks", [(10, 1), (10, 3), (64, 2)])
-def test_svdpp_qlog_fp64_matches_stalelog_oracle(torch, u1, K, chunks):
+@pytest.mark.parametrize("fused", [True, False])
+def test_svdpp_qlog_fp64_matches_stalelog_oracle(torch, u1, K, chunks, fused):
     """SVD++ with the q log (mf_svdpp_epoch_qlog: item rows read-only within a chunk, gradient
-    rows folded by mf_log_reduce / mf_log_apply with recency weights, y deferred) in fp64
-    against oracle_svdpp_sgd_stalelog with every item stale, same chunking, to 1e-9 -- K=64 is
-    the layout with the item bias beside the lane group (fp64 K * 8 = 512 B)."""
+    rows folded with recency weights, y deferred) in fp64 against oracle_svdpp_sgd_stalelog with
+    every item stale, same chunking, to 1e-9 -- K=64 is the layout with the item bias beside the
+    lane group (fp64 K * 8 = 512 B).  fused: the one-pass fold (mf_svdpp_qlog_fold); else
+    mf_log_reduce + mf_log_apply + mf_svdpp_y_fold."""
     from surprise_amd import SVDpp
     from surprise_amd.dist import chunk_users
     ts, test = u1
@@ -566,9 +568,10 @@ def test_svdpp_qlog_fp64_matches_stalelog_oracle(torch, u1, K, chunks):
     P, f = run_oracle_stalelog(params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
                                cou, chunks)
     algo = SVDpp(**params, dtype="float64", chunks_per_epoch=chunks)
-    algo._engine_options = {"qlog": True}
+    algo._engine_options = {"qlog": True, "fused": fused}
     algo.fit(ts)
     assert algo._engine.qlog_pp and not algo._engine.hx
+    assert algo._engine._fused_fold() == fused
     for k in ("pu", "qi", "yj", "bu", "bi"):
         np.testing.assert_allclose(getattr(algo, k), f[k], rtol=0, atol=1e-9, err_msg=k)
     ref = _oracle_test_rmse(P, f, "SVDpp", ts, list(test))[1]
@@ -805,6 +808,31 @@ def test_narrow_checkpoint_rows_match_padded_rows(torch, u1, K, dtype, heavy, au
     tol = 1e-12 if dtype == "float64" else 1e-5
     for k in ("pu", "qi", "bu", "bi"):
         np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=tol, err_msg=k)
+
+
+@pytest.mark.parametrize("K", [20, 128])
+def test_staggered_halves_match_deltalog_oracle(torch, u1, K):
+    """stagger (large chunks' default): the chunk's users in two halves, half B's epoch kernel
+    beside half A's log replay -- the fold adds both halves' piece sums, so fp64 factors equal
+    oracle_svd_sgd_deltalog (merge=3) to 1e-9 (K=128: the narrow rows of C4 at fp64)."""
+    from surprise_amd.engine import MFEngine
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
+                 reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    rng = np.random.RandomState(9)
+    pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
+    eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype="float64",
+                   mode="log", heavy=0, stagger=True)
+    assert eng.stagger and eng.logs[0]["heavy"] is not None
+    eng.set_factors(pu0, qi0)
+    eng.run_epochs(3)
+    got = eng.get_factors()
+    hp = orc.hyper(**{k: v for k, v in hyper.items() if k != "global_mean"})
+    pu, qi, bu, bi = orc.svd_sgd_deltalog(row_ptr, items, ratings, ts.n_items, K, 3, True,
+                                          ts.global_mean, hp, pu0.copy(), qi0.copy(), merge=3)
+    for k, ref in (("pu", pu), ("qi", qi), ("bu", bu), ("bi", bi)):
+        np.testing.assert_allclose(got[k], ref, rtol=0, atol=1e-9, err_msg=k)
 
 
 @pytest.mark.parametrize("heavy", [0.0, 16])
