@@ -294,21 +294,40 @@ int mf_user_sq_reduce(const double *user_sq, int64_t n_rows, int32_t n_cols, dou
 /* Checkpoint interval of the checkpoint log (ratings per stored user row). */
 int mf_ckpt_interval(void);
 
+/* The item layout of one SVD++ q-log epoch-chunk for mf_svdpp_qlog_fold, in item-grouped
+ * positions (the chunk's ratings grouped by item, users in order within an item).  Cold items
+ * (at most a few rows: one wavefront takes them in turn) list their rows directly; hot items
+ * (more rows) are cut into pieces of <= 64 rows, summed / composed per piece by the launch's two
+ * pre-passes first.  An item is either cold or hot. */
+typedef struct mf_qlog_fold {
+    const int32_t *perm;          /* cold items' log rows, by item                               */
+    const int32_t *rpos;          /* [perm entries] the row's position among its item's rows     */
+    const int32_t *item_row_beg;  /* [n_items + 1] item i's cold rows: perm[beg[i] .. beg[i+1]) */
+    const int32_t *users;         /* cold items' raters (CSR order within an item)              */
+    const int32_t *item_user_beg; /* [n_items + 1] item i's cold raters                         */
+    const int32_t *hot_perm, *hot_rpos, *hot_users;  /* hot items' rows / positions / raters     */
+    const int32_t *hot_piece_beg;       /* [n_hot_pieces + 1] pieces of <= 64 hot positions     */
+    const int32_t *hot_piece_item;      /* [n_hot_pieces] each piece's item                     */
+    const int32_t *hot_item_piece_ptr;  /* [n_items + 1] item i's pieces                        */
+    int64_t n_hot_pieces;
+    void *hot_sums;                     /* scratch [n_hot_pieces][ldq]                          */
+    void *hot_piece_c, *hot_piece_A;    /* scratch [n_hot_pieces][ldu], [n_hot_pieces]          */
+} mf_qlog_fold_t;
+
 /* One rank's fold of an SVD++ q-log epoch-chunk in ONE pass over the items (replaces
  * mf_log_reduce + mf_log_apply + mf_svdpp_y_fold for mf_svdpp_epoch_qlog's chunks; SVDpp.sgd's
  * item and implicit-factor steps, matrix_factorization.pyx:486-498, in the q log's schedule).
  * Per item i touched by the chunk, one wavefront:
- *   S_i = sum over the item's logged rows x in perm[item_row_beg[i] .. item_row_beg[i+1]) of
- *         (1 - eta)^(N_i - 1 - rpos[x]) qlog[perm[x]] (eta of the bias column in column n_factors),
+ *   S_i = sum over the item's logged rows x of (1 - eta)^(N_i - 1 - rpos[x]) qlog[perm[x]]
+ *         (eta of the bias column in column n_factors; hot items: their pieces' sums),
  *   qb[i] += lr o (S_i - W reg o qb[i])      (MF_MERGE_RECENCY of mf_log_apply; N_i = totals[i]),
- *   yj[i] <- A_u yj[i] + ycbuf[u] for u = item_users[item_user_beg[i] ..] in order (A_u = uA[u]).
- * rec: rpos / totals / p2stat (pos0 must be NULL: one rank).  stat_next / user_sq / n_users: as
+ *   yj[i] <- A_u yj[i] + ycbuf[u] for the item's raters u in CSR order (A_u = uA[u]).
+ * p2stat: the chunk-start {sum p^2, count} (one rank).  stat_next / user_sq / n_users: as
  * mf_log_apply's.  Rows: qb, qlog [.][ldq], yj, ycbuf [.][ldu]. */
 int mf_svdpp_qlog_fold(void *qb, int32_t ldq, int32_t n_factors, void *yj, int32_t ldu,
-                       const void *qlog, const int32_t *perm, const int32_t *item_row_beg,
-                       const int32_t *totals, const mf_recency_t *rec, const mf_hyper_t *hp,
-                       const void *ycbuf, const void *uA, const int32_t *item_users,
-                       const int32_t *item_user_beg, int32_t n_items, double *stat_next,
+                       const void *qlog, const mf_qlog_fold_t *lay, const int32_t *totals,
+                       const double *p2stat, const mf_hyper_t *hp, const void *ycbuf,
+                       const void *uA, int32_t n_items, double *stat_next,
                        const double *user_sq, int64_t n_users, int32_t dtype, void *stream);
 
 /*

@@ -54,6 +54,14 @@ class MfRecency(ctypes.Structure):
                 ("p2stat", ctypes.c_void_p)]
 
 
+class MfQlogFold(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "perm", "rpos", "item_row_beg", "users", "item_user_beg", "hot_perm", "hot_rpos",
+        "hot_users", "hot_piece_beg", "hot_piece_item", "hot_item_piece_ptr")] + \
+        [("n_hot_pieces", ctypes.c_int64)] + \
+        [(n, ctypes.c_void_p) for n in ("hot_sums", "hot_piece_c", "hot_piece_A")]
+
+
 _vp, _i32, _i64, _dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
 
 # name -> argtypes (all return int except mf_last_error)
@@ -82,9 +90,9 @@ SIGNATURES = {
                       ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i64, _vp, _vp,
                       ctypes.POINTER(MfRecency), _i32, _i32, _vp],
     "mf_ckpt_interval": [],
-    "mf_svdpp_qlog_fold": [_vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp,
-                           ctypes.POINTER(MfRecency), ctypes.POINTER(MfHyper), _vp, _vp, _vp,
-                           _vp, _i32, _vp, _vp, _i64, _i32, _vp],
+    "mf_svdpp_qlog_fold": [_vp, _i32, _i32, _vp, _i32, _vp, ctypes.POINTER(MfQlogFold), _vp,
+                           _vp, ctypes.POINTER(MfHyper), _vp, _vp, _i32, _vp, _vp, _i64, _i32,
+                           _vp],
     "mf_log_apply": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
                      ctypes.POINTER(MfHyper), _vp, _i32, _vp, _i32, _vp, _vp, _i64, _i32, _vp],
     "mf_item_merge": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,

@@ -3864,7 +3864,9 @@ __global__ __launch_bounds__(kBlock) void qlog_fold_kernel(
     double reg_b, const T *__restrict__ ycbuf, const T *__restrict__ uA,
     const int32_t *__restrict__ item_users, const int32_t *__restrict__ item_user_beg,
     int n_items, double *__restrict__ stat_next, const double *__restrict__ user_sq,
-    int64_t n_sq, int sq_cols)
+    int64_t n_sq, int sq_cols, const T *__restrict__ hot_sums,
+    const int32_t *__restrict__ hot_item_piece_ptr, const T *__restrict__ hot_pc_c,
+    const T *__restrict__ hot_pc_A)
 {
     if (stat_next && blockIdx.x == 0) {
         if (user_sq) block_sum_sq(user_sq, n_sq, sq_cols, stat_next);
@@ -3884,7 +3886,11 @@ __global__ __launch_bounds__(kBlock) void qlog_fold_kernel(
     for (int64_t i = wave; i < n_items; i += n_waves) {
         const int r0 = item_row_beg[i], r1 = item_row_beg[i + 1];
         const int u0 = item_user_beg[i], u1 = item_user_beg[i + 1];
-        if (r0 == r1 && u0 == u1) continue;  // (untouched this chunk)
+        // a hot item (more rows than one wave takes in turn): its rows already summed per piece
+        // and its users' maps composed per piece by the launch's two pre-passes
+        const int h0 = hot_item_piece_ptr ? hot_item_piece_ptr[i] : 0;
+        const int h1 = hot_item_piece_ptr ? hot_item_piece_ptr[i + 1] : 0;
+        if (r0 == r1 && u0 == u1 && h0 == h1) continue;  // (untouched this chunk)
         const int N = totals[i];
         T q[VQ], y[VY], acc[VQ];
 #pragma unroll
@@ -3927,6 +3933,42 @@ __global__ __launch_bounds__(kBlock) void qlog_fold_kernel(
                         acc[v] += (lane + kWave * v == K ? wb : wf) * g[a][v];
                 }
             }
+        }
+        // (1') a hot item: its pieces' weighted sums, kFoldF pieces in flight
+        for (int p0 = h0; p0 < h1; p0 += kFoldF) {
+            T g[kFoldF][VQ];
+#pragma unroll
+            for (int a = 0; a < kFoldF; ++a) {
+                const bool ok = p0 + a < h1;
+                const T *row = hot_sums + (int64_t)(ok ? p0 + a : h0) * ldq;
+#pragma unroll
+                for (int v = 0; v < VQ; ++v) {
+                    const int c = lane + kWave * v;
+                    g[a][v] = ok && c <= K ? row[c] : T(0);
+                }
+            }
+#pragma unroll
+            for (int a = 0; a < kFoldF; ++a)
+#pragma unroll
+                for (int v = 0; v < VQ; ++v) acc[v] += g[a][v];
+        }
+        // (2') a hot item's y: its pieces' composed maps in piece (user) order
+        for (int p0 = h0; p0 < h1; p0 += kFoldF) {
+            T g[kFoldF][VY], A[kFoldF];
+#pragma unroll
+            for (int a = 0; a < kFoldF; ++a) {
+                const bool ok = p0 + a < h1;
+                A[a] = ok ? hot_pc_A[p0 + a] : T(1);  // (past the item: the identity map)
+#pragma unroll
+                for (int v = 0; v < VY; ++v) {
+                    const int c = lane + kWave * v;
+                    g[a][v] = ok && c < K ? hot_pc_c[(int64_t)(p0 + a) * ldu + c] : T(0);
+                }
+            }
+#pragma unroll
+            for (int a = 0; a < kFoldF; ++a)
+#pragma unroll
+                for (int v = 0; v < VY; ++v) y[v] = A[a] * y[v] + g[a][v];
         }
         // (2) y: the chunk's users' maps in CSR order, 64 users per vector load
         for (int x0 = u0; x0 < u1; x0 += kWave) {
@@ -4659,28 +4701,58 @@ int mf_svdpp_y_fold(void *yj, int32_t ldu, int32_t n_factors, const void *ycbuf,
 }
 
 int mf_svdpp_qlog_fold(void *qb, int32_t ldq, int32_t n_factors, void *yj, int32_t ldu,
-                       const void *qlog, const int32_t *perm, const int32_t *item_row_beg,
-                       const int32_t *totals, const mf_recency_t *rec, const mf_hyper_t *hp,
-                       const void *ycbuf, const void *uA, const int32_t *item_users,
-                       const int32_t *item_user_beg, int32_t n_items, double *stat_next,
+                       const void *qlog, const mf_qlog_fold_t *lay, const int32_t *totals,
+                       const double *p2stat, const mf_hyper_t *hp, const void *ycbuf,
+                       const void *uA, int32_t n_items, double *stat_next,
                        const double *user_sq, int64_t n_users, int32_t dtype, void *stream)
 {
     if (n_items < 0 || n_factors < 1 || ldq < n_factors + 1 || ldu < n_factors)
         return set_err(MF_E_ARG, "bad shape");
-    if (!qb || !yj || !qlog || !perm || !item_row_beg || !totals || !rec || !hp || !ycbuf ||
-        !uA || !item_users || !item_user_beg)
+    if (!qb || !yj || !qlog || !lay || !totals || !p2stat || !hp || !ycbuf || !uA ||
+        !lay->perm || !lay->rpos || !lay->item_row_beg || !lay->users || !lay->item_user_beg)
         return set_err(MF_E_ARG, "null argument");
-    if (rec->pos0) return set_err(MF_E_UNSUPPORTED, "the fused fold is one rank's (pos0 = 0)");
+    const bool hot = lay->n_hot_pieces > 0;
+    if (hot && (!lay->hot_perm || !lay->hot_rpos || !lay->hot_users || !lay->hot_piece_beg ||
+                !lay->hot_piece_item || !lay->hot_item_piece_ptr || !lay->hot_sums ||
+                !lay->hot_piece_c || !lay->hot_piece_A))
+        return set_err(MF_E_ARG, "null hot-item argument");
     if (user_sq && (!stat_next || n_users < 0)) return set_err(MF_E_ARG, "user_sq needs stat_next");
-    if (stat_next && stat_next == rec->p2stat) return set_err(MF_E_ARG, "stat_next aliases p2stat");
+    if (stat_next && stat_next == p2stat) return set_err(MF_E_ARG, "stat_next aliases p2stat");
     if (n_items == 0) return 0;
-    Recency rc;
-    if (int e = make_recency(rec, hp, rc)) return e;
+    mf_recency_t cold_rec{lay->rpos, nullptr, totals, p2stat};
+    mf_recency_t hot_rec{lay->hot_rpos, nullptr, totals, p2stat};
+    Recency rc, rch;
+    if (int e = make_recency(&cold_rec, hp, rc)) return e;
+    if (int e = make_recency(&hot_rec, hp, rch)) return e;
     const int64_t cap = (int64_t)n_cus() * kFoldWPC;
     const int g = grid_for_waves(n_items < cap ? n_items : cap) + (stat_next ? 1 : 0);
+    const int gh = hot ? grid_for_waves(default_waves(lay->n_hot_pieces)) : 0;
     hipStream_t st = (hipStream_t)stream;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
+        // the hot items' pre-passes: piece sums of their gradient rows (log_reduce_kernel) and
+        // piece maps of their users' y updates (y_piece_kernel)
+        if (hot) {
+            int rc_g = dispatch_g<T>(ldq, [&](auto gc) -> int {
+                constexpr int V = decltype(gc)::value;
+                hipLaunchKernelGGL((log_reduce_kernel<T, V, true>), dim3(gh), dim3(kBlock), 0, st,
+                                   (const T *)qlog, ldq, n_factors + 1, lay->hot_perm,
+                                   lay->hot_piece_beg, lay->n_hot_pieces, (T *)lay->hot_sums,
+                                   (const int32_t *)nullptr, lay->hot_piece_item, rch, n_factors);
+                return check_launch("log_reduce_kernel");
+            });
+            if (rc_g) return rc_g;
+            int rc_y = dispatch_v<T>(ldu, [&](auto vc) -> int {
+                constexpr int V = decltype(vc)::value;
+                hipLaunchKernelGGL((y_piece_kernel<T, V>), dim3(gh), dim3(kBlock), 0, st, ldu,
+                                   n_factors, (const T *)ycbuf, (const T *)uA, lay->hot_users,
+                                   lay->hot_piece_beg, lay->n_hot_pieces, (T *)lay->hot_piece_c,
+                                   (T *)lay->hot_piece_A, (const int32_t *)nullptr,
+                                   (const int32_t *)nullptr, (T *)yj);
+                return check_launch("y_piece_kernel");
+            });
+            if (rc_y) return rc_y;
+        }
         return dispatch_v<T>(ldq, [&](auto vq) -> int {
             constexpr int VQ = decltype(vq)::value;
             return dispatch_v<T>(ldu, [&](auto vy) -> int {
@@ -4689,11 +4761,15 @@ int mf_svdpp_qlog_fold(void *qb, int32_t ldq, int32_t n_factors, void *yj, int32
                     return set_err(MF_E_UNSUPPORTED, "the fused fold: rows of <= 320 columns");
                 } else {
                     hipLaunchKernelGGL((qlog_fold_kernel<T, VQ, VY>), dim3(g), dim3(kBlock), 0, st,
-                                       (T *)qb, ldq, n_factors, (T *)yj, ldu, (const T *)qlog, perm,
-                                       item_row_beg, totals, rc, hp->lr_qi, hp->reg_qi, hp->lr_bi,
-                                       hp->reg_bi, (const T *)ycbuf, (const T *)uA, item_users,
-                                       item_user_beg, n_items, stat_next, user_sq, n_users,
-                                       n_factors);
+                                       (T *)qb, ldq, n_factors, (T *)yj, ldu, (const T *)qlog,
+                                       lay->perm, lay->item_row_beg, totals, rc, hp->lr_qi,
+                                       hp->reg_qi, hp->lr_bi, hp->reg_bi, (const T *)ycbuf,
+                                       (const T *)uA, lay->users, lay->item_user_beg, n_items,
+                                       stat_next, user_sq, n_users, n_factors,
+                                       (const T *)(hot ? lay->hot_sums : nullptr),
+                                       hot ? lay->hot_item_piece_ptr : nullptr,
+                                       (const T *)(hot ? lay->hot_piece_c : nullptr),
+                                       (const T *)(hot ? lay->hot_piece_A : nullptr));
                     return check_launch("qlog_fold_kernel");
                 }
             });

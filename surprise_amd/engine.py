@@ -131,6 +131,29 @@ def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS, local=Fals
     return perm, piece_beg.astype(np.int32), item_piece_ptr, counts.astype(np.int32)
 
 
+def qlog_fold_layout(counts, perm, rpos, users, hot_rows=PIECE_ROWS, piece_rows=PIECE_ROWS):
+    """mf_svdpp_qlog_fold's layout of one chunk (include/surprise_amd.h mf_qlog_fold_t) from the
+    q log's item-grouped positions: perm (log rows), rpos (each row's position among its item's)
+    and users (each row's rater), grouped by item with counts[i] rows.  Items of <= hot_rows rows
+    are cold (one wavefront takes their rows in turn); the others hot, cut into pieces of
+    <= piece_rows positions that the launch's pre-passes reduce first."""
+    counts = np.asarray(counts, np.int64)
+    n_items = len(counts)
+    hot = counts > hot_rows
+    at_hot = np.repeat(hot, counts)
+    pre = lambda c: np.concatenate([[0], np.cumsum(c)]).astype(np.int32)
+    cold_c, hot_c = np.where(hot, 0, counts), np.where(hot, counts, 0)
+    hipp, hpb = piece_bounds(np.concatenate([[0], np.cumsum(hot_c)]), hot_c, piece_rows)
+    return dict(perm=np.asarray(perm, np.int32)[~at_hot], rpos=np.asarray(rpos, np.int32)[~at_hot],
+                item_row_beg=pre(cold_c), users=np.asarray(users, np.int32)[~at_hot],
+                item_user_beg=pre(cold_c), hot_perm=np.asarray(perm, np.int32)[at_hot],
+                hot_rpos=np.asarray(rpos, np.int32)[at_hot],
+                hot_users=np.asarray(users, np.int32)[at_hot],
+                hot_piece_beg=hpb.astype(np.int32),
+                hot_piece_item=np.repeat(np.arange(n_items, dtype=np.int32), np.diff(hipp)),
+                hot_item_piece_ptr=hipp.astype(np.int32), n_hot_pieces=len(hpb) - 1)
+
+
 def chunk_log_rows(row_ptr, users):
     """First chunk-local log row of each of `users` (the SVD++ q log: a chunk's ratings numbered
     in ascending user order, as log_layout(local=True)): (sorted users, int64 rows)."""
@@ -434,7 +457,8 @@ class MFEngine(ItemSync, Predictor):
                       other user in schedule order), half A's epoch kernel first on the main
                       stream, then half B's epoch on the side stream beside A's log replay, then
                       B's replay -- the same arithmetic (the fold adds both halves' piece sums);
-                      None: on where a chunk holds >= STAGGER_MIN_NNZ ratings and no heavy split
+                      None / False: off (measured slower at C4: the concurrent replay's log
+                      stream evicts the epoch kernel's item rows from the MALL)
           fused       SVD++ q log on one rank: the chunk's fold in one pass over the items
                       (mf_svdpp_qlog_fold: the q gradients' weighted sums, the q step and the y
                       maps' composition together); False: mf_log_reduce + mf_log_apply +
@@ -582,9 +606,10 @@ class MFEngine(ItemSync, Predictor):
         _pu = []
         pos_user = lambda: _pu[0] if _pu else _pu.append(position_users(row_ptr)) or _pu[0]
         # stagger (large chunks): two halves, B's epoch beside A's replay
+        # (off by default: measured slower at C4 -- B's epoch beside A's replay 39.7 vs 29.6 ms
+        # per epoch in fp32, 70.3 vs 53.3 in fp64, profiles/r5d_c4_stagger.txt)
         if stagger is None:
-            stagger = (self.ckpt and heavy <= 0 and not self.deterministic and
-                       int(row_ptr[-1] - row_ptr[0]) >= self.n_chunks * self.STAGGER_MIN_NNZ)
+            stagger = False
         self.stagger = bool(stagger) and self.ckpt and heavy <= 0
         self.side = torch.cuda.Stream(device=dev) if self.ckpt and (heavy > 0 or self.stagger) \
             else None
@@ -652,8 +677,8 @@ class MFEngine(ItemSync, Predictor):
                     rp = kpos[perm] if kpos is not None else \
                         np.arange(len(perm), dtype=np.int64) - np.repeat(pb[ipp[:-1]], cnt)
                     lg["rpos"] = to_dev(rp.astype(np.int32))
-                if self.qlog_pp:  # (the fused fold: each item's range of perm)
-                    lg["irb"] = to_dev(pb[ipp].astype(np.int32))
+                if self.qlog_pp and self.recency:  # (the fused fold's layout: with y's below)
+                    lg["_fold_src"] = (cnt, perm, rp)
                 lgs.append(lg)
             main = lgs[0]
             main["heavy"] = lgs[1] if len(lgs) > 1 else None
@@ -708,10 +733,19 @@ class MFEngine(ItemSync, Predictor):
                 perm, pb, ipp, _ = log_layout(row_ptr, items, us.cpu().numpy(), self.n_items)
                 iusr = pos_user()[perm]
                 self.ycsc.append(dict(users=to_dev(iusr), pb=to_dev(pb), ipp=to_dev(ipp),
-                                      n_pieces=len(pb) - 1, iub=to_dev(pb[ipp].astype(np.int32)),
+                                      n_pieces=len(pb) - 1, _iusr=iusr,
                                       pitem=to_dev(np.repeat(np.arange(self.n_items,
                                                                        dtype=np.int32),
                                                              np.diff(ipp)))))
+            # the fused fold's per-chunk layout (q log, one rank): cold items' rows and raters
+            # listed directly, hot items' in pieces (qlog_fold_layout)
+            if self.qlog_pp and self.fused and self.recency:
+                for c, (lg, y) in enumerate(zip(self.logs, self.ycsc)):
+                    cnt, perm_c, rp = lg.pop("_fold_src")
+                    iusr_c = y.pop("_iusr")
+                    lay = qlog_fold_layout(cnt, perm_c, rp, iusr_c)
+                    lg["fold"] = {k: (to_dev(v) if isinstance(v, np.ndarray) else v)
+                                  for k, v in lay.items()}
             h = dict(hyper or {})
             decay = 1.0 - h.get("lr_yj", 0.0) * h.get("reg_yj", 0.0)
             # A_u = decay^{|I_u|} (the epoch kernel's per-user factor), fp64 on the host
@@ -746,8 +780,14 @@ class MFEngine(ItemSync, Predictor):
         self.yj = z(I, ld) if algo == "svdpp" else None
         self.ycbuf = z(U, ld) if self.ydefer else None
         if self.ydefer:
+            for y in self.ycsc:
+                y.pop("_iusr", None)
             n_pc = max(1, max(y["n_pieces"] for y in self.ycsc))
             self.ypc_c, self.ypc_A = z(n_pc, ld), z(n_pc)
+        self.fold_sums = None
+        if self.qlog_pp and self.fused and self.recency:  # (the fused fold's hot-piece scratch)
+            n_hp = max(1, max(lg["fold"]["n_hot_pieces"] for lg in self.logs))
+            self.fold_sums = z(n_hp, ldq)
         # every user row on the device belongs to this rank (a rank-local CSR)
         self.u_lo, self.u_hi = 0, self.n_users
         self.qlog = None
@@ -813,7 +853,6 @@ class MFEngine(ItemSync, Predictor):
     HEAVY_TOP_USERS = 0
     HEAVY_USERS_GRAM = 256  # ... with the blocked solve (one workgroup per user)
     HEAVY_MAX_NNZ = 8_000_000
-    STAGGER_MIN_NNZ = 8_000_000  # (chunks at least this large: two staggered halves)
 
     def _auto_heavy(self, row_ptr):
         """The heavy/light XCD split pays where the epoch is bound by its longest user chains:
@@ -1420,14 +1459,18 @@ class MFEngine(ItemSync, Predictor):
     def _merge_local(self):
         if self._fused_fold():
             c = getattr(self, "_chunk", 0)
-            lg, y = self.logs[c], self.ycsc[c]
-            rec = _lib.MfRecency(lg["rpos"].data_ptr(), None, self._totals()[c].data_ptr(),
-                                 self.work.data_ptr())
+            f = self.logs[c]["fold"]
+            p = lambda k: f[k].data_ptr()
+            lay = _lib.MfQlogFold(p("perm"), p("rpos"), p("item_row_beg"), p("users"),
+                                  p("item_user_beg"), p("hot_perm"), p("hot_rpos"),
+                                  p("hot_users"), p("hot_piece_beg"), p("hot_piece_item"),
+                                  p("hot_item_piece_ptr"), int(f["n_hot_pieces"]),
+                                  self.fold_sums.data_ptr(), self.ypc_c.data_ptr(),
+                                  self.ypc_A.data_ptr())
             _lib.call("mf_svdpp_qlog_fold", self._ptr(self.qb), self.ldq, self.K,
                       self._ptr(self.yj), self.ld, ctypes.c_void_p(self._qlog_base),
-                      self._ptr(lg["perm"]), self._ptr(lg["irb"]), self._ptr(self._totals()[c]),
-                      ctypes.byref(rec), ctypes.byref(self._hyper), self._ptr(self.ycbuf),
-                      self._ptr(self.uA), self._ptr(y["users"]), self._ptr(y["iub"]),
+                      ctypes.byref(lay), self._ptr(self._totals()[c]), self._ptr(self.work),
+                      ctypes.byref(self._hyper), self._ptr(self.ycbuf), self._ptr(self.uA),
                       self.n_items, *self._stat_args(True), self.dtype, self._st())
             return
         if self.is_log:

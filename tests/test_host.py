@@ -607,3 +607,37 @@ def test_default_dtype_is_fp64_up_to_the_fp64_row_limit():
     b = SVD(n_factors=10, dtype="float64")
     b.n_factors = 300
     assert not b._dtype_auto  # (an explicit dtype stays: fit then refuses 300 fp64 factors)
+
+
+def test_qlog_fold_layout_partitions_cold_and_hot_items():
+    """mf_svdpp_qlog_fold's layout (engine.qlog_fold_layout): every item-grouped position is
+    either a cold item's (listed directly, item_row_beg / item_user_beg ranges) or a hot item's
+    (more than hot_rows rows: pieces of <= 64 positions, each piece of one item, in order)."""
+    from surprise_amd.engine import qlog_fold_layout
+    rng = np.random.RandomState(5)
+    counts = rng.choice([0, 1, 3, 64, 65, 200, 700], size=40)
+    tot = int(counts.sum())
+    perm = rng.permutation(tot).astype(np.int32)
+    rpos = np.concatenate([np.arange(c) for c in counts]).astype(np.int32)
+    users = rng.randint(0, 1000, tot).astype(np.int32)
+    lay = qlog_fold_layout(counts, perm, rpos, users, hot_rows=64)
+    hot = counts > 64
+    assert lay["item_row_beg"][-1] + len(lay["hot_perm"]) == tot
+    np.testing.assert_array_equal(np.diff(lay["item_row_beg"]), np.where(hot, 0, counts))
+    np.testing.assert_array_equal(lay["item_row_beg"], lay["item_user_beg"])
+    np.testing.assert_array_equal(np.diff(lay["hot_item_piece_ptr"]), np.where(hot, -(-counts // 64), 0))
+    pb = lay["hot_piece_beg"]
+    assert pb[0] == 0 and pb[-1] == len(lay["hot_perm"]) and np.all(np.diff(pb) <= 64)
+    assert lay["n_hot_pieces"] == len(pb) - 1 == len(lay["hot_piece_item"])
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    for i in range(len(counts)):
+        rows = perm[offs[i]:offs[i + 1]]
+        if hot[i]:
+            p0, p1 = lay["hot_item_piece_ptr"][i], lay["hot_item_piece_ptr"][i + 1]
+            assert np.all(lay["hot_piece_item"][p0:p1] == i)
+            np.testing.assert_array_equal(lay["hot_perm"][pb[p0]:pb[p1]], rows)
+            np.testing.assert_array_equal(lay["hot_rpos"][pb[p0]:pb[p1]], np.arange(counts[i]))
+        else:
+            b0, b1 = lay["item_row_beg"][i], lay["item_row_beg"][i + 1]
+            np.testing.assert_array_equal(lay["perm"][b0:b1], rows)
+            np.testing.assert_array_equal(lay["users"][b0:b1], users[offs[i]:offs[i + 1]])
