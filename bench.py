@@ -124,6 +124,9 @@ def parse():
                         "after it; engine option qlog) instead of the float-atomic schedule")
     p.add_argument("--no-c4", action="store_true",
                    help="skip the C4 leg (BASELINE configs[3]'s shape on this GPU)")
+    p.add_argument("--light-replay-wpc", type=int, default=-1,
+                   help="split chunk: the light group's replay waves per CU (engine option "
+                        "light_replay_wpc; -1: the engine's default)")
     p.add_argument("--stagger", type=int, default=-1,
                    help="checkpoint log: the chunk's users in two staggered halves (engine option "
                         "stagger; -1: the engine's policy, 0 off, 1 on)")
@@ -754,7 +757,9 @@ def main():
                        **({"gram": bool(args.gram)} if args.gram >= 0 else {}),
                        **({"xcd_split": bool(args.xcd_split)} if args.xcd_split >= 0 else {}),
                        **({"long_chain": args.long_chain} if args.long_chain >= 0 else {}),
-                       **({"stagger": bool(args.stagger)} if args.stagger >= 0 else {}))
+                       **({"stagger": bool(args.stagger)} if args.stagger >= 0 else {}),
+                       **({"light_replay_wpc": args.light_replay_wpc}
+                          if args.light_replay_wpc >= 0 else {}))
         eng.set_factors(pu, qi, yj=yj)
         eng._prepare(ctx)  # global per-item counts (all ranks)
         return eng

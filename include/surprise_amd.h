@@ -121,6 +121,8 @@ typedef struct mf_csr {
  * mf_log_replay with the same flag reads them so (the bias column's gradient, err_k * 1, is
  * summed from the errors). */
 #define MF_EPOCH_CKPT_NARROW 16
+/* mf_log_replay flags bits 16..23: the launch's waves per CU (0: the default, 16) */
+#define MF_REPLAY_WPC_SHIFT 16
 int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu, void *bu,
                  int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
                  const mf_hyper_t *hp, int32_t mode, void *qlog, void *elog, int32_t n_waves,
@@ -241,8 +243,10 @@ int mf_log_reduce(const void *qlog, int32_t ld, int32_t n_cols, const int32_t *p
  * p_k = (row - err_k * lr_pu * q_{item(k)}) / ap (ap = 1 - lr_pu * reg_pu on factor columns;
  * q from the snapshot table qb; every rating of a piece has the same item) -- call it before
  * mf_log_apply.  piece_item (nullable): the item of each piece (else read through perm and the
- * CSR items).  Requires ldq * sizeof(dtype) <= 1 KiB.  flags: bits 8..15 an XCD mask as in
- * mf_svd_epoch (MF_EPOCH_XCD_SHIFT), 0 = every XCD; MF_EPOCH_ERR_IN_ROW: errors in the rows;
+ * CSR items).  Requires ldq * sizeof(dtype) <= 1 KiB (narrow rows: their n_factors columns
+ * <= 1 KiB, ldq <= 1.5 KiB -- fp64 K = 128).  flags: bits 8..15 an XCD mask as in
+ * mf_svd_epoch (MF_EPOCH_XCD_SHIFT), 0 = every XCD; bits 16..23 the launch's waves per CU
+ * (MF_REPLAY_WPC_SHIFT; 0 = 16); MF_EPOCH_ERR_IN_ROW: errors in the rows;
  * MF_EPOCH_CKPT_NARROW: narrow checkpoint rows.  Unlike mf_log_reduce, a piece may hold any
  * number >= 1 of ratings (of one item): longer pieces mean fewer sums rows for mf_log_apply.
  * rec (nullable): each gradient err_k * p_k weighted by its recency weight (mf_recency_t).

@@ -4637,7 +4637,9 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
         return set_err(MF_E_UNSUPPORTED, "checkpoint log: ldq * size <= 1 KiB (narrow rows: ldc) only");
     Recency rc;
     if (int e = make_recency(rec, hp, rc)) return e;
-    const int64_t cap = (int64_t)n_cus() * MF_REPLAY_WPC * (xmask ? __builtin_popcount(xmask) : 8) / 8;
+    const int wpc = (flags >> MF_REPLAY_WPC_SHIFT) & 0xFF;
+    const int64_t cap = (int64_t)n_cus() * (wpc ? wpc : MF_REPLAY_WPC) *
+                        (xmask ? __builtin_popcount(xmask) : 8) / 8;
     const int g = grid_for_waves_x(n_pieces < 1 ? 1 : n_pieces < cap ? n_pieces : cap, xmask);
     hipStream_t st = (hipStream_t)stream;
     auto run = [&](auto tag_t) -> int {

@@ -408,7 +408,8 @@ class MFEngine(ItemSync, Predictor):
                  join="event",
                  helpers=None, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
                  replay_rows=None, gram=None, xcd_split=None, qlog=None, top=None,
-                 exchange=None, long_chain=256, overlap_q=True, fused=True, stagger=None):
+                 exchange=None, long_chain=256, overlap_q=True, fused=True, stagger=None,
+                 light_replay_wpc=0):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -459,6 +460,9 @@ class MFEngine(ItemSync, Predictor):
                       B's replay -- the same arithmetic (the fold adds both halves' piece sums);
                       None / False: off (measured slower at C4: the concurrent replay's log
                       stream evicts the epoch kernel's item rows from the MALL)
+          light_replay_wpc  split chunk: the light group's log replay at this many waves per
+                      CU (0: the library's 16) -- fewer leave the heavy chains' memory path
+                      quieter while the replay still ends before them
           fused       SVD++ q log on one rank: the chunk's fold in one pass over the items
                       (mf_svdpp_qlog_fold: the q gradients' weighted sums, the q step and the y
                       maps' composition together); False: mf_log_reduce + mf_log_apply +
@@ -523,6 +527,7 @@ class MFEngine(ItemSync, Predictor):
         self.world = int(world)
         self.multi = self.world > 1 or bool(exchange)  # (the exchange path's tables and rules)
         self.fused = bool(fused)
+        self.light_replay_wpc = int(light_replay_wpc)  # (split chunk: the light replay's waves/CU)
         self.overlap_q = bool(overlap_q)
         self._q_work = None
         if merge not in ("count", "recency", "sum"):
@@ -1175,7 +1180,7 @@ class MFEngine(ItemSync, Predictor):
                 _lib.call("mf_launch_join", self._ptr(jw), 1, self._join_epoch)
             elif self._nev is not None:
                 _lib.call("mf_launch_event", self._nev["join"])  # completed by the light replay
-            self._reduce_log(lg, self.sums.data_ptr(), sh, lx)
+            self._reduce_log(lg, self.sums.data_ptr(), sh, lx, self.light_replay_wpc)
             if jw is None and self._nev is None:
                 self._ev_record("join", side)
             # (the heavy replay starts when the longest chain ends: by then the light users'
@@ -1289,9 +1294,10 @@ class MFEngine(ItemSync, Predictor):
     def _ev_wait(self, stream, name):
         stream.wait_event(self._events[name])
 
-    def _reduce_log(self, lg, sums_ptr, st, xmask=0):
+    def _reduce_log(self, lg, sums_ptr, st, xmask=0, wpc=0):
         """Piece sums of one user group's log: mf_log_replay (checkpoint form) or mf_log_reduce.
-        xmask: run on those XCDs only (bit x: XCD x; 0: all)."""
+        xmask: run on those XCDs only (bit x: XCD x; 0: all); wpc: the replay's waves per CU
+        (0: the library's default)."""
         rec = self._recency_args(lg)
         if self.ckpt:
             _lib.call("mf_log_replay", ctypes.c_void_p(self._qlog_base),
@@ -1299,7 +1305,7 @@ class MFEngine(ItemSync, Predictor):
                       self._ptr(self.qb), ctypes.byref(self._hyper), self._ptr(lg["perm"]),
                       self._ptr(lg["ck"]), self._ptr(lg["pb"]), lg["n_pieces"],
                       ctypes.c_void_p(sums_ptr), self._ptr(lg["pitem"]), rec,
-                      (xmask << _lib.MF_EPOCH_XCD_SHIFT) |
+                      (xmask << _lib.MF_EPOCH_XCD_SHIFT) | (int(wpc) << _lib.MF_REPLAY_WPC_SHIFT) |
                       (_lib.MF_EPOCH_ERR_IN_ROW if self.err_in_row else 0) |
                       (_lib.MF_EPOCH_CKPT_NARROW if self.narrow else 0), self.dtype, st)
         else:
