@@ -897,6 +897,9 @@ constexpr int kLaMaxG = MF_LA_MAX_G;
 #ifndef MF_LA_BANK
 #define MF_LA_BANK 8  // ratings per bank in the lookahead body (two banks alternate)
 #endif
+#ifndef MF_LA_IDS_AHEAD
+#define MF_LA_IDS_AHEAD 2  // the SVD lookahead body loads a bank's item ids this many banks ahead
+#endif
 #ifndef MF_LOG_AUX
 #define MF_LOG_AUX 0  // cache policy of the lookahead body's log stores
 #endif
@@ -979,6 +982,8 @@ __device__ __forceinline__ void epoch_body_la(
     // kernel at C4 19.7 -> 18.9 ms, profiles/r4q_bank_sweep.txt; banks of 4: 25.0)
     constexpr int kB = SB ? MF_LA_BANK_SB : (G == 1 ? MF_LA_BANK : MF_LA_BANK_G2);
     static_assert(!CK || (kB % kCkpt == 0 && kB <= kWave), "checkpoints: whole banks");
+    constexpr int kAhead = MF_LA_IDS_AHEAD;  // banks between a bank's id loads and its gathers
+    static_assert(kAhead >= 2, "the next bank's ids are loaded before its rows");
     const int lane = threadIdx.x & (kWave - 1);
     int64_t wave, grid_waves;
     if (!wave_slot(xmask, wave, grid_waves)) return;
@@ -1071,8 +1076,10 @@ __device__ __forceinline__ void epoch_body_la(
         constexpr int kLg = CK ? kB / kCkpt : kB;
         vec lg[kLg][G];
         T ev = T(0);
-        uint32_t go_n1, go_n2;
-        T gr_n1, gr_n2;
+        // ids / ratings of the next kAhead - 1 banks (bank j0 + kB .. j0 + (kAhead - 1) kB), their
+        // loads issued kAhead - 1 banks before the bank's row gathers need them
+        uint32_t go_q[kAhead - 1];
+        T gr_q[kAhead - 1];
         auto fill = [&](const int bk, const uint32_t go, const T gr) {
 #pragma unroll
             for (int d = 0; d < kB; ++d) {
@@ -1110,8 +1117,9 @@ __device__ __forceinline__ void epoch_body_la(
             uint32_t go0;
             T gr0;
             grp_load(0, go0, gr0);
-            grp_load(kB, go_n1, gr_n1);
-            asm volatile("" ::"v"(go0), "v"(gr0), "v"(go_n1), "v"(gr_n1));
+#pragma unroll
+            for (int a = 0; a < kAhead - 1; ++a) grp_load((a + 1) * kB, go_q[a], gr_q[a]);
+            asm volatile("" ::"v"(go0), "v"(gr0), "v"(go_q[0]), "v"(gr_q[0]));
             __builtin_amdgcn_sched_barrier(0);
             fill(0, go0, gr0);
         }
@@ -1194,13 +1202,20 @@ __device__ __forceinline__ void epoch_body_la(
         // one full bank: ratings j0 .. j0 + kB - 1 in bank bk (FIRST: nothing to flush yet)
         auto full_bank = [&](auto bank_c, auto first_c) {
             constexpr int bk = decltype(bank_c)::value;
-            grp_load(j0 + 2 * kB, go_n2, gr_n2);
+            uint32_t go_new;
+            T gr_new;
+            grp_load(j0 + kAhead * kB, go_new, gr_new);
             asm volatile("" ::: "memory");  // issue order: ids, rows, then the stores
-            fill(bk ^ 1, go_n1, gr_n1);
+            fill(bk ^ 1, go_q[0], gr_q[0]);
             asm volatile("" ::: "memory");
             if (!decltype(first_c)::value) flush(j0 - kB);
-            go_n1 = go_n2;
-            gr_n1 = gr_n2;
+#pragma unroll
+            for (int a = 0; a + 1 < kAhead - 1; ++a) {
+                go_q[a] = go_q[a + 1];
+                gr_q[a] = gr_q[a + 1];
+            }
+            go_q[kAhead - 2] = go_new;
+            gr_q[kAhead - 2] = gr_new;
 #pragma unroll
             for (int d = 0; d < kB; ++d) step(std::true_type{}, bank_c, j0, d);
             j0 += kB;
