@@ -306,9 +306,9 @@ int mf_ckpt_interval(void);
 typedef struct mf_qlog_fold {
     const int32_t *perm;          /* cold items' log rows, by item                               */
     const int32_t *rpos;          /* [perm entries] the row's position among its item's rows     */
-    const int32_t *item_row_beg;  /* [n_items + 1] item i's cold rows: perm[beg[i] .. beg[i+1]) */
-    const int32_t *users;         /* cold items' raters (CSR order within an item)              */
-    const int32_t *item_user_beg; /* [n_items + 1] item i's cold raters                         */
+    const int32_t *item_row_beg;  /* [n_items + 1] item i's cold rows: perm[beg[i] .. beg[i+1]),
+                                     at most 64 of them                                         */
+    const int32_t *users;         /* [perm entries] each cold row's rater (CSR order)           */
     const int32_t *hot_perm, *hot_rpos, *hot_users;  /* hot items' rows / positions / raters     */
     const int32_t *hot_piece_beg;       /* [n_hot_pieces + 1] pieces of <= 64 hot positions     */
     const int32_t *hot_piece_item;      /* [n_hot_pieces] each piece's item                     */

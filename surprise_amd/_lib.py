@@ -57,7 +57,7 @@ class MfRecency(ctypes.Structure):
 
 class MfQlogFold(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
-        "perm", "rpos", "item_row_beg", "users", "item_user_beg", "hot_perm", "hot_rpos",
+        "perm", "rpos", "item_row_beg", "users", "hot_perm", "hot_rpos",
         "hot_users", "hot_piece_beg", "hot_piece_item", "hot_item_piece_ptr")] + \
         [("n_hot_pieces", ctypes.c_int64)] + \
         [(n, ctypes.c_void_p) for n in ("hot_sums", "hot_piece_c", "hot_piece_A")]

@@ -3863,7 +3863,7 @@ __global__ __launch_bounds__(kBlock) void y_apply_kernel(
 // item_row_beg[i] .. item_row_beg[i+1] of perm, users in order) summed with their recency weights
 // (1 - eta)^(N - 1 - pos) (log_reduce_kernel's weights), then q += lr (S - w N reg q) -- what
 // mf_log_reduce + mf_log_apply compute; (2) its y row composed with the chunk's users' affine
-// maps y <- A_u y + c_u in CSR order (positions item_user_beg[i] .. of item_users) -- what
+// maps y <- A_u y + c_u in CSR order (the raters of the same positions, item_users) -- what
 // mf_svdpp_y_fold computes.  Nothing round-trips through piece sums; every load is a row gather
 // whose indices come from ONE coalesced vector load per 64 rows, so a wave keeps kF rows in
 // flight per part and the launch's occupancy (kFoldWPC waves per CU) hides the rest of the
@@ -3877,9 +3877,8 @@ __global__ __launch_bounds__(kBlock) void qlog_fold_kernel(
     const int32_t *__restrict__ perm, const int32_t *__restrict__ item_row_beg,
     const int32_t *__restrict__ totals, Recency rc, double lr_f, double reg_f, double lr_b,
     double reg_b, const T *__restrict__ ycbuf, const T *__restrict__ uA,
-    const int32_t *__restrict__ item_users, const int32_t *__restrict__ item_user_beg,
-    int n_items, double *__restrict__ stat_next, const double *__restrict__ user_sq,
-    int64_t n_sq, int sq_cols, const T *__restrict__ hot_sums,
+    const int32_t *__restrict__ item_users, int n_items, double *__restrict__ stat_next,
+    const double *__restrict__ user_sq, int64_t n_sq, int sq_cols, const T *__restrict__ hot_sums,
     const int32_t *__restrict__ hot_item_piece_ptr, const T *__restrict__ hot_pc_c,
     const T *__restrict__ hot_pc_A)
 {
@@ -3898,135 +3897,142 @@ __global__ __launch_bounds__(kBlock) void qlog_fold_kernel(
     const double n_p2 = rc.p2stat[1];
     const double eta_f = rc.lr_qi * ((n_p2 > 0 ? rc.p2stat[0] / n_p2 : 0.0) + rc.reg_qi);
     const double eta_b = rc.eta_b;
-    for (int64_t i = wave; i < n_items; i += n_waves) {
-        const int r0 = item_row_beg[i], r1 = item_row_beg[i + 1];
-        const int u0 = item_user_beg[i], u1 = item_user_beg[i + 1];
-        // a hot item (more rows than one wave takes in turn): its rows already summed per piece
-        // and its users' maps composed per piece by the launch's two pre-passes
-        const int h0 = hot_item_piece_ptr ? hot_item_piece_ptr[i] : 0;
-        const int h1 = hot_item_piece_ptr ? hot_item_piece_ptr[i + 1] : 0;
-        if (r0 == r1 && u0 == u1 && h0 == h1) continue;  // (untouched this chunk)
-        const int N = totals[i];
-        T q[VQ], y[VY], acc[VQ];
-#pragma unroll
-        for (int v = 0; v < VQ; ++v) {
-            const int c = lane + kWave * v;
-            q[v] = c < ldq ? qb[i * ldq + c] : T(0);
-            acc[v] = T(0);
-        }
-#pragma unroll
-        for (int v = 0; v < VY; ++v) {
-            const int c = lane + kWave * v;
-            y[v] = c < K ? yj[i * ldu + c] : T(0);
-        }
-        // (1) the weighted sum of the item's gradient rows, 64 row indices per vector load
-        for (int x0 = r0; x0 < r1; x0 += kWave) {
-            const int cnt = r1 - x0 < kWave ? r1 - x0 : kWave;
-            const int xl = x0 + (lane < cnt ? lane : cnt - 1);
-            const int k_l = perm[xl];
-            const double back = (double)(N - 1 - rc.rpos[xl] - (rc.pos0 ? rc.pos0[i] : 0));
-            const T wf_l = lane < cnt ? (T)exp(back * l_q) : T(0);
-            const T wb_l = lane < cnt ? (T)exp(back * l_b) : T(0);
-            for (int a0 = 0; a0 < cnt; a0 += kFoldF) {
-                T g[kFoldF][VQ];
-#pragma unroll
-                for (int a = 0; a < kFoldF; ++a) {
-                    const int x = a0 + a < cnt ? a0 + a : cnt - 1;
-                    const T *row = qlog + (int64_t)readlane(k_l, x) * ldq;
-#pragma unroll
-                    for (int v = 0; v < VQ; ++v) {
-                        const int c = lane + kWave * v;
-                        g[a][v] = c <= K ? row[c] : T(0);
-                    }
-                }
-#pragma unroll
-                for (int a = 0; a < kFoldF; ++a) {
-                    const int x = a0 + a < kWave ? a0 + a : kWave - 1;
-                    const T wf = readlane(wf_l, x), wb = readlane(wb_l, x);  // (0 past cnt)
-#pragma unroll
-                    for (int v = 0; v < VQ; ++v)
-                        acc[v] += (lane + kWave * v == K ? wb : wf) * g[a][v];
-                }
-            }
-        }
-        // (1') a hot item: its pieces' weighted sums, kFoldF pieces in flight
-        for (int p0 = h0; p0 < h1; p0 += kFoldF) {
-            T g[kFoldF][VQ];
-#pragma unroll
-            for (int a = 0; a < kFoldF; ++a) {
-                const bool ok = p0 + a < h1;
-                const T *row = hot_sums + (int64_t)(ok ? p0 + a : h0) * ldq;
+    // items in batches of 64, batch b = items b + NB t (t < 64): the most-rated (lowest-id)
+    // items land in different batches, so no wave takes several hot items in a row
+    const int64_t NB = (n_items + kWave - 1) / kWave;
+    for (int64_t b = wave; b < NB; b += n_waves) {
+        // lane t: item b + NB t's cold row range (one piece: <= 64 rows), hot piece range, N
+        const int64_t it_l = b + NB * lane;
+        const bool in_l = it_l < n_items;
+        const int r0_l = in_l ? item_row_beg[it_l] : 0, r1_l = in_l ? item_row_beg[it_l + 1] : 0;
+        const int h0_l = in_l && hot_item_piece_ptr ? hot_item_piece_ptr[it_l] : 0;
+        const int h1_l = in_l && hot_item_piece_ptr ? hot_item_piece_ptr[it_l + 1] : 0;
+        const int N_l = in_l ? totals[it_l] : 0;
+        // the cold rows' indices of item t (lane x: row x), loaded one item ahead of its gathers
+        auto vload = [&](const int t, int &k_l, int &u_l, T &wf_l, T &wb_l, T &A_l) {
+            const int r0 = readlane(r0_l, t), cnt = readlane(r1_l, t) - r0;
+            const int N = readlane(N_l, t);
+            const int xl = r0 + (lane < cnt ? lane : (cnt > 0 ? cnt - 1 : 0));
+            const bool ok = lane < cnt;
+            k_l = cnt > 0 ? perm[xl] : 0;
+            u_l = cnt > 0 ? item_users[xl] : 0;
+            const double back = (double)(N - 1 - (cnt > 0 ? rc.rpos[xl] : 0));
+            wf_l = ok ? (T)exp(back * l_q) : T(0);
+            wb_l = ok ? (T)exp(back * l_b) : T(0);
+            A_l = cnt > 0 ? uA[u_l] : T(1);
+        };
+        int k_c, u_c;
+        T wf_c, wb_c, A_c;
+        vload(0, k_c, u_c, wf_c, wb_c, A_c);
+        for (int t = 0; t < kWave; ++t) {
+            const int64_t i = b + NB * t;
+            if (i >= n_items) break;  // (uniform)
+            int k_n = 0, u_n = 0;
+            T wf_n = T(0), wb_n = T(0), A_n = T(1);
+            if (t + 1 < kWave && i + NB < n_items) vload(t + 1, k_n, u_n, wf_n, wb_n, A_n);
+            const int cnt = readlane(r1_l, t) - readlane(r0_l, t);
+            const int h0 = readlane(h0_l, t), h1 = readlane(h1_l, t);
+            if (cnt > 0 || h0 < h1) {
+                const int N = readlane(N_l, t);
+                T q[VQ], y[VY], acc[VQ];
 #pragma unroll
                 for (int v = 0; v < VQ; ++v) {
                     const int c = lane + kWave * v;
-                    g[a][v] = ok && c <= K ? row[c] : T(0);
+                    q[v] = c < ldq ? qb[i * ldq + c] : T(0);
+                    acc[v] = T(0);
                 }
-            }
-#pragma unroll
-            for (int a = 0; a < kFoldF; ++a)
-#pragma unroll
-                for (int v = 0; v < VQ; ++v) acc[v] += g[a][v];
-        }
-        // (2') a hot item's y: its pieces' composed maps in piece (user) order
-        for (int p0 = h0; p0 < h1; p0 += kFoldF) {
-            T g[kFoldF][VY], A[kFoldF];
-#pragma unroll
-            for (int a = 0; a < kFoldF; ++a) {
-                const bool ok = p0 + a < h1;
-                A[a] = ok ? hot_pc_A[p0 + a] : T(1);  // (past the item: the identity map)
 #pragma unroll
                 for (int v = 0; v < VY; ++v) {
                     const int c = lane + kWave * v;
-                    g[a][v] = ok && c < K ? hot_pc_c[(int64_t)(p0 + a) * ldu + c] : T(0);
+                    y[v] = c < K ? yj[i * ldu + c] : T(0);
                 }
-            }
+                // (1 + 2) a cold item: its gradient rows and its raters' c_u rows together,
+                // kFoldF of each in flight
+                for (int a0 = 0; a0 < cnt; a0 += kFoldF) {
+                    T g[kFoldF][VQ], gy[kFoldF][VY];
 #pragma unroll
-            for (int a = 0; a < kFoldF; ++a)
+                    for (int a = 0; a < kFoldF; ++a) {
+                        const int x = a0 + a < cnt ? a0 + a : cnt - 1;
+                        const T *row = qlog + (int64_t)readlane(k_c, x) * ldq;
+                        const T *yrow = ycbuf + (int64_t)readlane(u_c, x) * ldu;
 #pragma unroll
-                for (int v = 0; v < VY; ++v) y[v] = A[a] * y[v] + g[a][v];
-        }
-        // (2) y: the chunk's users' maps in CSR order, 64 users per vector load
-        for (int x0 = u0; x0 < u1; x0 += kWave) {
-            const int cnt = u1 - x0 < kWave ? u1 - x0 : kWave;
-            const int u_l = item_users[x0 + (lane < cnt ? lane : cnt - 1)];
-            const T A_l = uA[u_l];
-            for (int a0 = 0; a0 < cnt; a0 += kFoldF) {
-                T g[kFoldF][VY];
+                        for (int v = 0; v < VQ; ++v) {
+                            const int c = lane + kWave * v;
+                            g[a][v] = c <= K ? row[c] : T(0);
+                        }
 #pragma unroll
-                for (int a = 0; a < kFoldF; ++a) {
-                    const int x = a0 + a < cnt ? a0 + a : cnt - 1;
-                    const T *row = ycbuf + (int64_t)readlane(u_l, x) * ldu;
+                        for (int v = 0; v < VY; ++v) {
+                            const int c = lane + kWave * v;
+                            gy[a][v] = c < K ? yrow[c] : T(0);
+                        }
+                    }
 #pragma unroll
-                    for (int v = 0; v < VY; ++v) {
-                        const int c = lane + kWave * v;
-                        g[a][v] = c < K ? row[c] : T(0);
+                    for (int a = 0; a < kFoldF; ++a) {
+                        const int x = a0 + a < kWave ? a0 + a : kWave - 1;
+                        const T wf = readlane(wf_c, x), wb = readlane(wb_c, x);  // (0 past cnt)
+#pragma unroll
+                        for (int v = 0; v < VQ; ++v)
+                            acc[v] += (lane + kWave * v == K ? wb : wf) * g[a][v];
+                    }
+#pragma unroll
+                    for (int a = 0; a < kFoldF; ++a) {
+                        if (a0 + a >= cnt) break;  // (uniform)
+                        const T A = readlane(A_c, a0 + a);
+#pragma unroll
+                        for (int v = 0; v < VY; ++v) y[v] = A * y[v] + gy[a][v];
+                    }
+                }
+                // (1' + 2') a hot item: its pieces' weighted sums and composed maps, in order
+                for (int p0 = h0; p0 < h1; p0 += kFoldF) {
+                    T g[kFoldF][VQ], gy[kFoldF][VY], A[kFoldF];
+#pragma unroll
+                    for (int a = 0; a < kFoldF; ++a) {
+                        const bool ok = p0 + a < h1;
+                        const int64_t p = ok ? p0 + a : h0;
+                        A[a] = ok ? hot_pc_A[p] : T(1);  // (past the item: the identity map)
+#pragma unroll
+                        for (int v = 0; v < VQ; ++v) {
+                            const int c = lane + kWave * v;
+                            g[a][v] = ok && c <= K ? hot_sums[p * ldq + c] : T(0);
+                        }
+#pragma unroll
+                        for (int v = 0; v < VY; ++v) {
+                            const int c = lane + kWave * v;
+                            gy[a][v] = ok && c < K ? hot_pc_c[p * ldu + c] : T(0);
+                        }
+                    }
+#pragma unroll
+                    for (int a = 0; a < kFoldF; ++a) {
+#pragma unroll
+                        for (int v = 0; v < VQ; ++v) acc[v] += g[a][v];
+#pragma unroll
+                        for (int v = 0; v < VY; ++v) y[v] = A[a] * y[v] + gy[a][v];
+                    }
+                }
+                // q += lr (S - w N reg q), w N = sum_k (1 - eta)^(N-1-k) (mf_log_apply's rule)
+                const double wn_f = N > 1 ? -expm1(N * l_q) / eta_f : (double)N;
+                const double wn_b = N > 1 ? -expm1(N * l_b) / eta_b : (double)N;
+#pragma unroll
+                for (int v = 0; v < VQ; ++v) {
+                    const int c = lane + kWave * v;
+                    if (c <= K) {
+                        const bool bc = c == K;
+                        qb[i * ldq + c] = q[v] + (T)(bc ? lr_b : lr_f) *
+                                                     (acc[v] - (T)(bc ? wn_b : wn_f) *
+                                                                   (T)(bc ? reg_b : reg_f) * q[v]);
                     }
                 }
 #pragma unroll
-                for (int a = 0; a < kFoldF; ++a) {
-                    if (a0 + a >= cnt) break;  // (uniform)
-                    const T A = readlane(A_l, a0 + a);
-#pragma unroll
-                    for (int v = 0; v < VY; ++v) y[v] = A * y[v] + g[a][v];
+                for (int v = 0; v < VY; ++v) {
+                    const int c = lane + kWave * v;
+                    if (c < K) yj[i * ldu + c] = y[v];
                 }
             }
-        }
-        // q += lr (S - w N reg q), w N = sum_k (1 - eta)^(N-1-k) (mf_log_apply's recency rule)
-        const double wn_f = N > 1 ? -expm1(N * l_q) / eta_f : (double)N;
-        const double wn_b = N > 1 ? -expm1(N * l_b) / eta_b : (double)N;
-#pragma unroll
-        for (int v = 0; v < VQ; ++v) {
-            const int c = lane + kWave * v;
-            if (c <= K) {
-                const bool b = c == K;
-                qb[i * ldq + c] = q[v] + (T)(b ? lr_b : lr_f) *
-                                             (acc[v] - (T)(b ? wn_b : wn_f) * (T)(b ? reg_b : reg_f) * q[v]);
-            }
-        }
-#pragma unroll
-        for (int v = 0; v < VY; ++v) {
-            const int c = lane + kWave * v;
-            if (c < K) yj[i * ldu + c] = y[v];
+            k_c = k_n;
+            u_c = u_n;
+            wf_c = wf_n;
+            wb_c = wb_n;
+            A_c = A_n;
         }
     }
 }
@@ -4726,7 +4732,7 @@ int mf_svdpp_qlog_fold(void *qb, int32_t ldq, int32_t n_factors, void *yj, int32
     if (n_items < 0 || n_factors < 1 || ldq < n_factors + 1 || ldu < n_factors)
         return set_err(MF_E_ARG, "bad shape");
     if (!qb || !yj || !qlog || !lay || !totals || !p2stat || !hp || !ycbuf || !uA ||
-        !lay->perm || !lay->rpos || !lay->item_row_beg || !lay->users || !lay->item_user_beg)
+        !lay->perm || !lay->rpos || !lay->item_row_beg || !lay->users)
         return set_err(MF_E_ARG, "null argument");
     const bool hot = lay->n_hot_pieces > 0;
     if (hot && (!lay->hot_perm || !lay->hot_rpos || !lay->hot_users || !lay->hot_piece_beg ||
@@ -4740,9 +4746,12 @@ int mf_svdpp_qlog_fold(void *qb, int32_t ldq, int32_t n_factors, void *yj, int32
     mf_recency_t hot_rec{lay->hot_rpos, nullptr, totals, p2stat};
     Recency rc, rch;
     if (int e = make_recency(&cold_rec, hp, rc)) return e;
-    if (int e = make_recency(&hot_rec, hp, rch)) return e;
-    const int64_t cap = (int64_t)n_cus() * kFoldWPC;
-    const int g = grid_for_waves(n_items < cap ? n_items : cap) + (stat_next ? 1 : 0);
+    if (hot) {
+        if (int e = make_recency(&hot_rec, hp, rch)) return e;
+    }
+    // (waves take batches of 64 items)
+    const int64_t nb = ((int64_t)n_items + kWave - 1) / kWave, cap = (int64_t)n_cus() * kFoldWPC;
+    const int g = grid_for_waves(nb < cap ? nb : cap) + (stat_next ? 1 : 0);
     const int gh = hot ? grid_for_waves(default_waves(lay->n_hot_pieces)) : 0;
     hipStream_t st = (hipStream_t)stream;
     auto run = [&](auto tag_t) -> int {
@@ -4781,7 +4790,7 @@ int mf_svdpp_qlog_fold(void *qb, int32_t ldq, int32_t n_factors, void *yj, int32
                                        (T *)qb, ldq, n_factors, (T *)yj, ldu, (const T *)qlog,
                                        lay->perm, lay->item_row_beg, totals, rc, hp->lr_qi,
                                        hp->reg_qi, hp->lr_bi, hp->reg_bi, (const T *)ycbuf,
-                                       (const T *)uA, lay->users, lay->item_user_beg, n_items,
+                                       (const T *)uA, lay->users, n_items,
                                        stat_next, user_sq, n_users, n_factors,
                                        (const T *)(hot ? lay->hot_sums : nullptr),
                                        hot ? lay->hot_item_piece_ptr : nullptr,

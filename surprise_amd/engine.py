@@ -137,6 +137,7 @@ def qlog_fold_layout(counts, perm, rpos, users, hot_rows=PIECE_ROWS, piece_rows=
     and users (each row's rater), grouped by item with counts[i] rows.  Items of <= hot_rows rows
     are cold (one wavefront takes their rows in turn); the others hot, cut into pieces of
     <= piece_rows positions that the launch's pre-passes reduce first."""
+    assert hot_rows <= 64, "a cold item's rows are taken in one 64-lane vector load"
     counts = np.asarray(counts, np.int64)
     n_items = len(counts)
     hot = counts > hot_rows
@@ -146,7 +147,7 @@ def qlog_fold_layout(counts, perm, rpos, users, hot_rows=PIECE_ROWS, piece_rows=
     hipp, hpb = piece_bounds(np.concatenate([[0], np.cumsum(hot_c)]), hot_c, piece_rows)
     return dict(perm=np.asarray(perm, np.int32)[~at_hot], rpos=np.asarray(rpos, np.int32)[~at_hot],
                 item_row_beg=pre(cold_c), users=np.asarray(users, np.int32)[~at_hot],
-                item_user_beg=pre(cold_c), hot_perm=np.asarray(perm, np.int32)[at_hot],
+                hot_perm=np.asarray(perm, np.int32)[at_hot],
                 hot_rpos=np.asarray(rpos, np.int32)[at_hot],
                 hot_users=np.asarray(users, np.int32)[at_hot],
                 hot_piece_beg=hpb.astype(np.int32),
@@ -749,7 +750,10 @@ class MFEngine(ItemSync, Predictor):
                     cnt, perm_c, rp = lg.pop("_fold_src")
                     iusr_c = y.pop("_iusr")
                     lay = qlog_fold_layout(cnt, perm_c, rp, iusr_c)
-                    lg["fold"] = {k: (to_dev(v) if isinstance(v, np.ndarray) else v)
+                    # (empty arrays padded to one entry: the kernel never reads past a range,
+                    # and a null pointer would be refused)
+                    lg["fold"] = {k: (to_dev(v if len(v) else np.zeros(1, v.dtype))
+                                      if isinstance(v, np.ndarray) else v)
                                   for k, v in lay.items()}
             h = dict(hyper or {})
             decay = 1.0 - h.get("lr_yj", 0.0) * h.get("reg_yj", 0.0)
@@ -1468,7 +1472,7 @@ class MFEngine(ItemSync, Predictor):
             f = self.logs[c]["fold"]
             p = lambda k: f[k].data_ptr()
             lay = _lib.MfQlogFold(p("perm"), p("rpos"), p("item_row_beg"), p("users"),
-                                  p("item_user_beg"), p("hot_perm"), p("hot_rpos"),
+                                  p("hot_perm"), p("hot_rpos"),
                                   p("hot_users"), p("hot_piece_beg"), p("hot_piece_item"),
                                   p("hot_item_piece_ptr"), int(f["n_hot_pieces"]),
                                   self.fold_sums.data_ptr(), self.ypc_c.data_ptr(),

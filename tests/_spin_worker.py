@@ -22,6 +22,7 @@ def dispatch_case(out):
     from surprise_amd.trainset import Trainset
     u, i, r = shape("ml-100k")
     ts = Trainset.from_inner_arrays(u, i, r, n_users=int(u.max()) + 1, n_items=int(i.max()) + 1)
+    _lib.require_gpu()  # (torch's HIP context first; then the library's own calls)
     res = {"case": "dispatch", "layout": _lib.xcd_layout_ok()}
     algo = SVD(n_factors=20, n_epochs=2, random_state=0)
     algo._engine_options = {"heavy": 16, "xcd_split": True}

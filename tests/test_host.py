@@ -624,7 +624,6 @@ def test_qlog_fold_layout_partitions_cold_and_hot_items():
     hot = counts > 64
     assert lay["item_row_beg"][-1] + len(lay["hot_perm"]) == tot
     np.testing.assert_array_equal(np.diff(lay["item_row_beg"]), np.where(hot, 0, counts))
-    np.testing.assert_array_equal(lay["item_row_beg"], lay["item_user_beg"])
     np.testing.assert_array_equal(np.diff(lay["hot_item_piece_ptr"]), np.where(hot, -(-counts // 64), 0))
     pb = lay["hot_piece_beg"]
     assert pb[0] == 0 and pb[-1] == len(lay["hot_perm"]) and np.all(np.diff(pb) <= 64)

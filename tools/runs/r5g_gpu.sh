@@ -9,7 +9,7 @@ show() { grep '^{' gpurun_out/$1.json | python -c "import json,sys; r=json.loads
 for w in 4 8; do
   timeout -k 10 200 python3 -u bench.py --light-replay-wpc $w --no-cpu-baseline --no-rmse --no-svdpp --no-predict --no-c4 --steps 30 --warmup 5 --detail gpurun_out/${tag}_lrw${w}_d.json > gpurun_out/${tag}_lrw${w}.json 2> gpurun_out/${tag}_lrw${w}.log; rc=$?; show ${tag}_lrw${w}; fatal $rc
 done
-for v in base aux16 aux2 ids3 ids4; do
+for v in base aux16 aux2 ids3 ids4 ids8; do
   lib=""; [ $v != base ] && lib="SURPRISE_AMD_LIB=tests/variants/libsurprise_amd_$v.so"
   for rep in 1 2; do
     env $lib timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-rmse --no-svdpp --no-predict --no-c4 --steps 30 --warmup 5 --detail gpurun_out/${tag}_${v}_${rep}_d.json > gpurun_out/${tag}_${v}_${rep}.json 2> gpurun_out/${tag}_${v}_${rep}.log; rc=$?; show ${tag}_${v}_${rep}; fatal $rc
