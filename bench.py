@@ -127,6 +127,9 @@ def parse():
     p.add_argument("--light-replay-wpc", type=int, default=-1,
                    help="split chunk: the light group's replay waves per CU (engine option "
                         "light_replay_wpc; -1: the engine's default)")
+    p.add_argument("--log-nt", type=int, default=-1,
+                   help="the log's stores non-temporal (engine option log_nt; -1: the engine's "
+                        "size rule, 0 off, 1 on)")
     p.add_argument("--stagger", type=int, default=-1,
                    help="checkpoint log: the chunk's users in two staggered halves (engine option "
                         "stagger; -1: the engine's policy, 0 off, 1 on)")
@@ -758,6 +761,7 @@ def main():
                        **({"xcd_split": bool(args.xcd_split)} if args.xcd_split >= 0 else {}),
                        **({"long_chain": args.long_chain} if args.long_chain >= 0 else {}),
                        **({"stagger": bool(args.stagger)} if args.stagger >= 0 else {}),
+                       **({"log_nt": bool(args.log_nt)} if args.log_nt >= 0 else {}),
                        **({"light_replay_wpc": args.light_replay_wpc}
                           if args.light_replay_wpc >= 0 else {}))
         eng.set_factors(pu, qi, yj=yj)

@@ -41,7 +41,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
                     int hx, double *psq, int err_col, int ck_ld, int32_t *status,
-                    const uint8_t *hot, const int64_t *urow, void *stream);
+                    const uint8_t *hot, const int64_t *urow, bool nt, void *stream);
 // this unit's g_dispatch_sum (the dispatch check of the masked launches it holds)
 template <typename T, int M, bool PP>
 int dispatch_sum_tm(unsigned long long *out);
@@ -310,6 +310,7 @@ using rsrc_t = __amdgpu_buffer_rsrc_t;
 // in 32 bits here, so tables must stay below 2^31 bytes (kMaxTable, less one 4 KiB row).
 constexpr uint64_t kMaxTable = 0x80000000ull - 4096;
 constexpr int kSc1 = 16;                // gfx950 cache policy: sc1 (bypass the CU's L1)
+constexpr int kNt = 2;                  // gfx950 cache policy: nt (streamed: not kept in L2 / MALL)
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void *p, uint32_t bytes) {
     const uint64_t a = (uint64_t)p;
@@ -966,7 +967,7 @@ __device__ __forceinline__ void wave_sum2_u(T x, T y, T &sx, T &sy) {
 // wave-uniform element and the user bias c_k = mu + bu_k is the scalar recursion
 // c_{k+1} = C0_k + lr_bu err_k, C0_k = abu c_k + kb: X_{k+1} gains b_{k+1} + C0_k and Y_{k+1}
 // gains lr_bu -- the same err_k as the in-row form, with one lane group instead of two.
-template <typename T, int G, bool CK, bool ER = false, bool SB = false>
+template <typename T, int G, bool CK, bool ER = false, bool SB = false, bool NT = false>
 __device__ __forceinline__ void epoch_body_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
@@ -983,6 +984,8 @@ __device__ __forceinline__ void epoch_body_la(
     constexpr int kB = SB ? MF_LA_BANK_SB : (G == 1 ? MF_LA_BANK : MF_LA_BANK_G2);
     static_assert(!CK || (kB % kCkpt == 0 && kB <= kWave), "checkpoints: whole banks");
     constexpr int kAhead = MF_LA_IDS_AHEAD;  // banks between a bank's id loads and its gathers
+    // the log stores' cache policy: NT (MF_EPOCH_LOG_NT) streams them past the caches
+    constexpr int kLogAux = NT ? kNt : MF_LOG_AUX;
     static_assert(kAhead >= 2, "the next bank's ids are loaded before its rows");
     const int lane = threadIdx.x & (kWave - 1);
     int64_t wave, grid_waves;
@@ -1096,8 +1099,8 @@ __device__ __forceinline__ void epoch_body_la(
                 for (int x = 0; x < kLg; ++x)
 #pragma unroll
                     for (int v = 0; v < G; ++v)
-                        L::template sts<MF_LOG_AUX>(l_rs, cl[v], (uint32_t)(j0p / kCkpt + x) * lrow,
-                                                    lg[x][v]);
+                        L::template sts<kLogAux>(l_rs, cl[v], (uint32_t)(j0p / kCkpt + x) * lrow,
+                                                 lg[x][v]);
                 // err_k: into its pair's row (columns err_col, err_col + 1; the row stores above
                 // leave those columns alone) or to elog[k]; one store per bank either way
                 if constexpr (ER)
@@ -1110,7 +1113,7 @@ __device__ __forceinline__ void epoch_body_la(
             for (int d = 0; d < kB; ++d) {
 #pragma unroll
                 for (int v = 0; v < G; ++v)
-                    L::template sts<MF_LOG_AUX>(l_rs, cl[v], (uint32_t)(j0p + d) * qrow, lg[d][v]);
+                    L::template sts<kLogAux>(l_rs, cl[v], (uint32_t)(j0p + d) * qrow, lg[d][v]);
             }
         };
         {
@@ -1431,7 +1434,7 @@ __device__ void pp_ring_helper(PPRing<T, G, H> *ring, int h, T *qb, int ldq, int
 // after the chunk with the recency weights, as the SVD gradient log (oracle:
 // oracle_svdpp_sgd_stalelog with every item stale).  No float atomic, no helper wave.
 template <typename T, int G, bool HX, bool HOT = false, bool SB = false, int H = kHxHelpers,
-          bool LQ = false>
+          bool LQ = false, bool NT = false>
 __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
@@ -1615,9 +1618,11 @@ __device__ __forceinline__ void epoch_body_pp_la(
 #pragma unroll
                 for (int d = 0; d < kB; ++d) {
 #pragma unroll
-                    for (int v = 0; v < G; ++v) L::template sts<0>(l_rs, cq[v], dlo[d], dl[d][v]);
+                    for (int v = 0; v < G; ++v)
+                        L::template sts<NT ? kNt : 0>(l_rs, cq[v], dlo[d], dl[d][v]);
                     if constexpr (SB)
-                        Buf<T>::template sts<0>(l_rs, lane == 0 ? kbo : kColOob, dlo[d], dlb[d]);
+                        Buf<T>::template sts<NT ? kNt : 0>(l_rs, lane == 0 ? kbo : kColOob, dlo[d],
+                                                           dlb[d]);
                 }
                 return;
             }
@@ -1860,10 +1865,10 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
 // SVD checkpoint log (elog != NULL): its own kernel, so that its register allocation is its own
 // (ER: the errors go into the checkpoint rows, MF_EPOCH_ERR_IN_ROW; SB: the biases beside the
 // lane groups, narrow rows of whole groups)
-template <typename T, int G, bool ER, bool SB = false>
+template <typename T, int G, bool ER, bool SB = false, bool NT = false>
 __global__ __launch_bounds__(kBlock) void mf_ckpt_epoch_kernel(MF_EPOCH_PARAMS)
 {
-    epoch_body_la<T, G, true, ER, SB>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb,
+    epoch_body_la<T, G, true, ER, SB, NT>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb,
                                       ldq, qlog, elog, K, biased, hp, n_items, n_waves_req, xmask,
                                       psq, err_col, ck_ld);
 }
@@ -1900,11 +1905,11 @@ __global__ __launch_bounds__(kWave * (1 + H)) void mf_svdpp_hx_kernel(MF_EPOCH_P
 
 // SVD++ with the q log (mf_svdpp_epoch_qlog): every wave a user chain, the item rows read-only,
 // each rating's gradient row stored to the chunk's log (urow[u]: the user's first log row)
-template <typename T, int G, bool SB>
+template <typename T, int G, bool SB, bool NT = false>
 __global__ __launch_bounds__(kBlock) void mf_svdpp_qlog_kernel(MF_EPOCH_PARAMS,
                                                               const int64_t *urow)
 {
-    epoch_body_pp_la<T, G, false, false, SB, 1, true>(
+    epoch_body_pp_la<T, G, false, false, SB, 1, true, NT>(
         row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, elog, K, hp, n_items,
         n_waves_req, xmask, (PPRing<T, G, 1> *)nullptr, nullptr, nullptr, qlog, urow, psq);
 }
@@ -1918,7 +1923,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
                     int hx, double *psq, int err_col, int ck_ld, int32_t *status,
-                    const uint8_t *hot, const int64_t *urow, void *stream)
+                    const uint8_t *hot, const int64_t *urow, bool nt, void *stream)
 {
     if ((psq || err_col) && (PP || M != kLog || !elog) && !(psq && urow && !err_col))
         return set_err(MF_E_UNSUPPORTED, "user_sq / errors in rows: the SVD checkpoint log or the SVD++ q log only");
@@ -1975,7 +1980,10 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
         }
         if constexpr (PP && M == kLog && V <= kLaMaxG) {
             if (urow) {  // the q log: a user chain per wave, gradient rows to the chunk's log
-                auto kern = whole ? mf_svdpp_qlog_kernel<T, V, true> : mf_svdpp_qlog_kernel<T, V, false>;
+                auto kern = whole ? (nt ? mf_svdpp_qlog_kernel<T, V, true, true>
+                                        : mf_svdpp_qlog_kernel<T, V, true>)
+                                  : (nt ? mf_svdpp_qlog_kernel<T, V, false, true>
+                                        : mf_svdpp_qlog_kernel<T, V, false>);
                 hipLaunchKernelGGL(kern, dim3(grid_for_waves_x(waves, xmask)), dim3(kBlock), 0,
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
@@ -1989,9 +1997,12 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
         }
         if constexpr (M == kLog && !PP && V <= kLaMaxG && MF_LA) {
             if (elog) {  // the checkpoint log
-                auto ck = err_col > 0 ? mf_ckpt_epoch_kernel<T, V, true>
-                          : sbk       ? mf_ckpt_epoch_kernel<T, V, false, true>
-                                      : mf_ckpt_epoch_kernel<T, V, false>;
+                auto ck = err_col > 0 ? (nt ? mf_ckpt_epoch_kernel<T, V, true, false, true>
+                                            : mf_ckpt_epoch_kernel<T, V, true>)
+                          : sbk ? (nt ? mf_ckpt_epoch_kernel<T, V, false, true, true>
+                                      : mf_ckpt_epoch_kernel<T, V, false, true>)
+                                : (nt ? mf_ckpt_epoch_kernel<T, V, false, false, true>
+                                      : mf_ckpt_epoch_kernel<T, V, false>);
                 hipLaunchKernelGGL(ck, dim3(grid_for_waves_x(waves, xmask)), dim3(kBlock), 0,
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
@@ -2016,7 +2027,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
 template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
     void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, int, double *,
-    int, int, int32_t *, const uint8_t *, const int64_t *, void *);
+    int, int, int32_t *, const uint8_t *, const int64_t *, bool, void *);
 template <typename T, int M, bool PP>
 int dispatch_sum_tm(unsigned long long *out)
 {
@@ -4342,7 +4353,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         return mf_ext::launch_epoch_tm<T, M, PP>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj,
                                                   qlog, elog, K, biased, hp, waves, dups, xmask,
                                                   hx, psq, err_col, ck_ld, status, hot, urow,
-                                                  stream);
+                                                  (flags & MF_EPOCH_LOG_NT) != 0, stream);
     };
     auto by_mode = [&](auto tag_t) -> int {
         switch (mode) {
@@ -4523,8 +4534,9 @@ int mf_svdpp_epoch_qlog(const mf_csr_t *csr, const int32_t *sched, int64_t n_sch
                         void *stream)
 {
     if (!qlog || !log_row0 || !ycbuf) return set_err(MF_E_ARG, "the q log needs qlog, log_row0, ycbuf");
-    if (flags & ~(MF_EPOCH_DUP_ITEMS | (0xFF << MF_EPOCH_XCD_SHIFT)))
-        return set_err(MF_E_ARG, "mf_svdpp_epoch_qlog: flags MF_EPOCH_DUP_ITEMS / XCD mask only");
+    if (flags & ~(MF_EPOCH_DUP_ITEMS | MF_EPOCH_LOG_NT | (0xFF << MF_EPOCH_XCD_SHIFT)))
+        return set_err(MF_E_ARG, "mf_svdpp_epoch_qlog: flags MF_EPOCH_DUP_ITEMS / MF_EPOCH_LOG_NT / "
+                                 "XCD mask only");
     return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, ycbuf,
                               n_factors, 1, hp, MF_MODE_LOG, n_waves, flags, dtype, stream,
                               user_sq, nullptr, nullptr, log_row0);

@@ -410,7 +410,7 @@ class MFEngine(ItemSync, Predictor):
                  helpers=None, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
                  replay_rows=None, gram=None, xcd_split=None, qlog=None, top=None,
                  exchange=None, long_chain=256, overlap_q=True, fused=True, stagger=None,
-                 light_replay_wpc=0):
+                 light_replay_wpc=0, log_nt=None):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -464,6 +464,10 @@ class MFEngine(ItemSync, Predictor):
           light_replay_wpc  split chunk: the light group's log replay at this many waves per
                       CU (0: the library's 16) -- fewer leave the heavy chains' memory path
                       quieter while the replay still ends before them
+          log_nt      the checkpoint log's / SVD++ q log's rows stored non-temporal (streamed
+                      past L2 / MALL: MF_EPOCH_LOG_NT); None: where the log is >= LOG_NT_MIN_BYTES
+                      (C4: 27 GB of log evicted the item table from the MALL -- epoch kernel
+                      18.0 -> 14.6 ms; ML-1M's 0.3-GB log: +3%, off)
           fused       SVD++ q log on one rank: the chunk's fold in one pass over the items
                       (mf_svdpp_qlog_fold: the q gradients' weighted sums, the q step and the y
                       maps' composition together); False: mf_log_reduce + mf_log_apply +
@@ -832,6 +836,9 @@ class MFEngine(ItemSync, Predictor):
             if self.ckpt:  # (errors in the rows: elog is never read or written)
                 self.elog = z(64 if self.err_in_row else k_hi - k_lo + 64)
                 self._elog_base = self.elog.data_ptr() - (0 if self.err_in_row else k_lo * esz)
+        lbytes = self.qlog.numel() * self.qlog.element_size() if self.qlog is not None else 0
+        self.log_nt = bool(log_nt) if log_nt is not None else lbytes >= self.LOG_NT_MIN_BYTES
+        self.log_nt = self.log_nt and (self.ckpt or self.qlog_pp)
         snap_q = self.multi and self.mode != _lib.MF_MODE_LOG
         self.qb_s = z(I, ldq) if snap_q else None
         self.yj_s = z(I, ld) if (self.multi and self.yj is not None) else None
@@ -862,6 +869,7 @@ class MFEngine(ItemSync, Predictor):
     HEAVY_TOP_USERS = 0
     HEAVY_USERS_GRAM = 256  # ... with the blocked solve (one workgroup per user)
     HEAVY_MAX_NNZ = 8_000_000
+    LOG_NT_MIN_BYTES = 2 << 30  # (logs at least this large: non-temporal log stores)
 
     def _auto_heavy(self, row_ptr):
         """The heavy/light XCD split pays where the epoch is bound by its longest user chains:
@@ -990,6 +998,7 @@ class MFEngine(ItemSync, Predictor):
                       self.ldq, self.K, int(self.biased), ctypes.byref(self._hyper), self.mode,
                       qlog, elog, n_waves, flags, self.dtype, st)
         elif self.qlog_pp:
+            flags |= _lib.MF_EPOCH_LOG_NT if self.log_nt else 0
             _lib.call("mf_svdpp_epoch_qlog", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
                       self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper), qlog,
@@ -1094,6 +1103,7 @@ class MFEngine(ItemSync, Predictor):
                   (_lib.MF_EPOCH_DUP_ITEMS if self.dup_items else 0) |
                   (_lib.MF_EPOCH_ERR_IN_ROW if self.err_in_row else 0) |
                   (_lib.MF_EPOCH_CKPT_NARROW if self.narrow else 0) |
+                  (_lib.MF_EPOCH_LOG_NT if self.log_nt else 0) |
                   (xmask << _lib.MF_EPOCH_XCD_SHIFT), self.dtype, st)
 
     def _heavy_epoch(self, sched, n_sched, st, xmask=0):

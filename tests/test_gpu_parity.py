@@ -568,7 +568,7 @@ def test_svdpp_qlog_fp64_matches_stalelog_oracle(torch, u1, K, chunks, fused):
     P, f = run_oracle_stalelog(params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
                                cou, chunks)
     algo = SVDpp(**params, dtype="float64", chunks_per_epoch=chunks)
-    algo._engine_options = {"qlog": True, "fused": fused}
+    algo._engine_options = {"qlog": True, "fused": fused, "log_nt": fused}  # (nt with fused)
     algo.fit(ts)
     assert algo._engine.qlog_pp and not algo._engine.hx
     assert algo._engine._fused_fold() == fused
@@ -808,6 +808,32 @@ def test_narrow_checkpoint_rows_match_padded_rows(torch, u1, K, dtype, heavy, au
     tol = 1e-12 if dtype == "float64" else 1e-5
     for k in ("pu", "qi", "bu", "bi"):
         np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=tol, err_msg=k)
+
+
+@pytest.mark.parametrize("K,heavy", [(20, 0.0), (100, 16), (128, 0.0)])
+def test_nontemporal_log_stores_match_deltalog_oracle(torch, u1, K, heavy):
+    """log_nt (MF_EPOCH_LOG_NT, the default for logs of >= 2 GiB -- C4): the checkpoint rows
+    stored non-temporal change a cache policy, not a value: fp64 factors equal
+    oracle_svd_sgd_deltalog (merge=3) to 1e-9 (K=20 padded rows with errors, K=100 with the
+    heavy split, K=128 the narrow rows)."""
+    from surprise_amd.engine import MFEngine
+    ts, _ = u1
+    row_ptr, items, ratings = ts.csr()
+    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
+                 reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    rng = np.random.RandomState(10)
+    pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
+    eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype="float64",
+                   mode="log", heavy=heavy, log_nt=True)
+    assert eng.ckpt and eng.log_nt
+    eng.set_factors(pu0, qi0)
+    eng.run_epochs(3)
+    got = eng.get_factors()
+    hp = orc.hyper(**{k: v for k, v in hyper.items() if k != "global_mean"})
+    pu, qi, bu, bi = orc.svd_sgd_deltalog(row_ptr, items, ratings, ts.n_items, K, 3, True,
+                                          ts.global_mean, hp, pu0.copy(), qi0.copy(), merge=3)
+    for k, ref in (("pu", pu), ("qi", qi), ("bu", bu), ("bi", bi)):
+        np.testing.assert_allclose(got[k], ref, rtol=0, atol=1e-9, err_msg=k)
 
 
 @pytest.mark.parametrize("K", [20, 128])
