@@ -103,6 +103,19 @@ def test_c5_shard_svdpp_k128_e20_within_1e3_of_committed_oracle(torch):
     assert abs(r["rmse"]["delta"]) < 1e-3, r["rmse"]
 
 
+def test_c5_shard_qlog_e20_within_1e3_of_committed_oracle(torch):
+    """The C5 shard (1.25M users, 123M ratings, SVD++ K=128) on the q log (item rows read-only
+    within each of the 16 chunks, gradients folded by the fused per-item fold, nt log stores) at
+    20 epochs: within 1e-3 of the exact per-user oracle's held-out RMSE (scale_golden.json
+    c5shard, mf.pyx:463-498)."""
+    g = _golden("c5shard")
+    r = _bench("--shape", "c5", "--users", "1250000", "--qlog", "--rmse-epochs", "20",
+               timeout=1100)
+    assert "+qlog" in r["config"]["workload"]
+    assert r["rmse"]["reference_oracle_fp64"] == g["rmse_by_epoch"][19]
+    assert abs(r["rmse"]["delta"]) < 1e-3, r["rmse"]
+
+
 def test_c5_at_8_ranks_schedule_within_1e3_of_committed_oracle(torch):
     """C5@8's own schedule at shard scale (gloo rehearsal on the one GPU): the 1.25M-user shard
     split over 8 ranks exactly as bench.py --gpus 8 splits C5 (dist.shard_users), 2 epoch-chunks
