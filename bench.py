@@ -592,7 +592,8 @@ def executed_bytes(lay, ratings, users, pieces=0, whole_step=False):
     return ratings * algorithmic_bytes_per_update(lay["algo"], K, s)
 
 
-def roofline_of(algo, K, dtype, n_train, ms_step, shape, phases=None, lay=None, chain=None):
+def roofline_of(algo, K, dtype, n_train, ms_step, shape, phases=None, lay=None, chain=None,
+                qlog=False):
     """The dominant kernel's roofline.  The dominant kernel is the epoch kernel; one "launch" in
     the contract's sense is its invocation over one step's ratings, whose launches of a split
     chunk (the heavy users' on XCD 0, the others' on XCDs 1-7) run concurrently -- so its
@@ -607,7 +608,8 @@ def roofline_of(algo, K, dtype, n_train, ms_step, shape, phases=None, lay=None, 
     B8 = algorithmic_bytes_per_update(algo, K, s)
     traffic, tinfo = traffic_for(algo, K, shape, dtype)
     ek = (phases or {}).get("epoch_kernel")
-    kname = "mf_svdpp_hx_kernel" if algo == "svdpp" else "mf_ckpt_epoch_kernel"
+    kname = ("mf_svdpp_qlog_kernel" if qlog else "mf_svdpp_hx_kernel") if algo == "svdpp" \
+        else "mf_ckpt_epoch_kernel"
     gbs = lambda b, ms: b / (ms * 1e-3) / 1e9
     out = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     if not (ek and lay):
@@ -812,13 +814,16 @@ def main():
     lay = layout_of(eng)
     chain = time_top_chain(eng, torch) if args.shape == "ml-1m" and not args.no_chain_probe \
         else None
+    qlog = bool(getattr(eng, "qlog_pp", False))
     rl = roofline_of(algo, K, args.dtype, n_train, ms_step, shape_key(args.shape, args.users),
-                     phases, lay, chain)
+                     phases, lay, chain, qlog=qlog)
     rl.update({
         "kernel": "dominant: %s; step (%s): %s" % (
             (rl.get("dominant_kernel") or {}).get("kernel"), mode,
             "mf_ckpt_epoch_kernel (heavy + light users) + log_replay_kernel (both groups) "
-            "+ log_apply_kernel" if mode == "log" else "mf_svdpp_hx_kernel + y fold (+ merge)"),
+            "+ log_apply_kernel" if mode == "log" else
+            "mf_svdpp_qlog_kernel + mf_svdpp_qlog_fold (log_reduce_kernel, y_piece_kernel, "
+            "qlog_fold_kernel)" if qlog else "mf_svdpp_hx_kernel + y fold (+ merge)"),
         "phases_gpu_ms": phases, "note": ROOFLINE_NOTE})
     result["roofline"] = rl
 
@@ -1170,7 +1175,9 @@ def rmse_leg(args, ctx, csr, test, n_items, K, gm, mode, rank, world, torch, mak
     out = {"gpu": (se / n) ** .5, "global_mean_baseline": (se_mu / n) ** .5,
            "below_global_mean": bool(se < se_mu),
            "fit": "%s K=%d E=%d %s (%s) through the bench engine, %d held-out ratings over %d "
-                  "rank(s)" % (args.algo.upper(), K, E, eng.tdt, mode, int(n), world)}
+                  "rank(s)" % (args.algo.upper(), K, E, eng.tdt,
+                               mode + ("+qlog" if getattr(eng, "qlog_pp", False) else ""),
+                               int(n), world)}
     del eng
     if world == 1 and (args.shape == "ml-1m" or args.oracle):
         ref, secs = oracle_rmse(args, csr, test, n_items, K, gm, oracle_cache)

@@ -3919,28 +3919,43 @@ __global__ __launch_bounds__(kBlock) void qlog_fold_kernel(
         const int h0_l = in_l && hot_item_piece_ptr ? hot_item_piece_ptr[it_l] : 0;
         const int h1_l = in_l && hot_item_piece_ptr ? hot_item_piece_ptr[it_l + 1] : 0;
         const int N_l = in_l ? totals[it_l] : 0;
-        // the cold rows' indices of item t (lane x: row x), loaded one item ahead of its gathers
-        auto vload = [&](const int t, int &k_l, int &u_l, T &wf_l, T &wb_l, T &A_l) {
+        // the cold rows' indices of item t (lane x: row x) are loaded two items ahead of its
+        // gathers, its weights and A_u one item ahead: the A_u gather and the weights need the
+        // indices, so issuing all three at once stalls every item on two dependent round trips
+        auto iload = [&](const int t, int &k_l, int &u_l, int &p_l) {
             const int r0 = readlane(r0_l, t), cnt = readlane(r1_l, t) - r0;
-            const int N = readlane(N_l, t);
             const int xl = r0 + (lane < cnt ? lane : (cnt > 0 ? cnt - 1 : 0));
-            const bool ok = lane < cnt;
             k_l = cnt > 0 ? perm[xl] : 0;
             u_l = cnt > 0 ? item_users[xl] : 0;
-            const double back = (double)(N - 1 - (cnt > 0 ? rc.rpos[xl] : 0));
-            wf_l = ok ? (T)exp(back * l_q) : T(0);
-            wb_l = ok ? (T)exp(back * l_b) : T(0);
+            p_l = cnt > 0 ? rc.rpos[xl] : 0;
+        };
+        auto wload = [&](const int t, const int u_l, const int p_l, T &wf_l, T &wb_l, T &A_l) {
+            const int cnt = readlane(r1_l, t) - readlane(r0_l, t);
+            const int N = readlane(N_l, t);
+            const bool ok = lane < cnt;
+            if constexpr (sizeof(T) == 4) {  // (fp32 weights: the float exp, ~8x cheaper)
+                const float back = (float)(N - 1 - p_l);
+                wf_l = ok ? expf(back * (float)l_q) : 0.f;
+                wb_l = ok ? expf(back * (float)l_b) : 0.f;
+            } else {
+                const double back = (double)(N - 1 - p_l);
+                wf_l = ok ? (T)exp(back * l_q) : T(0);
+                wb_l = ok ? (T)exp(back * l_b) : T(0);
+            }
             A_l = cnt > 0 ? uA[u_l] : T(1);
         };
-        int k_c, u_c;
+        int k_c = 0, u_c = 0, p_c = 0, k_n = 0, u_n = 0, p_n = 0;
         T wf_c, wb_c, A_c;
-        vload(0, k_c, u_c, wf_c, wb_c, A_c);
+        iload(0, k_c, u_c, p_c);
+        if (b + NB < n_items) iload(1, k_n, u_n, p_n);
+        wload(0, u_c, p_c, wf_c, wb_c, A_c);
         for (int t = 0; t < kWave; ++t) {
             const int64_t i = b + NB * t;
             if (i >= n_items) break;  // (uniform)
-            int k_n = 0, u_n = 0;
+            int k_nn = 0, u_nn = 0, p_nn = 0;
+            if (t + 2 < kWave && i + 2 * NB < n_items) iload(t + 2, k_nn, u_nn, p_nn);
             T wf_n = T(0), wb_n = T(0), A_n = T(1);
-            if (t + 1 < kWave && i + NB < n_items) vload(t + 1, k_n, u_n, wf_n, wb_n, A_n);
+            if (t + 1 < kWave && i + NB < n_items) wload(t + 1, u_n, p_n, wf_n, wb_n, A_n);
             const int cnt = readlane(r1_l, t) - readlane(r0_l, t);
             const int h0 = readlane(h0_l, t), h1 = readlane(h1_l, t);
             if (cnt > 0 || h0 < h1) {
@@ -4044,6 +4059,9 @@ __global__ __launch_bounds__(kBlock) void qlog_fold_kernel(
             wf_c = wf_n;
             wb_c = wb_n;
             A_c = A_n;
+            k_n = k_nn;
+            u_n = u_nn;
+            p_n = p_nn;
         }
     }
 }

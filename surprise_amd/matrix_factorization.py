@@ -23,7 +23,13 @@ no CPU fallback.  Extra, keyword-only device options:
                      SVD, "atomic" for SVD++)
   chunks_per_epoch   epoch-chunks (item merges / all-reduces per epoch); "auto" (default): 1
                      for SVD, one per 80,000 users of a rank for SVD++ (engine.default_chunks)
-  deterministic      one wavefront, users in Trainset order: the reference's exact sequence
+  deterministic      True: one wavefront, users in Trainset order -- the reference's exact
+                     sequence (bit-for-bit the reference's factors in fp64); False: the parallel
+                     schedule; None (SVD default, "auto"): the exact sequence for small fits --
+                     at most EXACT_MAX_UPDATES rating-updates (n_ratings x n_epochs) and
+                     EXACT_MAX_WORK updates x factors, with mode, chunks_per_epoch and n_waves
+                     left at their defaults and not distributed -- the parallel schedule
+                     otherwise (SVDpp: False)
   n_waves            wavefronts per launch (0 = fill the GPU)
   distributed        opt-in: shard users over the torch.distributed ranks of the job (one
                      process per GPU, torchrun env); every rank must fit the same trainset
@@ -43,6 +49,14 @@ from .algo_base import AlgoBase
 from .predictions import Prediction, PredictionImpossible
 from .trainset import Trainset
 from .utils import get_rng
+
+
+# deterministic=None: the reference's exact order where it costs little.  u1 (80k ratings) SVD
+# K=100 E=20 fp64: 45 ms exact vs 4.5 ms parallel on one MI355X, and the exact order lands on the
+# reference's RMSE to the last digit where the parallel schedule is +5.5e-2 off on the diverging
+# unbiased case (profiles/r5k_probe.jsonl)
+EXACT_MAX_UPDATES = 2_000_000
+EXACT_MAX_WORK = 200_000_000
 
 
 class _MFBase(AlgoBase):
@@ -70,6 +84,18 @@ class _MFBase(AlgoBase):
         helper-wave launch -- DESIGN.md 2.)"""
         return "float64" if getattr(self, "n_factors", 0) <= _lib.MAX_FACTORS[_lib.MF_F64] \
             else "float32"
+
+    def _resolve_deterministic(self, n_ratings):
+        """deterministic=None ("auto", SVD's default): the exact sequential order for a small fit
+        (EXACT_MAX_UPDATES, EXACT_MAX_WORK) with every schedule option at its default."""
+        if self.deterministic is not None:
+            return bool(self.deterministic)
+        updates = int(n_ratings) * int(self.n_epochs)
+        return (self._algo == "svd" and self.mode == "auto" and self.chunks_per_epoch == "auto"
+                and not self.n_waves and not self.distributed
+                and not getattr(self, "_engine_options", None)
+                and updates <= EXACT_MAX_UPDATES
+                and updates * max(int(self.n_factors), 1) <= EXACT_MAX_WORK)
 
     def __getstate__(self):
         state = self.__dict__.copy()
@@ -148,7 +174,9 @@ class _MFBase(AlgoBase):
         global_mean = self.trainset.global_mean
         n_users, n_items = trainset.n_users, trainset.n_items
 
-        ctx = DistContext.from_env() if (self.distributed and not self.deterministic) else None
+        det = self._resolve_deterministic(csr[0][-1] - csr[0][0])
+        self.exact_order_ = det  # (what the fit ran: the reference's sequence or the parallel one)
+        ctx = DistContext.from_env() if (self.distributed and not det) else None
         if ctx is not None and ctx.world > 1:
             # every rank must hold the same trainset: it shards it by user range below
             ctx.check_agreement(csr_fingerprint(csr, n_items), "the trainset (users, items, "
@@ -167,7 +195,7 @@ class _MFBase(AlgoBase):
         eng = MFEngine(csr, n_items, self.n_factors, algo=self._algo,
                        hyper=self._hyper(global_mean), biased=getattr(self, "biased", True),
                        dtype=self.dtype, mode=self._resolve_mode(),
-                       n_chunks=chunks, deterministic=self.deterministic,
+                       n_chunks=chunks, deterministic=det,
                        user_order=user_order, n_waves=self.n_waves, world=world,
                        **getattr(self, "_engine_options", {}))
         eng.set_factors(pu[lo:hi], qi, yj=yj)
@@ -324,7 +352,7 @@ class SVD(_MFBase):
                  lr_all=.005, reg_all=.02, lr_bu=None, lr_bi=None, lr_pu=None, lr_qi=None,
                  reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, random_state=None,
                  verbose=False, *, dtype=None, mode="auto",
-                 chunks_per_epoch="auto", deterministic=False, n_waves=0, distributed=False):
+                 chunks_per_epoch="auto", deterministic=None, n_waves=0, distributed=False):
         self.n_factors = n_factors
         self.n_epochs = n_epochs
         self.biased = biased

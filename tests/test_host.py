@@ -609,6 +609,29 @@ def test_default_dtype_is_fp64_up_to_the_fp64_row_limit():
     assert not b._dtype_auto  # (an explicit dtype stays: fit then refuses 300 fp64 factors)
 
 
+def test_default_schedule_is_the_exact_order_for_small_svd_fits():
+    """SVD(deterministic=None), the default: the reference's exact sequence when the fit is small
+    (n_ratings x n_epochs <= EXACT_MAX_UPDATES and x n_factors <= EXACT_MAX_WORK) and every
+    schedule option is at its default; the parallel schedule otherwise.  SVDpp: parallel."""
+    from surprise_amd import SVD, SVDpp
+    from surprise_amd.matrix_factorization import EXACT_MAX_UPDATES, EXACT_MAX_WORK
+    u1 = 80_000
+    assert SVD(n_factors=100, n_epochs=20)._resolve_deterministic(u1)      # 1.6M updates
+    assert SVD(n_factors=20, n_epochs=5)._resolve_deterministic(u1)        # configs[0]
+    assert not SVD(n_factors=100, n_epochs=20)._resolve_deterministic(1_000_209)  # ML-1M
+    assert not SVD(n_factors=100, n_epochs=21)._resolve_deterministic(100_000)  # 2.1M updates
+    assert not SVD(n_factors=200, n_epochs=20)._resolve_deterministic(u1)  # 3.2e8 > EXACT_MAX_WORK
+    assert EXACT_MAX_UPDATES * 100 == EXACT_MAX_WORK
+    for kw in (dict(mode="log"), dict(chunks_per_epoch=2), dict(n_waves=64),
+               dict(distributed=True), dict(deterministic=False)):
+        assert not SVD(n_factors=20, n_epochs=5, **kw)._resolve_deterministic(u1), kw
+    assert SVD(n_factors=20, n_epochs=5, deterministic=True)._resolve_deterministic(10 ** 9)
+    opt = SVD(n_factors=20, n_epochs=5)
+    opt._engine_options = {"heavy": 16}  # (an engine option asks for the parallel schedule)
+    assert not opt._resolve_deterministic(u1)
+    assert not SVDpp(n_factors=20, n_epochs=5)._resolve_deterministic(u1)
+
+
 def test_qlog_fold_layout_partitions_cold_and_hot_items():
     """mf_svdpp_qlog_fold's layout (engine.qlog_fold_layout): every item-grouped position is
     either a cold item's (listed directly, item_row_beg / item_user_beg ranges) or a hot item's

@@ -48,6 +48,12 @@ if os.path.exists(bench):
     lines = [l for l in open(bench) if l.startswith("{")]
     if lines:
         summary["bench_line_under_profiler"] = json.loads(lines[-1])
+        # (the stdout line is the compact one since round 5: the full dictionary is its detail file,
+        # which every pass of tools/profile.sh rewrites with the same configuration)
+        det = summary["bench_line_under_profiler"].get("detail")
+        if det and os.path.exists(os.path.join(ROOT, det)):
+            with open(os.path.join(ROOT, det)) as f:
+                summary["bench_line_under_profiler"] = json.load(f)
 
 
 def pmc(kind, counter):
