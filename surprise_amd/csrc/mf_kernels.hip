@@ -904,6 +904,12 @@ constexpr int kLaMaxG = MF_LA_MAX_G;
 #ifndef MF_LOG_AUX
 #define MF_LOG_AUX 0  // cache policy of the lookahead body's log stores
 #endif
+#ifndef MF_STREAM_AUX
+#define MF_STREAM_AUX 0  // epoch kernel: cache policy of the CSR reads and the user-row stream
+#endif
+#ifndef MF_ELOG_AUX
+#define MF_ELOG_AUX 0  // epoch kernel: cache policy of the error-log stores
+#endif
 
 // ---- two 64-lane sums at once (the lookahead body's X and Y): the halves are exchanged with one
 // v_permlane32_swap so that lanes 0-31 carry x's partials and lanes 32-63 y's, then one 5-step
@@ -1054,7 +1060,7 @@ __device__ __forceinline__ void epoch_body_la(
         vec p0[G];
 #pragma unroll
         for (int v = 0; v < G; ++v)
-            p0[v] = L::template ld<0>(p_rs, cu[v]) + one[v] + (hp.gm + bu0) * cvec[v];
+            p0[v] = L::template ld<MF_STREAM_AUX>(p_rs, cu[v]) + one[v] + (hp.gm + bu0) * cvec[v];
 
 
         // Two banks of kB gathered rows alternate.  At the start of a bank: the ids of the bank
@@ -1067,8 +1073,13 @@ __device__ __forceinline__ void epoch_body_la(
         auto grp_load = [&](int j0, uint32_t &go, T &gr) {
             int j = j0 + (lane & (kB - 1));
             j = j < n ? j : n - 1;
-            go = (uint32_t)it[j] * qrow;
-            gr = rt[j];
+            if constexpr (MF_STREAM_AUX == kNt) {
+                go = (uint32_t)__builtin_nontemporal_load(it + j) * qrow;
+                gr = __builtin_nontemporal_load(rt + j);
+            } else {
+                go = (uint32_t)it[j] * qrow;
+                gr = rt[j];
+            }
         };
         vec bank[2][kB][G];
         T br[2][kB];
@@ -1106,7 +1117,7 @@ __device__ __forceinline__ void epoch_body_la(
                 if constexpr (ER)
                     Buf<T>::template st<0>(l_rs, ce + (uint32_t)(j0p / kCkpt) * lrow, ev);
                 else
-                    Buf<T>::template st<0>(e_rs, lane < kB ? (uint32_t)(j0p + lane) * sizeof(T) : kLogOob, ev);
+                    Buf<T>::template st<MF_ELOG_AUX>(e_rs, lane < kB ? (uint32_t)(j0p + lane) * sizeof(T) : kLogOob, ev);
                 return;
             }
 #pragma unroll
@@ -1259,7 +1270,7 @@ __device__ __forceinline__ void epoch_body_la(
 #pragma unroll
         for (int v = 0; v < G; ++v) {
             const vec pn = A_p[v] + err_p * D_p[v];
-            L::template st<0>(p_rs, cu[v], pn);
+            L::template st<MF_STREAM_AUX>(p_rs, cu[v], pn);
             if (!SB && v == cb_grp) cn = readlane(L::get(pn, cb_e), cb_lane);
 #pragma unroll
             for (int e = 0; e < W; ++e) {
@@ -2428,6 +2439,12 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
 #ifndef MF_REPLAY_WPC
 #define MF_REPLAY_WPC 16  // replay waves per CU
 #endif
+#ifndef MF_REPLAY_ROW_NT
+// the replay's checkpoint-row gathers non-temporal: each row is read twice, far apart, so caching
+// it buys nothing, and streaming it past the MALL leaves the error log's lines there for the
+// error gathers (C4 replay fp32 12.8 -> 12.1 ms, fp64 18.9 -> 17.9; profiles/r5n_replay_nt.txt)
+#define MF_REPLAY_ROW_NT 1
+#endif
 
 // ---------------------------------------------------------------- checkpoint-log replay
 //
@@ -2538,7 +2555,12 @@ __device__ __forceinline__ void log_replay_body(
                     const int x = x0 + y < kWave ? x0 + y : kWave - 1;
                     const T *row = ckpt + (int64_t)readlane(c_l, x) * ldc;
 #pragma unroll
-                    for (int v = 0; v < GR; ++v) p[y][v] = *(const vec *)(row + cc[v]);
+                    for (int v = 0; v < GR; ++v)
+#if MF_REPLAY_ROW_NT
+                        p[y][v] = __builtin_nontemporal_load((const vec *)(row + cc[v]));
+#else
+                        p[y][v] = *(const vec *)(row + cc[v]);
+#endif
                 }
             };
             auto comp_grp = [&](const int x0, vec (&p)[kU][G]) {
