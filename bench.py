@@ -119,9 +119,11 @@ def parse():
     p.add_argument("--top", type=int, default=-1,
                    help="split chunk: heavy users kept on the main stream, the rest of the heavy "
                         "launch beside them (engine option top; -1: the engine's default, 0: off)")
-    p.add_argument("--qlog", action="store_true",
-                   help="SVD++: the q log (item rows read-only within a chunk, gradients folded "
-                        "after it; engine option qlog) instead of the float-atomic schedule")
+    p.add_argument("--qlog", type=int, nargs="?", const=1, default=-1,
+                   help="SVD++: 1 (or bare --qlog) the q log (item rows read-only per chunk, "
+                        "gradients logged and folded after it; engine option qlog), 0 the "
+                        "float-atomic schedule; default: the engine's auto_qlog (the q log on one "
+                        "rank with several chunks of <= 10 ratings per item: C5)")
     p.add_argument("--no-c4", action="store_true",
                    help="skip the C4 leg (BASELINE configs[3]'s shape on this GPU)")
     p.add_argument("--light-replay-wpc", type=int, default=-1,
@@ -371,10 +373,12 @@ def shape_key(shape, users=0):
     return shape + ("_u%d" % users if users and shape in ("c4", "c5") else "")
 
 
-def traffic_for(algo, K, shape, dtype="f32"):
-    """Measured HBM-side bytes per step (profiles/traffic_<algo>_k<K>_<shape>[_f64].json, written
-    by tools/profile.sh from separate rocprofv3 --pmc passes)."""
-    name = "traffic_%s_k%d_%s%s.json" % (algo, K, shape, "" if dtype == "f32" else "_" + dtype)
+def traffic_for(algo, K, shape, dtype="f32", qlog=False):
+    """Measured HBM-side bytes per step (profiles/traffic_<algo>_k<K>_<shape>[_f64][_qlog].json,
+    written by tools/profile.sh from separate rocprofv3 --pmc passes; SVD++ on the q log has its
+    own file -- the atomic schedule's bytes are not its)."""
+    name = "traffic_%s_k%d_%s%s%s.json" % (algo, K, shape, "" if dtype == "f32" else "_" + dtype,
+                                          "_qlog" if qlog else "")
     path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None, None
@@ -606,7 +610,7 @@ def roofline_of(algo, K, dtype, n_train, ms_step, shape, phases=None, lay=None, 
     chain: the heaviest user's chain timed alone -- the latency roof of the critical launch."""
     s = ELEM_BYTES[dtype]
     B8 = algorithmic_bytes_per_update(algo, K, s)
-    traffic, tinfo = traffic_for(algo, K, shape, dtype)
+    traffic, tinfo = traffic_for(algo, K, shape, dtype, qlog)
     ek = (phases or {}).get("epoch_kernel")
     kname = ("mf_svdpp_qlog_kernel" if qlog else "mf_svdpp_hx_kernel") if algo == "svdpp" \
         else "mf_ckpt_epoch_kernel"
@@ -756,7 +760,8 @@ def main():
                        **({"helpers": args.hx_helpers} if args.hx_helpers else {}),
                        **({"heavy": args.heavy} if args.heavy >= 0 else {}),
                        **({"hot_rows": args.hot_rows} if args.hot_rows >= 0 else {}),
-                       **({"qlog": True} if args.qlog and a == "svdpp" else {}),
+                       **({"qlog": bool(args.qlog)} if args.qlog >= 0 and a == "svdpp"
+                          else {}),
                        **({"top": args.top} if args.top >= 0 else {}),
                        **({"replay_rows": args.replay_rows} if args.replay_rows else {}),
                        **({"gram": bool(args.gram)} if args.gram >= 0 else {}),

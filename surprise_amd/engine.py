@@ -70,6 +70,28 @@ def default_chunks(algo: str, mode: str, n_users_total: int, world: int = 1) -> 
     return 1
 
 
+# SVD++ q log (qlog=None: auto).  The q log reads every item row from the chunk-start table, so
+# its staleness grows with how often one chunk rates the same item.  Measured (held-out RMSE - the
+# exact oracle at E=20, profiles/r5k_probe.jsonl, r5p_probe.jsonl): ML-1M (C3, one
+# rank) at 16 chunks -- 13.5 ratings per item and chunk -- +1.9e-3, at 24 / 32 / 64 / 128 chunks
+# (9.0 / 6.7 / 3.4 / 1.7) -2.6e-4 / -2.6e-4 / -2.9e-4 / -1.3e-4; C5 (7.7 per item and chunk)
+# within 1e-3 of the sequential oracle on the shard, 0.94543 vs the atomic schedule's 0.94641 on
+# the full C5.  At C5 it is the faster schedule (shard 70.5 vs 89.7 ms, full 802 vs 845 ms).
+QLOG_MAX_RATINGS_PER_ITEM_CHUNK = 10.0
+
+
+def auto_qlog(algo: str, mode: int, nnz: int, n_items: int, n_chunks: int, world: int,
+              exchange, dup_items: bool, deterministic: bool) -> bool:
+    """qlog=None: the q log for SVD++ on ONE rank with several epoch-chunks (the default chunking
+    gives more than one from 80k users up) whose mean ratings per item and chunk are at most
+    QLOG_MAX_RATINGS_PER_ITEM_CHUNK; the atomic schedule otherwise (ML-1M's one chunk: C3;
+    several ranks, whose rank-order merge is pinned for the atomic schedule)."""
+    return (algo == "svdpp" and mode == _lib.MF_MODE_ATOMIC and not deterministic
+            and int(world) == 1 and not exchange and not dup_items and int(n_chunks) >= 2
+            and n_items > 0
+            and nnz / (float(n_items) * int(n_chunks)) <= QLOG_MAX_RATINGS_PER_ITEM_CHUNK)
+
+
 def _pad64(n: int, dtype: int) -> int:
     per64 = 16 if dtype == _lib.MF_F32 else 8
     return -(-n // per64) * per64
@@ -451,7 +473,8 @@ class MFEngine(ItemSync, Predictor):
           qlog        SVD++: the item rows read-only within an epoch-chunk, each rating's q / b
                       gradient logged (mf_svdpp_epoch_qlog) and folded after the chunk with the
                       recency weights, y deferred -- no float atomics (oracle:
-                      oracle_svdpp_sgd_stalelog); None / False: the atomic schedule
+                      oracle_svdpp_sgd_stalelog); False: the atomic schedule; None: auto_qlog
+                      (one rank, several chunks, <= 10 ratings per item and chunk)
           long_chain  epoch-chunk dealing (dist.chunk_users): users of more than 1 / long_chain
                       of a chunk's ratings all go to chunk 0 (when at most n_chunks of them);
                       0: plain round-robin dealing (the dealing before round 4)
@@ -500,6 +523,12 @@ class MFEngine(ItemSync, Predictor):
         if self.deterministic:
             mode, n_chunks, n_waves = "plain", 1, 1
         self.mode = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
+        # (a user listing an item twice: the kernels forward rows in registers)
+        self.dup_items = int(_has_duplicate_items(row_ptr, items, self.n_items, torch, self.dev))
+        if qlog is None:
+            qlog = auto_qlog(algo, self.mode, int(row_ptr[-1] - row_ptr[0]), self.n_items,
+                             max(1, int(n_chunks)), world, exchange, self.dup_items,
+                             self.deterministic)
         # SVD++ q log: MF_MODE_LOG's log / fold machinery with the deferred-y lookahead chain
         esz0 = 8 if self.dtype == _lib.MF_F64 else 4
         self.qlog_pp = (algo == "svdpp" and not self.deterministic and bool(qlog)
@@ -587,8 +616,6 @@ class MFEngine(ItemSync, Predictor):
         # (read-only after construction: elog is sized for it)
         self._err_in_row = (self.ckpt and not self.narrow and e0 + 2 <= self.ldq
                             and bool(err_in_row))
-        # (a user listing an item twice: the kernels forward rows in registers)
-        self.dup_items = int(_has_duplicate_items(row_ptr, items, self.n_items, torch, dev))
         if self.qlog_pp and self.dup_items:
             raise ValueError("qlog: a user lists an item twice (the q log reads each item row "
                              "once per rating from the chunk-start table)")

@@ -94,9 +94,13 @@ def test_c4_two_ranks_equal_one(torch, c4_one):
 
 def test_c5_shard_svdpp_k128_e20_within_1e3_of_committed_oracle(torch):
     """One of 8 ranks' share of C5 (the first 1.25M users, every one of the 1M items, 123M
-    ratings, SVD++ K=128) at 20 epochs against the committed exact per-user oracle value."""
+    ratings, SVD++ K=128) at 20 epochs on the float-atomic schedule (--qlog 0: on one rank the
+    engine's default here is the q log, auto_qlog) against the committed exact per-user oracle
+    value."""
     g = _golden("c5shard")
-    r = _bench("--shape", "c5", "--users", "1250000", "--rmse-epochs", "20", timeout=1100)
+    r = _bench("--shape", "c5", "--users", "1250000", "--qlog", "0", "--rmse-epochs", "20",
+               timeout=1100)
+    assert "+qlog" not in r["config"]["workload"]
     assert r["config"]["algo"] == "svdpp" and r["config"]["items"] == 1_000_000
     assert r["config"]["train_ratings_rank0"] == g["train_ratings"]
     assert r["rmse"]["reference_oracle_fp64"] == g["rmse_by_epoch"][19]
@@ -104,14 +108,14 @@ def test_c5_shard_svdpp_k128_e20_within_1e3_of_committed_oracle(torch):
 
 
 def test_c5_shard_qlog_e20_within_1e3_of_committed_oracle(torch):
-    """The C5 shard (1.25M users, 123M ratings, SVD++ K=128) on the q log (item rows read-only
+    """The C5 shard (1.25M users, 123M ratings, SVD++ K=128) on its default schedule on one rank,
+    the q log (auto_qlog: 16 chunks of ~7.7 ratings per item; item rows read-only
     within each of the 16 chunks, gradients folded by the fused per-item fold, nt log stores) at
     20 epochs: within 1e-3 of the exact per-user oracle's held-out RMSE (scale_golden.json
     c5shard, mf.pyx:463-498)."""
     g = _golden("c5shard")
-    r = _bench("--shape", "c5", "--users", "1250000", "--qlog", "--rmse-epochs", "20",
-               timeout=1100)
-    assert "+qlog" in r["config"]["workload"]
+    r = _bench("--shape", "c5", "--users", "1250000", "--rmse-epochs", "20", timeout=1100)
+    assert "+qlog" in r["config"]["workload"]  # (the default here: auto_qlog)
     assert r["rmse"]["reference_oracle_fp64"] == g["rmse_by_epoch"][19]
     assert abs(r["rmse"]["delta"]) < 1e-3, r["rmse"]
 
@@ -149,14 +153,18 @@ def test_c5_miniature_long_chain_dealing_within_1e3_of_committed_oracle(torch):
     60k users of C5 at 8 epoch-chunks (8 such users, tests/test_dist.py), SVD++ K=128, 20 epochs,
     against the exact per-user oracle's held-out RMSE committed in scale_golden.json (c5_u60000,
     mf.pyx:463-498).  The round-robin dealing (long_chain=0, one long user per chunk) on the
-    same data is held to the same bar; both deltas are printed for the record."""
+    same data is held to the same bar, on the one-rank default schedule (the q log: auto_qlog,
+    0.7 ratings per item and chunk) and on the float-atomic one; the deltas are printed."""
     g = _golden("c5_u60000")
     r = _bench("--shape", "c5", "--users", C5_USERS, "--chunks", "8", "--rmse-epochs", "20")
     r0 = _bench("--shape", "c5", "--users", C5_USERS, "--chunks", "8", "--rmse-epochs", "20",
                 "--long-chain", "0")
-    print("c5_u60000 E=20: long-chain dealing %+.3e, round-robin %+.3e (oracle %.6f)"
-          % (r["rmse"]["delta"], r0["rmse"]["delta"], g["rmse_by_epoch"][19]))
-    for x in (r, r0):
+    ra = _bench("--shape", "c5", "--users", C5_USERS, "--chunks", "8", "--rmse-epochs", "20",
+                "--qlog", "0")
+    print("c5_u60000 E=20: long-chain dealing %+.3e, round-robin %+.3e, atomic %+.3e (oracle %.6f)"
+          % (r["rmse"]["delta"], r0["rmse"]["delta"], ra["rmse"]["delta"], g["rmse_by_epoch"][19]))
+    assert "+qlog" in r["config"]["workload"] and "+qlog" not in ra["config"]["workload"]
+    for x in (r, r0, ra):
         assert "chunks/epoch=8" in x["config"]["workload"]
         assert x["config"]["train_ratings_rank0"] == g["train_ratings"]
         assert x["rmse"]["reference_oracle_fp64"] == g["rmse_by_epoch"][19]
@@ -165,7 +173,7 @@ def test_c5_miniature_long_chain_dealing_within_1e3_of_committed_oracle(torch):
 
 @pytest.fixture(scope="module")
 def c5_small(torch):
-    return _bench("--shape", "c5", "--users", C5_USERS)
+    return _bench("--shape", "c5", "--users", C5_USERS, "--qlog", "0")  # (2 ranks: atomic)
 
 
 def test_c5_two_ranks_within_1e3_of_one(torch, c5_small):

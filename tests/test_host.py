@@ -663,3 +663,28 @@ def test_qlog_fold_layout_partitions_cold_and_hot_items():
             b0, b1 = lay["item_row_beg"][i], lay["item_row_beg"][i + 1]
             np.testing.assert_array_equal(lay["perm"][b0:b1], rows)
             np.testing.assert_array_equal(lay["users"][b0:b1], users[offs[i]:offs[i + 1]])
+
+
+def test_auto_qlog_rule():
+    """engine.auto_qlog (qlog=None): the SVD++ q log on ONE rank with several chunks of at most
+    QLOG_MAX_RATINGS_PER_ITEM_CHUNK ratings per item -- C5 (full: 125 chunks, shard: 16), ML-1M at
+    24+ chunks -- and the float-atomic schedule for ML-1M's default single chunk (C3), 16 chunks
+    (13.5 per item: +1.9e-3 measured), several ranks, the exchange path, duplicate items, SVD."""
+    from surprise_amd import _lib
+    from surprise_amd.engine import auto_qlog, default_chunks
+    A = _lib.MF_MODE_ATOMIC
+    ml1m = (800_167, 3706)
+    c5 = (989_997_254, 1_000_000)
+    c5_shard = (123_000_000, 1_000_000)
+    assert default_chunks("svdpp", "atomic", 10_000_000) == 125
+    assert auto_qlog("svdpp", A, *c5, 125, 1, None, False, False)
+    assert auto_qlog("svdpp", A, *c5_shard, 16, 1, None, False, False)
+    assert not auto_qlog("svdpp", A, *ml1m, 1, 1, None, False, False)  # C3
+    assert not auto_qlog("svdpp", A, *ml1m, 16, 1, None, False, False)
+    assert auto_qlog("svdpp", A, *ml1m, 24, 1, None, False, False)
+    assert not auto_qlog("svdpp", A, *c5_shard, 16, 8, None, False, False)  # several ranks
+    assert not auto_qlog("svdpp", A, *c5_shard, 16, 1, True, False, False)  # exchange (test)
+    assert not auto_qlog("svdpp", A, *c5_shard, 16, 1, None, True, False)   # duplicate items
+    assert not auto_qlog("svdpp", A, *c5_shard, 16, 1, None, False, True)   # deterministic
+    assert not auto_qlog("svd", _lib.MF_MODE_LOG, *c5_shard, 16, 1, None, False, False)
+    assert not auto_qlog("svdpp", _lib.MF_MODE_PLAIN, *c5_shard, 16, 1, None, False, False)

@@ -6,7 +6,8 @@
 2. The deterministic (one wave, the reference's order) SVD fit's cost on u1 vs the parallel
    schedule (K=20 E=5, K=100 E=20).
 
-Usage: python3 tools/probes/qlog_chunks_exact_speed.py OUT.jsonl [--no-c3]
+Usage: python3 tools/probes/qlog_chunks_exact_speed.py OUT.jsonl [--no-c3] [--no-u1]
+       [--chunks 1,2,4,8,16]
 """
 import json
 import os
@@ -36,7 +37,7 @@ def main():
     from surprise_amd import SVD, SVDpp
     golden_meta, _ = conftest.golden.__wrapped__()
     ts, test = conftest.u1.__wrapped__()
-    for name in ("svd_k20_e5", "svd_k100_e20", "svd_k100_e20_unbiased"):
+    for name in () if "--no-u1" in sys.argv else ("svd_k20_e5", "svd_k100_e20", "svd_k100_e20_unbiased"):
         case = golden_meta["cases"][name]
         for det in (False, True, False, True):  # (the first pair warms the code paths)
             t0 = time.perf_counter()
@@ -54,13 +55,16 @@ def main():
              delta=rmse(a.test(test)) - case["rmse"])
     if "--no-c3" in sys.argv:
         return
+    chunk_list = (1, 2, 4, 8, 16)
+    if "--chunks" in sys.argv:
+        chunk_list = tuple(int(x) for x in sys.argv[sys.argv.index("--chunks") + 1].split(","))
     from test_gpu_parity import _synthetic_fold, _oracle_rmse
     ts, test = _synthetic_fold("ml-1m")
     params = dict(n_factors=100, n_epochs=20, random_state=0)
     t0 = time.perf_counter()
     ref = _oracle_rmse("SVDpp", params, ts, test, affine=True)
     emit(probe="c3_oracle", rmse=ref, seconds=time.perf_counter() - t0)
-    for chunks in (1, 2, 4, 8, 16):
+    for chunks in chunk_list:
         for qlog in (False, True):
             a = SVDpp(**params, dtype="float32", chunks_per_epoch=chunks)
             a._engine_options = {"qlog": qlog}

@@ -104,8 +104,9 @@ if fetch and write and bench_line:
     shp = cfg.get("shape", "ml-1m")
     users = cfg.get("users_total", 0)
     key = bench.shape_key(shp, users if users and users < U_FULL.get(shp, 0) else 0)
-    name = "traffic_%s_k%d_%s%s.json" % (cfg["algo"], cfg["n_factors"], key,
-                                         "" if dt == "f32" else "_" + dt)
+    name = "traffic_%s_k%d_%s%s%s.json" % (cfg["algo"], cfg["n_factors"], key,
+                                           "" if dt == "f32" else "_" + dt,
+                                           "_qlog" if "+qlog" in cfg["workload"] else "")
     with open(os.path.join(prof, name), "w") as f:
         json.dump(traffic, f, indent=1)
 hit, miss = pmc("l2", "TCC_HIT_sum"), pmc("l2", "TCC_MISS_sum")
