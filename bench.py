@@ -129,9 +129,12 @@ def parse():
     p.add_argument("--light-replay-wpc", type=int, default=-1,
                    help="split chunk: the light group's replay waves per CU (engine option "
                         "light_replay_wpc; -1: the engine's default)")
-    p.add_argument("--log-nt", type=int, default=-1,
+    p.add_argument("--log-nt", default="-1", choices=("-1", "0", "1", "heavy", "light"),
                    help="the log's stores non-temporal (engine option log_nt; -1: the engine's "
-                        "size rule, 0 off, 1 on)")
+                        "size rule, 0 off, 1 on, heavy / light: that launch group only)")
+    p.add_argument("--item-align", type=int, default=0,
+                   help="item rows padded to a multiple of this many bytes (engine option "
+                        "item_align, timing probes; 0: the engine's 64)")
     p.add_argument("--stagger", type=int, default=-1,
                    help="checkpoint log: the chunk's users in two staggered halves (engine option "
                         "stagger; -1: the engine's policy, 0 off, 1 on)")
@@ -768,7 +771,9 @@ def main():
                        **({"xcd_split": bool(args.xcd_split)} if args.xcd_split >= 0 else {}),
                        **({"long_chain": args.long_chain} if args.long_chain >= 0 else {}),
                        **({"stagger": bool(args.stagger)} if args.stagger >= 0 else {}),
-                       **({"log_nt": bool(args.log_nt)} if args.log_nt >= 0 else {}),
+                       **({"item_align": args.item_align} if args.item_align else {}),
+                       **({"log_nt": args.log_nt if args.log_nt in ("heavy", "light")
+                           else bool(int(args.log_nt))} if args.log_nt != "-1" else {}),
                        **({"light_replay_wpc": args.light_replay_wpc}
                           if args.light_replay_wpc >= 0 else {}))
         eng.set_factors(pu, qi, yj=yj)

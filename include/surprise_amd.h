@@ -294,8 +294,16 @@ int mf_svd_epoch_gram(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched
 int mf_user_sq(const void *pu, int64_t n_rows, int32_t n_cols, int32_t ld, double *user_sq,
                int32_t dtype, void *stream);
 
+/* The {sum, count} statistic buffers below (out, stat_next) hold 2 doubles, plus MF_SQ_PARTS
+ * doubles of scratch after them when n_rows / n_users >= MF_SQ_PARTS_MIN: above that size the
+ * sum runs as MF_SQ_PARTS fixed-range partial sums (a launch of its own, on the same stream)
+ * added in order -- still bit-reproducible, at the chip's bandwidth instead of one workgroup's. */
+#define MF_SQ_PARTS 256
+#define MF_SQ_PARTS_MIN 65536
+
 /* out[0] = sum of user_sq[0..n_rows) in a fixed order, out[1] = n_rows * n_cols: the {sum,
- * count} pair mf_sumsq accumulates (here written, not added; bit-reproducible). */
+ * count} pair mf_sumsq accumulates (here written, not added; bit-reproducible).  out: 2 doubles
+ * (+ MF_SQ_PARTS scratch from MF_SQ_PARTS_MIN rows). */
 int mf_user_sq_reduce(const double *user_sq, int64_t n_rows, int32_t n_cols, double *out,
                       void *stream);
 
@@ -353,7 +361,8 @@ int mf_svdpp_qlog_fold(void *qb, int32_t ldq, int32_t n_factors, void *yj, int32
  *                   in factor columns, <p^2> = p2stat[0] / p2stat[1] (mf_sumsq's two doubles);
  *   MF_MERGE_RECENCY: the sums carry the recency weights (mf_recency_t); adds
  *                   lr o (S_i - W reg o qb[i]) with W = (1 - (1-eta)^N) / eta, the weights' sum.
- * stat_next (nullable, 2 device doubles, not p2stat): user_sq NULL: set to {0, 0} -- the next
+ * stat_next (nullable, 2 device doubles -- + MF_SQ_PARTS scratch from MF_SQ_PARTS_MIN users --,
+ * not p2stat): user_sq NULL: set to {0, 0} -- the next
  * chunk's mf_sumsq accumulator, cleared here instead of by a separate fill; user_sq != NULL
  * (mf_svd_epoch_sq's array, n_users rows): set to mf_user_sq_reduce's {sum, n_users * n_factors}
  * -- the next chunk's <p^2>, summed inside this launch (every epoch kernel of the chunk must have

@@ -26,6 +26,7 @@ MF_EPOCH_ERR_IN_ROW = 4  # checkpoint log: errors in the checkpoint rows' paddin
 MF_EPOCH_CKPT_NARROW = 16  # checkpoint log: rows of the factor columns only (errors in elog)
 MF_REPLAY_WPC_SHIFT = 16  # mf_log_replay flags bits 16..23: waves per CU (0: 16)
 MF_EPOCH_LOG_NT = 64  # the epoch kernels' log stores non-temporal (streamed past L2 / MALL)
+MF_SQ_PARTS = 256  # scratch doubles after a {sum, count} statistic buffer (from MF_SQ_PARTS_MIN rows)
 MF_HX_HELPER_TIMEOUT, MF_HX_CHAIN_FALLBACK = 1, 2  # mf_svdpp_epoch status word bits
 
 

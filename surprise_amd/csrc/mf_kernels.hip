@@ -1101,7 +1101,11 @@ __device__ __forceinline__ void epoch_body_la(
                 br[bk][d] = readlane(gr, d);
 #pragma unroll
                 for (int v = 0; v < G; ++v) bank[bk][d][v] = L::template lds<0>(q_rs, cq[v], off);
+#ifdef MF_SB_NO_BIAS_LOAD  // (timing probe only: what the row's bias line costs the gathers)
+                if constexpr (SB) bb[bk][d] = T(0);
+#else
                 if constexpr (SB) bb[bk][d] = Buf<T>::template lds<0>(q_rs, kbo, off);
+#endif
             }
         };
         auto flush = [&](const int j0p) {  // log rows j0p .. j0p + kB - 1
@@ -2130,10 +2134,9 @@ __global__ __launch_bounds__(kBlock) void sumsq_kernel(const T *__restrict__ x, 
     }
 }
 
-// out = {sum of sq[0..n) in a fixed order, n * K}, by one whole workgroup: per-thread strided sums
-// (8 loads in flight), then a fixed tree in LDS
-__device__ __forceinline__ void block_sum_sq(const double *__restrict__ sq, int64_t n, int K,
-                                             double *out)
+// sum of sq[0..n) in a fixed order by one whole workgroup (per-thread strided sums, 32 loads in
+// flight, then a fixed tree in LDS); the result in thread 0
+__device__ __forceinline__ double block_sum(const double *__restrict__ sq, int64_t n)
 {
     __shared__ double part[kBlock];
     double acc = 0;
@@ -2154,10 +2157,50 @@ __device__ __forceinline__ void block_sum_sq(const double *__restrict__ sq, int6
         if ((int)threadIdx.x < h) part[threadIdx.x] += part[threadIdx.x + h];
         __syncthreads();
     }
+    return part[0];
+}
+
+// The <p^2> statistic {sum of sq[0..n), n * K} for the next chunk.  Up to kSqPartsMin users one
+// workgroup sums them (fixed order).  Above it -- one workgroup's ~32 GB/s made the sum the tail
+// of every C5 fold (10M users: 80 MB, ~2.5 ms per chunk) -- user_sq_parts_kernel, launched just
+// before on the same stream, has left kSqParts fixed-range partial sums in out[2 ..], and thread
+// 0 adds them in order.  Either way bit-reproducible.
+constexpr int kSqParts = MF_SQ_PARTS;
+constexpr int64_t kSqPartsMin = MF_SQ_PARTS_MIN;
+__device__ __forceinline__ void block_sum_sq(const double *__restrict__ sq, int64_t n, int K,
+                                             double *out)
+{
+    if (n >= kSqPartsMin) {
+        if (threadIdx.x == 0) {
+            double t = 0;
+            for (int b = 0; b < kSqParts; ++b) t += out[2 + b];
+            out[0] = t;
+            out[1] = (double)n * K;
+        }
+        return;
+    }
+    const double t = block_sum(sq, n);
     if (threadIdx.x == 0) {
-        out[0] = part[0];
+        out[0] = t;
         out[1] = (double)n * K;
     }
+}
+
+// block b: the sum of sq over [n b / P, n (b + 1) / P) in a fixed order -> parts[b]
+__global__ __launch_bounds__(kBlock) void user_sq_parts_kernel(const double *__restrict__ sq,
+                                                               int64_t n, double *__restrict__ parts)
+{
+    const int64_t lo = n * blockIdx.x / kSqParts, hi = n * (blockIdx.x + 1) / kSqParts;
+    const double t = block_sum(sq + lo, hi - lo);
+    if (threadIdx.x == 0) parts[blockIdx.x] = t;
+}
+
+// the partial sums block_sum_sq reads above kSqPartsMin users (stat: 2 + kSqParts doubles)
+static int launch_sq_parts(const double *sq, int64_t n, double *stat, hipStream_t st)
+{
+    if (!sq || !stat || n < kSqPartsMin) return 0;
+    hipLaunchKernelGGL(user_sq_parts_kernel, dim3(kSqParts), dim3(kBlock), 0, st, sq, n, stat + 2);
+    return check_launch("user_sq_parts_kernel");
 }
 
 // Per-user sum of squares of the factor columns (fp64), one wave per row: the initial values of
@@ -4437,7 +4480,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 932; }
+int mf_version(void) { return 933; }
 
 #ifndef MF_SOURCE_HASH
 #define MF_SOURCE_HASH "unknown"
@@ -4644,6 +4687,7 @@ int mf_user_sq_reduce(const double *user_sq, int64_t n_rows, int32_t n_cols, dou
 {
     if (!out || n_rows < 0 || n_cols < 0 || (n_rows > 0 && !user_sq))
         return set_err(MF_E_ARG, "bad argument");
+    if (int e = launch_sq_parts(user_sq, n_rows, out, (hipStream_t)stream)) return e;
     hipLaunchKernelGGL(user_sq_reduce_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream,
                        user_sq, n_rows, n_cols, out);
     return check_launch("user_sq_reduce_kernel");
@@ -4806,6 +4850,7 @@ int mf_svdpp_qlog_fold(void *qb, int32_t ldq, int32_t n_factors, void *yj, int32
     const int g = grid_for_waves(nb < cap ? nb : cap) + (stat_next ? 1 : 0);
     const int gh = hot ? grid_for_waves(default_waves(lay->n_hot_pieces)) : 0;
     hipStream_t st = (hipStream_t)stream;
+    if (int e = launch_sq_parts(user_sq, n_users, stat_next, st)) return e;
     auto run = [&](auto tag_t) -> int {
         using T = decltype(tag_t);
         // the hot items' pre-passes: piece sums of their gradient rows (log_reduce_kernel) and
@@ -4883,6 +4928,7 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
     // (+1: the block that sums / clears stat_next)
     const int g = grid_for_waves(default_waves(n_items)) + (stat_next ? 1 : 0);
     hipStream_t st = (hipStream_t)stream;
+    if (int e = launch_sq_parts(user_sq, n_users, stat_next, st)) return e;
     const double eta_b = count_rule ? hp->lr_bi * (1.0 + hp->reg_bi) : 0.0;
     const double lr_c = count_rule ? hp->lr_qi : 0.0, reg_c = count_rule ? hp->reg_qi : 0.0;
     const double lr_f = hp ? hp->lr_qi : 0.0, reg_f = hp ? hp->reg_qi : 0.0;

@@ -432,7 +432,7 @@ class MFEngine(ItemSync, Predictor):
                  helpers=None, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
                  replay_rows=None, gram=None, xcd_split=None, qlog=None, top=None,
                  exchange=None, long_chain=256, overlap_q=True, fused=True, stagger=None,
-                 light_replay_wpc=0, log_nt=None):
+                 light_replay_wpc=0, log_nt=None, item_align=None):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -488,7 +488,10 @@ class MFEngine(ItemSync, Predictor):
                       CU (0: the library's 16) -- fewer leave the heavy chains' memory path
                       quieter while the replay still ends before them
           log_nt      the checkpoint log's / SVD++ q log's rows stored non-temporal (streamed
-                      past L2 / MALL: MF_EPOCH_LOG_NT); None: where the log is >= LOG_NT_MIN_BYTES
+                      past L2 / MALL: MF_EPOCH_LOG_NT); None: where the log is >= LOG_NT_MIN_BYTES;
+                      "heavy" / "light": only that group's launch of a split chunk
+          item_align  item rows padded to a multiple of this many bytes (timing probes; None:
+                      ITEM_ROW_ALIGN)
                       (C4: 27 GB of log evicted the item table from the MALL -- epoch kernel
                       18.0 -> 14.6 ms; ML-1M's 0.3-GB log: +3%, off)
           fused       SVD++ q log on one rank: the chunk's fold in one pass over the items
@@ -538,6 +541,9 @@ class MFEngine(ItemSync, Predictor):
         # (the user-bias column of the SVD log's lookahead body: that schedule's rows only)
         self.ldq = default_ldq(self.K, self.dtype,
                                user_bias_col=algo == "svd" and self.mode == _lib.MF_MODE_LOG)
+        if item_align:  # (timing probes: item rows padded to this many bytes)
+            per = int(item_align) // esz0
+            self.ldq = -(-self.ldq // per) * per
         # item-side merge rule: the log fold weights each logged gradient by its recency
         # (MF_MERGE_RECENCY); SVD++'s snapshot-delta merge of q / b across ranks
         # carries each rank's delta through the later ranks' steps (mf_item_merge's
@@ -794,7 +800,9 @@ class MFEngine(ItemSync, Predictor):
         self._pos0 = []  # (recency, several ranks: per chunk, the item counts of earlier ranks)
         # {sum pu^2, count} of the chunk start, double-buffered: chunk t accumulates into slot
         # t % 2 and its fold clears slot (t + 1) % 2 for the next chunk (no separate fill)
-        self._works = torch.zeros(2, 2, dtype=torch.float64, device=dev)
+        # (+ MF_SQ_PARTS doubles of scratch: the fixed-range partial sums of user_sq that
+        # mf_log_apply / mf_svdpp_qlog_fold / mf_user_sq_reduce add in order from 64k users)
+        self._works = torch.zeros(2, 2 + _lib.MF_SQ_PARTS, dtype=torch.float64, device=dev)
         self._wt = 0
         self._work_cleared = True
         self.work = self._works[0]
@@ -864,7 +872,10 @@ class MFEngine(ItemSync, Predictor):
                 self.elog = z(64 if self.err_in_row else k_hi - k_lo + 64)
                 self._elog_base = self.elog.data_ptr() - (0 if self.err_in_row else k_lo * esz)
         lbytes = self.qlog.numel() * self.qlog.element_size() if self.qlog is not None else 0
-        self.log_nt = bool(log_nt) if log_nt is not None else lbytes >= self.LOG_NT_MIN_BYTES
+        # log_nt "heavy" / "light": only that launch group's log stores (split chunks)
+        self._nt_group = log_nt if log_nt in ("heavy", "light") else None
+        self.log_nt = (bool(log_nt) if log_nt is not None and self._nt_group is None
+                       else lbytes >= self.LOG_NT_MIN_BYTES and self._nt_group is None)
         self.log_nt = self.log_nt and (self.ckpt or self.qlog_pp)
         snap_q = self.multi and self.mode != _lib.MF_MODE_LOG
         self.qb_s = z(I, ldq) if snap_q else None
@@ -1120,8 +1131,10 @@ class MFEngine(ItemSync, Predictor):
         if "end_r" in ev:
             ev["end_r"].record(self.stream)
 
-    def _epoch_sq(self, sched, n_sched, n_waves, st, xmask=0):
-        """The checkpoint-log epoch kernel keeping user_sq current (mf_svd_epoch_sq)."""
+    def _epoch_sq(self, sched, n_sched, n_waves, st, xmask=0, group=None):
+        """The checkpoint-log epoch kernel keeping user_sq current (mf_svd_epoch_sq); group: the
+        split chunk's launch group ("heavy" / "light"), for log_nt's per-group form."""
+        nt = self.log_nt or (group is not None and group == self._nt_group)
         _lib.call("mf_svd_epoch_sq", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                   self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb), self.ldq,
                   self.K, int(self.biased), ctypes.byref(self._hyper),
@@ -1130,14 +1143,14 @@ class MFEngine(ItemSync, Predictor):
                   (_lib.MF_EPOCH_DUP_ITEMS if self.dup_items else 0) |
                   (_lib.MF_EPOCH_ERR_IN_ROW if self.err_in_row else 0) |
                   (_lib.MF_EPOCH_CKPT_NARROW if self.narrow else 0) |
-                  (_lib.MF_EPOCH_LOG_NT if self.log_nt else 0) |
+                  (_lib.MF_EPOCH_LOG_NT if nt else 0) |
                   (xmask << _lib.MF_EPOCH_XCD_SHIFT), self.dtype, st)
 
     def _heavy_epoch(self, sched, n_sched, st, xmask=0):
         """The heavy users' epoch launch: the blocked solve (gram) or one lookahead chain per
         user."""
         if not self.gram:
-            self._epoch_sq(sched, n_sched, n_sched, st, xmask)
+            self._epoch_sq(sched, n_sched, n_sched, st, xmask, group="heavy")
             return
         _lib.call("mf_svd_epoch_gram", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                   self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb), self.ldq,
@@ -1177,7 +1190,7 @@ class MFEngine(ItemSync, Predictor):
             # B's epoch kernel runs beside A's replay; main joins side before the fold
             side = self.side
             sh = ctypes.c_void_p(side.cuda_stream)
-            self._epoch_sq(hv["sched"], hv["sched"].numel(), lw, st)
+            self._epoch_sq(hv["sched"], hv["sched"].numel(), lw, st, group="heavy")
             if "end" in ev:
                 ev["end"].record(self.stream)
             a_done = torch.cuda.Event()
@@ -1185,7 +1198,7 @@ class MFEngine(ItemSync, Predictor):
             side.wait_event(a_done)
             if "l_start" in ev:
                 ev["l_start"].record(side)
-            self._epoch_sq(ls, ln, lw, sh)
+            self._epoch_sq(ls, ln, lw, sh, group="light")
             if "l_end" in ev:
                 ev["l_end"].record(side)
             self._reduce_log(lg, self.sums.data_ptr(), sh)
@@ -1212,7 +1225,7 @@ class MFEngine(ItemSync, Predictor):
                 ev["end"].record(self.stream)
             if "l_start" in ev:  # (the light epoch kernel's own span, on its stream)
                 ev["l_start"].record(side)
-            self._epoch_sq(ls, ln, lw, sh, lx)
+            self._epoch_sq(ls, ln, lw, sh, lx, group="light")
             if "l_end" in ev:
                 ev["l_end"].record(side)
             jw = self._join_words
@@ -1376,7 +1389,7 @@ class MFEngine(ItemSync, Predictor):
         if self._stat_global:  # (summed by the previous chunk's exchange)
             self._stat_global = False
             return False
-        ctx.all_reduce_sum(self.work)
+        ctx.all_reduce_sum(self.work[:2])
         return True
 
     def _prepare(self, ctx):
@@ -1551,7 +1564,7 @@ class MFEngine(ItemSync, Predictor):
         self._delta_into(bufs)
         ride = self._stat_rides()
         if ride:  # the next chunk's <p^2> partial (summed by _delta_into) rides in the buffer
-            flat[-2:].copy_(self._works[self._wt % 2])
+            flat[-2:].copy_(self._works[self._wt % 2][:2])
         ev = getattr(self, "_sync_events", None)
         if ev:
             ev["ar_begin"].record(self.stream)
@@ -1559,7 +1572,7 @@ class MFEngine(ItemSync, Predictor):
         if ev:
             ev["ar_end"].record(self.stream)
         if ride:
-            self._works[self._wt % 2].copy_(flat[-2:])
+            self._works[self._wt % 2][:2].copy_(flat[-2:])
             self._stat_global = True
         self._apply(bufs)
 

@@ -1040,3 +1040,77 @@ def test_test_metrics_equal_reference_pipeline(torch, u1):
         cols = RatingColumns(np.array(ru, dtype=object), np.array(ri, dtype=object), rr)
         np.testing.assert_allclose(algo.test_metrics(cols), (rmse, mae), rtol=0, atol=1e-12)
         assert [p.est for p in algo.test(cols)] == [p.est for p in fast]
+
+
+def _many_users_csr(n_users=70_000, n_items=400, seed=3):
+    """A trainset past MF_SQ_PARTS_MIN users (the <p^2> statistic summed in fixed-range parts):
+    4-11 ratings per user over a few hundred items."""
+    from surprise_amd import Trainset
+    rng = np.random.RandomState(seed)
+    rows = [np.sort(rng.choice(n_items, rng.randint(4, 12), replace=False)) for _ in range(n_users)]
+    row_ptr = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
+    items = np.concatenate(rows).astype(np.int32)
+    ratings = rng.randint(1, 6, len(items)).astype(np.float64)
+    return Trainset.from_csr(row_ptr, items, ratings, n_items), (row_ptr, items, ratings)
+
+
+def test_user_sq_sum_in_fixed_parts_above_64k_rows(torch):
+    """mf_user_sq_reduce from MF_SQ_PARTS_MIN rows: MF_SQ_PARTS fixed-range partial sums (their
+    own launch) added in order -- the sum to 1e-12 relative, the count exact, bit-identical on a
+    second call; below the threshold the one-workgroup sum."""
+    import ctypes
+    from surprise_amd import _lib
+    for n in (1000, 65_535, 65_536, 300_001):
+        x = torch.rand(n, dtype=torch.float64, device="cuda")
+        outs = []
+        for _ in range(2):
+            out = torch.full((2 + _lib.MF_SQ_PARTS,), -1.0, dtype=torch.float64, device="cuda")
+            _lib.call("mf_user_sq_reduce", ctypes.c_void_p(x.data_ptr()), n, 7,
+                      ctypes.c_void_p(out.data_ptr()), None)
+            torch.cuda.synchronize()
+            outs.append(out.cpu().numpy())
+        ref = float(x.sum())
+        assert abs(outs[0][0] - ref) <= 1e-12 * ref, (n, outs[0][0], ref)
+        assert outs[0][1] == n * 7
+        assert outs[0][0] == outs[1][0]
+        if n >= 65_536:  # (the parts: each fixed range's own sum)
+            xs = x.cpu().numpy()
+            b = np.arange(_lib.MF_SQ_PARTS + 1) * n // _lib.MF_SQ_PARTS
+            np.testing.assert_allclose(outs[0][2:], [xs[b[i]:b[i + 1]].sum()
+                                                     for i in range(_lib.MF_SQ_PARTS)], rtol=1e-12)
+        else:
+            assert (outs[0][2:] == -1.0).all()  # (scratch untouched below the threshold)
+
+
+def test_log_and_qlog_past_64k_users_match_their_oracles(torch):
+    """The fold's next-chunk <p^2> summed in parts (70k users): SVD's checkpoint log (2 chunks)
+    and SVD++'s q log with the fused fold (3 chunks) in fp64 equal oracle_svd_sgd_deltalog(merge=3)
+    / oracle_svdpp_sgd_stalelog on the same chunking to 1e-9."""
+    from surprise_amd import SVD, SVDpp
+    from surprise_amd.dist import chunk_users
+    ts, (row_ptr, items, ratings) = _many_users_csr()
+    assert ts.n_users >= 65_536
+    for algo_cls, chunks in ((SVD, 2), (SVDpp, 3)):
+        params = dict(n_factors=8, n_epochs=2, random_state=0)
+        cou = np.zeros(ts.n_users, np.int32)
+        for c, us in enumerate(chunk_users(np.arange(ts.n_users), row_ptr, chunks)):
+            cou[us] = c
+        if algo_cls is SVD:
+            _, f = run_oracle_log("SVD", params, row_ptr, items, ratings, ts.n_items,
+                                  ts.global_mean, cou, chunks, merge=3)
+            algo = SVD(**params, dtype="float64", deterministic=False, chunks_per_epoch=chunks)
+            keys = ("pu", "qi", "bu", "bi")
+        else:
+            _, f = run_oracle_stalelog(params, row_ptr, items, ratings, ts.n_items,
+                                       ts.global_mean, cou, chunks)
+            algo = SVDpp(**params, dtype="float64", chunks_per_epoch=chunks)
+            algo._engine_options = {"qlog": True}
+            keys = ("pu", "qi", "yj", "bu", "bi")
+        algo.fit(ts)
+        if algo_cls is SVDpp:
+            assert algo._engine.qlog_pp and algo._engine._fused_fold()
+        else:
+            assert algo._engine.ckpt
+        for k in keys:
+            np.testing.assert_allclose(getattr(algo, k), f[k], rtol=0, atol=1e-9,
+                                       err_msg="%s %s" % (algo_cls.__name__, k))
