@@ -132,6 +132,9 @@ def parse():
     p.add_argument("--log-nt", default="-1", choices=("-1", "0", "1", "heavy", "light"),
                    help="the log's stores non-temporal (engine option log_nt; -1: the engine's "
                         "size rule, 0 off, 1 on, heavy / light: that launch group only)")
+    p.add_argument("--bias-mirror", type=int, default=-1,
+                   help="checkpoint log with SB rows: the item biases from a mirror array, rows "
+                        "on 128-B lines (engine option bias_mirror; -1: the engine's default, on)")
     p.add_argument("--item-align", type=int, default=0,
                    help="item rows padded to a multiple of this many bytes (engine option "
                         "item_align, timing probes; 0: the engine's 64)")
@@ -772,6 +775,8 @@ def main():
                        **({"long_chain": args.long_chain} if args.long_chain >= 0 else {}),
                        **({"stagger": bool(args.stagger)} if args.stagger >= 0 else {}),
                        **({"item_align": args.item_align} if args.item_align else {}),
+                       **({"bias_mirror": bool(args.bias_mirror)} if args.bias_mirror >= 0
+                          else {}),
                        **({"log_nt": args.log_nt if args.log_nt in ("heavy", "light")
                            else bool(int(args.log_nt))} if args.log_nt != "-1" else {}),
                        **({"light_replay_wpc": args.light_replay_wpc}

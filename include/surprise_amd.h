@@ -266,11 +266,16 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
  * keeping user_sq current: user_sq[u] = sum_{c < n_factors} p_u[c]^2 (fp64) of every trained
  * user's row after the epoch -- the <p^2> statistic of the log fold's count-aware weights
  * without another pass over pu (mf_user_sq_reduce).  Same item-side results as mf_svd_epoch.
+ * item_bias (nullable, [n_items] of dtype): with MF_EPOCH_CKPT_NARROW rows whose factor columns
+ * fill whole 512-B lane groups (fp32 K=128, fp64 K=64 / 128), the item biases are read from
+ * item_bias[i] -- a mirror of qb[i][n_factors], kept by mf_log_apply's bias_out -- instead of
+ * from the row, so a row gather touches only its factor lines (with ldq a multiple of 128 B).
  */
 int mf_svd_epoch_sq(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
                     void *bu, int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
                     const mf_hyper_t *hp, void *qlog, void *elog, double *user_sq,
-                    int32_t n_waves, int32_t flags, int32_t dtype, void *stream);
+                    const void *item_bias, int32_t n_waves, int32_t flags, int32_t dtype,
+                    void *stream);
 
 /*
  * mf_svd_epoch_sq for the heaviest users by a blocked solve (replaces the same loop,
@@ -366,14 +371,15 @@ int mf_svdpp_qlog_fold(void *qb, int32_t ldq, int32_t n_factors, void *yj, int32
  * chunk's mf_sumsq accumulator, cleared here instead of by a separate fill; user_sq != NULL
  * (mf_svd_epoch_sq's array, n_users rows): set to mf_user_sq_reduce's {sum, n_users * n_factors}
  * -- the next chunk's <p^2>, summed inside this launch (every epoch kernel of the chunk must have
- * finished before it).
+ * finished before it).  bias_out (nullable, [n_items], needs apply and bias_col >= 0): also
+ * receives each item's new qb[i][bias_col] (mf_svd_epoch_sq's item_bias mirror).
  */
 int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32_t bias_col,
                  const void *sums, const int32_t *item_piece_ptr, const void *sums2,
                  const int32_t *item_piece_ptr2, const int32_t *totals, const mf_hyper_t *hp,
                  const double *p2stat, int32_t rule, void *delta_out, int32_t apply,
-                 double *stat_next, const double *user_sq, int64_t n_users, int32_t dtype,
-                 void *stream);
+                 double *stat_next, const double *user_sq, int64_t n_users, void *bias_out,
+                 int32_t dtype, void *stream);
 
 /* Merge rules of mf_item_merge. */
 #define MF_MERGE_SUM   0 /* delta = sum_r d_r                                                      */

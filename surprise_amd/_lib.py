@@ -81,7 +81,7 @@ SIGNATURES = {
     "mf_svdpp_y_fold": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp,
                         _i32, _vp],
     "mf_svd_epoch_sq": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32,
-                        _i32, ctypes.POINTER(MfHyper), _vp, _vp, _vp, _i32, _i32, _i32, _vp],
+                        _i32, ctypes.POINTER(MfHyper), _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_svd_epoch_gram": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _i32,
                           _i32, ctypes.POINTER(MfHyper), _vp, _vp, _i32, _i32, _i32, _vp],
     "mf_sumsq": [_vp, _i64, _i32, _i32, _vp, _i32, _vp],
@@ -97,7 +97,8 @@ SIGNATURES = {
                            _vp, ctypes.POINTER(MfHyper), _vp, _vp, _i32, _vp, _vp, _i64, _i32,
                            _vp],
     "mf_log_apply": [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
-                     ctypes.POINTER(MfHyper), _vp, _i32, _vp, _i32, _vp, _vp, _i64, _i32, _vp],
+                     ctypes.POINTER(MfHyper), _vp, _i32, _vp, _i32, _vp, _vp, _i64, _vp, _i32,
+                     _vp],
     "mf_item_merge": [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
                       ctypes.POINTER(MfHyper), _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp],
     "mf_item_apply": [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _vp],

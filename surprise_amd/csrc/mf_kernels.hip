@@ -979,7 +979,7 @@ __device__ __forceinline__ void epoch_body_la(
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *qlog, T *elog, int K,
     int biased, Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, double *psq,
-    int err_col, int ck_ld)
+    int err_col, int ck_ld, const T *__restrict__ ibias = nullptr)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -1037,6 +1037,9 @@ __device__ __forceinline__ void epoch_body_la(
                             ? (uint32_t)(((lane >> 1) * ldq + err_col + (lane & 1)) * sizeof(T))
                             : kLogOob;
     const rsrc_t q_rs = make_rsrc(qb, q_oob);
+    // SB: where the item biases come from -- the mirror (gid * size) or the rows (column K)
+    const rsrc_t b_rs = ibias ? make_rsrc(ibias, (uint32_t)n_items * sizeof(T)) : q_rs;
+    const uint32_t b_mul = ibias ? (uint32_t)sizeof(T) : qrow, b_add = ibias ? 0u : kbo;
     const int prio_len = (int)(row_ptr[sched[0] + 1] - row_ptr[sched[0]]);
 
     auto do_user = [&](const int u) {
@@ -1073,11 +1076,13 @@ __device__ __forceinline__ void epoch_body_la(
         auto grp_load = [&](int j0, uint32_t &go, T &gr) {
             int j = j0 + (lane & (kB - 1));
             j = j < n ? j : n - 1;
+            // (the item id itself: fill() scales it to the row offset, and the SB body with an
+            // item-bias mirror indexes the mirror by it)
             if constexpr (MF_STREAM_AUX == kNt) {
-                go = (uint32_t)__builtin_nontemporal_load(it + j) * qrow;
+                go = (uint32_t)__builtin_nontemporal_load(it + j);
                 gr = __builtin_nontemporal_load(rt + j);
             } else {
-                go = (uint32_t)it[j] * qrow;
+                go = (uint32_t)it[j];
                 gr = rt[j];
             }
         };
@@ -1097,15 +1102,17 @@ __device__ __forceinline__ void epoch_body_la(
         auto fill = [&](const int bk, const uint32_t go, const T gr) {
 #pragma unroll
             for (int d = 0; d < kB; ++d) {
-                const uint32_t off = readlane((int)go, d);
+                const uint32_t gid = readlane((int)go, d);
+                const uint32_t off = gid * qrow;
                 br[bk][d] = readlane(gr, d);
 #pragma unroll
                 for (int v = 0; v < G; ++v) bank[bk][d][v] = L::template lds<0>(q_rs, cq[v], off);
-#ifdef MF_SB_NO_BIAS_LOAD  // (timing probe only: what the row's bias line costs the gathers)
-                if constexpr (SB) bb[bk][d] = T(0);
-#else
-                if constexpr (SB) bb[bk][d] = Buf<T>::template lds<0>(q_rs, kbo, off);
-#endif
+                // SB: the item bias from the mirror (an L2-resident array) where one is given, so
+                // that a gather touches only the row's factor lines -- 4 of 128 B at fp32 K=128
+                // with 128-B rows instead of 5 (profiles/r5u_probes.txt); else from the row's
+                // column K.  A vector load either way: a scalar load's wait (lgkmcnt counts out
+                // of order) would hold every bank for the next bank's bias loads
+                if constexpr (SB) bb[bk][d] = Buf<T>::template lds<0>(b_rs, b_add, gid * b_mul);
             }
         };
         auto flush = [&](const int j0p) {  // log rows j0p .. j0p + kB - 1
@@ -1883,9 +1890,10 @@ __global__ __launch_bounds__(kBlock) void mf_epoch_kernel(MF_EPOCH_PARAMS)
 template <typename T, int G, bool ER, bool SB = false, bool NT = false>
 __global__ __launch_bounds__(kBlock) void mf_ckpt_epoch_kernel(MF_EPOCH_PARAMS)
 {
+    // (yj: SVD has none -- the slot carries the SB body's item-bias mirror, nullable)
     epoch_body_la<T, G, true, ER, SB, NT>(row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb,
                                       ldq, qlog, elog, K, biased, hp, n_items, n_waves_req, xmask,
-                                      psq, err_col, ck_ld);
+                                      psq, err_col, ck_ld, (const T *)yj);
 }
 
 // SVD++ with helper waves (MF_SVDPP_HELPERS): workgroup = chain wave 0 + H atomic waves (3, or 1
@@ -2734,7 +2742,7 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     int count_rule, double eta_bias, double lr_fac, double reg_fac, double lr_f, double reg_f,
     double lr_b, double reg_b, const double *__restrict__ p2stat, T *__restrict__ delta_out,
     int apply, double *__restrict__ stat_next, const double *__restrict__ user_sq, int64_t n_sq,
-    int sq_cols)
+    int sq_cols, T *__restrict__ bias_out)
 {
     // the next chunk's {sum |p_u|^2, count}: the launch's extra FIRST block, which does no item
     // (dispatched first: at 2M users the one-block sum is the launch's longest piece of work)
@@ -2830,13 +2838,16 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
                 const bool b = c == bias_col;
                 const double w = b ? w_bias : w_fac;
                 // the log holds gradients g_k = err_k pe_k: sum_k d_k = lr (S - N reg q)
+                T nq;
                 if (rec) {
-                    qb[x] = q[v] + (T)(b ? lr_b : lr_f) *
-                                       (acc[v] - (T)(w * N) * (T)(b ? reg_b : reg_f) * q[v]);
+                    nq = q[v] + (T)(b ? lr_b : lr_f) *
+                                    (acc[v] - (T)(w * N) * (T)(b ? reg_b : reg_f) * q[v]);
                 } else {
                     const T d = (T)(b ? lr_b : lr_f) * (acc[v] - (T)N * (T)(b ? reg_b : reg_f) * q[v]);
-                    qb[x] = q[v] + (T)w * d;
+                    nq = q[v] + (T)w * d;
                 }
+                qb[x] = nq;
+                if (b && bias_out) bias_out[i] = nq;  // (the item-bias mirror of the SB epoch)
             }
         }
     }
@@ -4480,7 +4491,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 933; }
+int mf_version(void) { return 934; }
 
 #ifndef MF_SOURCE_HASH
 #define MF_SOURCE_HASH "unknown"
@@ -4552,12 +4563,14 @@ int mf_svd_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
 int mf_svd_epoch_sq(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
                     void *bu, int32_t ldu, void *qb, int32_t ldq, int32_t n_factors, int32_t biased,
                     const mf_hyper_t *hp, void *qlog, void *elog, double *user_sq,
-                    int32_t n_waves, int32_t flags, int32_t dtype, void *stream)
+                    const void *item_bias, int32_t n_waves, int32_t flags, int32_t dtype,
+                    void *stream)
 {
     if (!elog || !user_sq) return set_err(MF_E_ARG, "mf_svd_epoch_sq needs elog and user_sq");
-    return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, nullptr, qlog, elog,
-                               n_factors, biased, hp, MF_MODE_LOG, n_waves, flags, dtype, stream,
-                               user_sq);
+    // (item_bias rides in the yj slot, which SVD does not use)
+    return launch_epoch<false>(csr, sched, n_sched, pu, bu, ldu, qb, ldq,
+                               const_cast<void *>(item_bias), qlog, elog, n_factors, biased, hp,
+                               MF_MODE_LOG, n_waves, flags, dtype, stream, user_sq);
 }
 
 int mf_svd_epoch_gram(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
@@ -4907,9 +4920,10 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
                  const void *sums, const int32_t *item_piece_ptr, const void *sums2,
                  const int32_t *item_piece_ptr2, const int32_t *totals, const mf_hyper_t *hp,
                  const double *p2stat, int32_t rule, void *delta_out, int32_t apply,
-                 double *stat_next, const double *user_sq, int64_t n_users, int32_t dtype,
-                 void *stream)
+                 double *stat_next, const double *user_sq, int64_t n_users, void *bias_out,
+                 int32_t dtype, void *stream)
 {
+    if (bias_out && (!apply || bias_col < 0)) return set_err(MF_E_ARG, "bias_out needs apply and bias_col");
     StopEvent stop(stream);  // (mf_launch_event)
     if (stat_next && stat_next == p2stat) return set_err(MF_E_ARG, "stat_next aliases p2stat");
     if (user_sq && (!stat_next || n_users < 0)) return set_err(MF_E_ARG, "user_sq needs stat_next");
@@ -4942,14 +4956,14 @@ int mf_log_apply(void *qb, int32_t n_items, int32_t ld, int32_t n_factors, int32
                                item_piece_ptr, (const T *)sums2, item_piece_ptr2, totals,
                                count_rule, eta_b, lr_c, reg_c, lr_f,
                                reg_f, lr_b, reg_b, p2stat, (T *)delta_out, apply, stat_next,
-                               user_sq, (int64_t)n_users, n_factors);
+                               user_sq, (int64_t)n_users, n_factors, (T *)bias_out);
             else
                 launch_ev(stop.take(), (log_apply_kernel<T, decltype(vc)::value, false>), dim3(g), dim3(kBlock),
                                st, (T *)qb, n_items, ld, n_factors, bias_col, (const T *)sums,
                                item_piece_ptr, (const T *)sums2, item_piece_ptr2, totals,
                                count_rule, eta_b, lr_c, reg_c, lr_f,
                                reg_f, lr_b, reg_b, p2stat, (T *)delta_out, apply, stat_next,
-                               user_sq, (int64_t)n_users, n_factors);
+                               user_sq, (int64_t)n_users, n_factors, (T *)bias_out);
             return check_launch("log_apply_kernel");
         });
     };

@@ -76,7 +76,7 @@ def default_chunks(algo: str, mode: str, n_users_total: int, world: int = 1) -> 
 # rank) at 16 chunks -- 13.5 ratings per item and chunk -- +1.9e-3, at 24 / 32 / 64 / 128 chunks
 # (9.0 / 6.7 / 3.4 / 1.7) -2.6e-4 / -2.6e-4 / -2.9e-4 / -1.3e-4; C5 (7.7 per item and chunk)
 # within 1e-3 of the sequential oracle on the shard, 0.94543 vs the atomic schedule's 0.94641 on
-# the full C5.  At C5 it is the faster schedule (shard 70.5 vs 89.7 ms, full 802 vs 845 ms).
+# the full C5.  At C5 it is the faster schedule (shard 70.5 vs 89.7 ms, full 658 vs 845 ms).
 QLOG_MAX_RATINGS_PER_ITEM_CHUNK = 10.0
 
 
@@ -432,7 +432,7 @@ class MFEngine(ItemSync, Predictor):
                  helpers=None, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
                  replay_rows=None, gram=None, xcd_split=None, qlog=None, top=None,
                  exchange=None, long_chain=256, overlap_q=True, fused=True, stagger=None,
-                 light_replay_wpc=0, log_nt=None, item_align=None):
+                 light_replay_wpc=0, log_nt=None, item_align=None, bias_mirror=True):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -492,6 +492,9 @@ class MFEngine(ItemSync, Predictor):
                       "heavy" / "light": only that group's launch of a split chunk
           item_align  item rows padded to a multiple of this many bytes (timing probes; None:
                       ITEM_ROW_ALIGN)
+          bias_mirror checkpoint log with SB rows (fp32 K=128, fp64 K=64 / 128): the item biases
+                      read from a mirror array, the item rows on whole 128-B lines; False: from
+                      the rows
                       (C4: 27 GB of log evicted the item table from the MALL -- epoch kernel
                       18.0 -> 14.6 ms; ML-1M's 0.3-GB log: +3%, off)
           fused       SVD++ q log on one rank: the chunk's fold in one pass over the items
@@ -619,6 +622,15 @@ class MFEngine(ItemSync, Predictor):
             narrow = lc * esz % 128 == 0 or esz_q > 1024
         self.narrow = self.ckpt and bool(narrow) and 0 < lc < self.ldq
         self.ldc = lc if self.narrow else self.ldq  # the checkpoint rows' stride
+        # SB rows (narrow, the factor columns fill whole 512-B lane groups: fp32 K=128, fp64 K=64
+        # / 128): the epoch kernel reads each item's bias from a mirror array (mf_log_apply's
+        # bias_out keeps it) and the item rows are padded to whole 128-B lines, so a row gather
+        # touches only the factor lines -- 4 instead of 5 at fp32 K=128 (C4 epoch kernel -9%,
+        # profiles/r5u_probes.txt)
+        self.sb_mirror = self.narrow and (self.K * esz) % 512 == 0 and bool(bias_mirror)
+        if self.sb_mirror:
+            per = 128 // esz
+            self.ldq = -(-self.ldq // per) * per
         # (read-only after construction: elog is sized for it)
         self._err_in_row = (self.ckpt and not self.narrow and e0 + 2 <= self.ldq
                             and bool(err_in_row))
@@ -825,6 +837,7 @@ class MFEngine(ItemSync, Predictor):
         # between chunks; self.qb is the model's table, rows 0 .. n_items - 1)
         self._qb_alloc = z(2 * I if self.hot_list is not None else I, ldq)
         self.qb = self._qb_alloc[:I]
+        self.ibias = z(max(I, 1)) if self.sb_mirror else None  # (qb[:, K]'s mirror, SB rows)
         self.yj = z(I, ld) if algo == "svdpp" else None
         self.ycbuf = z(U, ld) if self.ydefer else None
         if self.ydefer:
@@ -942,6 +955,8 @@ class MFEngine(ItemSync, Predictor):
                                          np.asarray(bi, np.float64)).to(self.dev, self.tdt))
         if self.algo == "svd" and self.is_log:  # (the lookahead body's user-bias column)
             self.qb[:, K + 1] = 1
+        if self.ibias is not None:
+            self.ibias.copy_(self.qb[:, K])
         if self.yj is not None:
             put(self.yj, yj)
         if self.qb_s is not None:
@@ -1016,7 +1031,12 @@ class MFEngine(ItemSync, Predictor):
 
     # ------------------------------------------------------------------ kernels
     def _ptr(self, t):
-        return ctypes.c_void_p(t.data_ptr())
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+    def _bias_out(self, apply):
+        """mf_log_apply's bias_out: the SB epoch's item-bias mirror, where the fold moves b_i."""
+        ib = getattr(self, "ibias", None)
+        return self._ptr(ib) if apply and self.biased and ib is not None else None
 
     def _st(self):
         return ctypes.c_void_p(self.stream.cuda_stream)
@@ -1139,7 +1159,7 @@ class MFEngine(ItemSync, Predictor):
                   self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb), self.ldq,
                   self.K, int(self.biased), ctypes.byref(self._hyper),
                   ctypes.c_void_p(self._qlog_base), ctypes.c_void_p(self._elog_base),
-                  self._ptr(self.user_sq), n_waves,
+                  self._ptr(self.user_sq), self._ptr(self.ibias), n_waves,
                   (_lib.MF_EPOCH_DUP_ITEMS if self.dup_items else 0) |
                   (_lib.MF_EPOCH_ERR_IN_ROW if self.err_in_row else 0) |
                   (_lib.MF_EPOCH_CKPT_NARROW if self.narrow else 0) |
@@ -1306,7 +1326,7 @@ class MFEngine(ItemSync, Predictor):
                   ctypes.c_void_p(sums_m), self._ptr(md["ipp"]),
                   self._ptr(self._totals()[self._chunk]), ctypes.byref(self._hyper),
                   self._ptr(self.work), self._log_rule(), self._ptr(self.sbuf), 0, None, None, 0,
-                  self.dtype, sh)
+                  None, self.dtype, sh)
         if not native:
             self._ev_record("join", side)
         self._reduce_log(hv, sums_h, st)  # (the top users' replay: every XCD)
@@ -1476,7 +1496,8 @@ class MFEngine(ItemSync, Predictor):
                   self._ptr(self._totals()[c]), ctypes.byref(self._hyper),
                   self._ptr(self.work), self._log_rule(),
                   None if delta_out is None else self._ptr(delta_out), int(apply),
-                  *self._stat_args(apply if stat is None else stat), self.dtype, self._st())
+                  *self._stat_args(apply if stat is None else stat),
+                  self._bias_out(apply), self.dtype, self._st())
 
     def _bind_fork(self):
         """The next mf_log_apply completes the "fork" event the side stream waits for (the item
@@ -1662,7 +1683,8 @@ class MFEngine(ItemSync, Predictor):
                       self._bias_col, self._ptr(bufs[0]), None, None, None,
                       self._ptr(self._totals()[c]),
                       ctypes.byref(self._hyper), self._ptr(self.work), self._log_rule(), None,
-                      1, *self._stat_args(not self._stat_rides()), self.dtype, st)
+                      1, *self._stat_args(not self._stat_rides()), self._bias_out(True),
+                      self.dtype, st)
             x = 1
         for tab, snap, ld, _, rule in self._snap_tables():
             if rule == "affine":

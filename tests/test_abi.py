@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_without_device(lib):
-    assert lib.mf_version() == 933
+    assert lib.mf_version() == 934
     rc = lib.mf_item_affine(None, None, 10, 16, None, None, None, 0, 0, None)
     assert rc == 1001 and b"bad argument" in lib.mf_last_error()
     # argument validation happens before any device call
@@ -44,8 +44,11 @@ def test_version_and_error_without_device(lib):
     assert rc == 1001 and b"null argument" in lib.mf_last_error()
     assert lib.mf_ckpt_interval() in (2, 4, 8, 16)
     rc = lib.mf_log_apply(None, 10, 16, 10, 10, None, None, None, None, None, None, None, 1, None,
-                          1, None, None, 0, 0, None)
+                          1, None, None, 0, None, 0, None)
     assert rc == 1001 and b"count-aware rule needs" in lib.mf_last_error()
+    rc = lib.mf_log_apply(None, 10, 16, 10, -1, None, None, None, None, None, None, None, 0, None,
+                          1, None, None, 0, 1, 0, None)  # (bias_out without a bias column)
+    assert rc == 1001 and b"bias_out needs apply and bias_col" in lib.mf_last_error()
     rc = lib.mf_log_reduce(None, 16, 11, None, None, 5, None, None, None, None, 0, None)
     assert rc == 1001 and b"null argument" in lib.mf_last_error()
     rec = _lib.MfRecency(0, 0, 0, 0)
@@ -57,7 +60,7 @@ def test_version_and_error_without_device(lib):
     rc = lib.mf_sumsq(None, 4, 8, 4, None, 0, None)
     assert rc == 1001
     rc = lib.mf_svd_epoch_sq(ctypes.byref(csr), None, 1, None, None, 16, None, 16, 10, 1, None,
-                             None, None, None, 0, 0, 0, None)
+                             None, None, None, None, 0, 0, 0, None)
     assert rc == 1001 and b"needs elog and user_sq" in lib.mf_last_error()
     assert lib.mf_user_sq(None, 4, 8, 16, None, 0, None) == 1001
     assert lib.mf_user_sq_reduce(None, 4, 8, None, None) == 1001

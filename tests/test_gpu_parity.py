@@ -879,32 +879,46 @@ def test_staggered_halves_match_deltalog_oracle(torch, u1, K):
         np.testing.assert_allclose(got[k], ref, rtol=0, atol=1e-9, err_msg=k)
 
 
-@pytest.mark.parametrize("heavy", [0.0, 16])
-def test_fp64_k128_checkpoint_rows_match_deltalog_oracle(torch, golden, u1, heavy):
+@pytest.mark.parametrize("K,heavy,mirror", [(128, 0.0, True), (128, 16, True),
+                                             (128, 0.0, False), (64, 16, True), (64, 0.0, False)])
+def test_fp64_k128_checkpoint_rows_match_deltalog_oracle(torch, golden, u1, K, heavy, mirror):
     """fp64 K=128 (the C4 factor count at the reference's precision, mf.pyx:206-239): item rows
     of 1088 B, so the checkpoint log runs in narrow form -- rows of the 128 factor columns (two
     whole lane groups), both biases beside the groups in the epoch kernel, the replay's third
-    lane group holding the bias column alone.  Factors equal oracle_svd_sgd_deltalog (merge=3)
-    to 1e-9, with and without the heavy users' split."""
+    lane group holding the bias column alone.  K=64 is the one-group form (512-B rows).  mirror:
+    the epoch kernel reads the item biases from the mirror mf_log_apply keeps (bias_out) and the
+    item rows lie on whole 128-B lines (the default); else from the rows.  Factors equal
+    oracle_svd_sgd_deltalog (merge=3) to 1e-9, with and without the heavy users' split, over 2
+    chunks (the mirror crosses the chunk boundary)."""
+    from surprise_amd.dist import chunk_users
     from surprise_amd.engine import MFEngine
     ts, test = u1
-    K = 128
     row_ptr, items, ratings = ts.csr()
     hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
                  reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
     rng = np.random.RandomState(8)
     pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
+    bi0 = rng.normal(0, .1, ts.n_items)  # (a non-zero start, so a stale mirror would show)
     eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype="float64",
-                   mode="log", heavy=heavy)
-    assert eng.ckpt and eng.narrow and eng.ldq * 8 > 1024 and eng.ldc == K
-    eng.set_factors(pu0, qi0)
+                   mode="log", heavy=heavy, n_chunks=2, bias_mirror=mirror)
+    assert eng.ckpt and eng.narrow and eng.ldc == K and eng.sb_mirror == mirror
+    assert (eng.ldq * 8) % 128 == 0 if mirror else True
+    if K == 128:
+        assert eng.ldq * 8 > 1024
+    eng.set_factors(pu0, qi0, bi=bi0)
     eng.run_epochs(3)
     got = eng.get_factors()
     hp = orc.hyper(**{k: v for k, v in hyper.items() if k != "global_mean"})
+    cou = np.zeros(ts.n_users, np.int32)
+    for c, us in enumerate(chunk_users(np.arange(ts.n_users), row_ptr, 2)):
+        cou[us] = c
     pu, qi, bu, bi = orc.svd_sgd_deltalog(row_ptr, items, ratings, ts.n_items, K, 3, True,
-                                          ts.global_mean, hp, pu0.copy(), qi0.copy(), merge=3)
+                                          ts.global_mean, hp, pu0.copy(), qi0.copy(), cou, 2,
+                                          merge=3, bi=bi0.copy())
     for k, ref in (("pu", pu), ("qi", qi), ("bu", bu), ("bi", bi)):
         np.testing.assert_allclose(got[k], ref, rtol=0, atol=1e-9, err_msg=k)
+    if mirror:  # (the mirror holds the table's biases after the last fold)
+        np.testing.assert_array_equal(eng.ibias.cpu().numpy(), eng.qb[:, K].cpu().numpy())
 
 
 @pytest.mark.parametrize("rows,dtype,narrow,heavy", [(256, "float64", False, 0.0),
