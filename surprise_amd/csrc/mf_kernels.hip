@@ -1037,9 +1037,8 @@ __device__ __forceinline__ void epoch_body_la(
                             ? (uint32_t)(((lane >> 1) * ldq + err_col + (lane & 1)) * sizeof(T))
                             : kLogOob;
     const rsrc_t q_rs = make_rsrc(qb, q_oob);
-    // SB: where the item biases come from -- the mirror (gid * size) or the rows (column K)
-    const rsrc_t b_rs = ibias ? make_rsrc(ibias, (uint32_t)n_items * sizeof(T)) : q_rs;
-    const uint32_t b_mul = ibias ? (uint32_t)sizeof(T) : qrow, b_add = ibias ? 0u : kbo;
+    // SB with the item-bias mirror (the rsrc is only read where ibias is given)
+    const rsrc_t ib_rs = make_rsrc(ibias, (uint32_t)n_items * sizeof(T));
     const int prio_len = (int)(row_ptr[sched[0] + 1] - row_ptr[sched[0]]);
 
     auto do_user = [&](const int u) {
@@ -1088,7 +1087,7 @@ __device__ __forceinline__ void epoch_body_la(
         };
         vec bank[2][kB][G];
         T br[2][kB];
-        T bb[SB ? 2 : 1][SB ? kB : 1];  // SB: each entry's item bias (every lane the same)
+        T bbv[SB ? 2 : 1];  // SB: lane d holds the item bias of the bank's row d
         // log rows of the current bank: CK: per pair (c, c + 1) of the user's ratings (c even) the
         // row p_{c+1} at log row c, and err_k in lane k mod kB of ev; otherwise every rating's
         // gradient row g_k = err_k p_k
@@ -1100,6 +1099,18 @@ __device__ __forceinline__ void epoch_body_la(
         uint32_t go_q[kAhead - 1];
         T gr_q[kAhead - 1];
         auto fill = [&](const int bk, const uint32_t go, const T gr) {
+            // SB: the bank's item biases in ONE per-lane gather, issued before its rows (a wait
+            // for them is not a wait for the rows): from the mirror -- an L2-resident array --
+            // where one is given, so that a row gather touches only the row's factor lines (4
+            // of 128 B at fp32 K=128 on 128-B rows instead of 5, profiles/r5u_probes.txt), else
+            // from the rows' column K.  (Selecting between the two buffer resources instead of
+            // branching miscompiled: every SB parity test failed, tools/runs/r5w_gpu.sh.)
+            if constexpr (SB) {
+                if (ibias)
+                    bbv[bk] = Buf<T>::template ld<0>(ib_rs, go * (uint32_t)sizeof(T));
+                else
+                    bbv[bk] = Buf<T>::template ld<0>(q_rs, go * qrow + kbo);
+            }
 #pragma unroll
             for (int d = 0; d < kB; ++d) {
                 const uint32_t gid = readlane((int)go, d);
@@ -1107,12 +1118,6 @@ __device__ __forceinline__ void epoch_body_la(
                 br[bk][d] = readlane(gr, d);
 #pragma unroll
                 for (int v = 0; v < G; ++v) bank[bk][d][v] = L::template lds<0>(q_rs, cq[v], off);
-                // SB: the item bias from the mirror (an L2-resident array) where one is given, so
-                // that a gather touches only the row's factor lines -- 4 of 128 B at fp32 K=128
-                // with 128-B rows instead of 5 (profiles/r5u_probes.txt); else from the row's
-                // column K.  A vector load either way: a scalar load's wait (lgkmcnt counts out
-                // of order) would hold every bank for the next bank's bias loads
-                if constexpr (SB) bb[bk][d] = Buf<T>::template lds<0>(b_rs, b_add, gid * b_mul);
             }
         };
         auto flush = [&](const int j0p) {  // log rows j0p .. j0p + kB - 1
@@ -1162,7 +1167,7 @@ __device__ __forceinline__ void epoch_body_la(
                 part += bank[0][0][v] * p0[v];
             }
             X = wave_sum_u(L::hsum(part));
-            if constexpr (SB) X += bb[0][0] + C0_p;
+            if constexpr (SB) X += readlane(bbv[0], 0) + C0_p;
         }
 
         auto step = [&](auto full_c, auto bank_c, const int j0, const int d) {
@@ -1198,7 +1203,7 @@ __device__ __forceinline__ void epoch_body_la(
             if constexpr (SB) {  // c_k = C0_{k-1} + lr_bu err_{k-1}; C0_k = abu c_k + kb
                 C0 = abu * (C0_p + lr_bu * err_p) + kb;
                 const int bn = d + 1 < kB ? bk : bk ^ 1, dn = d + 1 < kB ? d + 1 : 0;
-                Xn += bb[bn][dn] + C0;
+                Xn += readlane(bbv[bn], dn) + C0;
                 Yn += lr_bu;
             }
             if (FULL) {
