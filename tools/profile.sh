@@ -11,7 +11,7 @@ shift
 EXTRA="$*"
 mkdir -p gpurun_out
 B="bench.py --no-cpu-baseline --no-rmse --no-svdpp --no-predict --no-chain-probe --no-c4 --dtype ${DTYPE:-f64}"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 $B --steps 20 --warmup 3 $EXTRA > gpurun_out/prof_${TAG}_bench.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 $B --steps 20 --warmup 3 $EXTRA --detail gpurun_out/prof_${TAG}_detail.json > gpurun_out/prof_${TAG}_bench.log 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d gpurun_out/pmc_fetch_$TAG -o run -- python3 $B --steps 5 --warmup 1 $EXTRA > gpurun_out/pmc_fetch_${TAG}.log 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d gpurun_out/pmc_write_$TAG -o run -- python3 $B --steps 5 --warmup 1 $EXTRA > gpurun_out/pmc_write_${TAG}.log 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -T --output-format csv -d gpurun_out/pmc_l2_$TAG -o run -- python3 $B --steps 5 --warmup 1 $EXTRA > gpurun_out/pmc_l2_${TAG}.log 2>&1 || exit $?

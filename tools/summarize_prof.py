@@ -50,10 +50,14 @@ if os.path.exists(bench):
         summary["bench_line_under_profiler"] = json.loads(lines[-1])
         # (the stdout line is the compact one since round 5: the full dictionary is its detail file,
         # which every pass of tools/profile.sh rewrites with the same configuration)
-        det = summary["bench_line_under_profiler"].get("detail")
+        line = summary["bench_line_under_profiler"]
+        det = line.get("detail")
         if det and os.path.exists(os.path.join(ROOT, det)):
             with open(os.path.join(ROOT, det)) as f:
-                summary["bench_line_under_profiler"] = json.load(f)
+                full = json.load(f)
+            # (a detail file another profile's pass rewrote: keep the compact line)
+            if full.get("config", {}).get("workload") == line["config"]["workload"]:
+                summary["bench_line_under_profiler"] = full
 
 
 def pmc(kind, counter):
@@ -90,16 +94,21 @@ if fetch and write and bench_line:
     cfg = bench_line["config"]
     rl = bench_line["roofline"]
     n_up = cfg["train_ratings_rank0"]  # one epoch per step: every training rating once
+    import bench
+    ex = rl.get("step", {}).get("executed_bytes")
     traffic = {"bytes_per_step": total, "bytes_per_update": total / n_up,
-               "algorithmic_bytes_per_update": rl["survey_8d"]["bytes_per_update"],
-               "executed_bytes_per_update": rl["step"]["executed_bytes"] / n_up,
+               "algorithmic_bytes_per_update": (rl["survey_8d"]["bytes_per_update"]
+                                                if "survey_8d" in rl else
+                                                bench.algorithmic_bytes_per_update(
+                                                    cfg["algo"], cfg["n_factors"],
+                                                    bench.ELEM_BYTES[cfg.get("dtype", "f32")])),
+               "executed_bytes_per_update": ex / n_up if ex else None,
                "per_kernel": per, "setup_kernels_excluded": setup,
                "source": "profiles/%s_summary.json (2 x FETCH_SIZE + WRITE_SIZE, separate --pmc "
                          "passes of %d epochs, every kernel of the step)" % (tag, PMC_STEPS),
                "workload": cfg["workload"]}
     summary["traffic"] = traffic
     dt = cfg.get("dtype", "f32")
-    import bench
     U_FULL = {"c4": 2_000_000, "c5": 10_000_000}
     shp = cfg.get("shape", "ml-1m")
     users = cfg.get("users_total", 0)
