@@ -1598,7 +1598,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
             if constexpr (HOT) gh = hot[i];
         };
         vec bank[2][kB][G];
-        T bb[SB ? 2 : 1][SB ? kB : 1];  // SB: each entry's item bias (every lane the same)
+        T bbv[SB ? 2 : 1];  // SB: lane d holds the item bias of the bank's entry d
         vec rep[HOT ? 2 : 1][HOT ? kB : 1][G];  // HOT: the replica rows of a bank's entries
         T br[2][kB];
         uint32_t bo[2][kB];
@@ -1612,6 +1612,8 @@ __device__ __forceinline__ void epoch_body_pp_la(
         auto fill = [&](const int bk, const uint32_t go, const T gr, const int gh) {
             if constexpr (HOT)
                 hm[bk] = (uint32_t)__builtin_amdgcn_ballot_w64(gh != 0) & ((1u << kB) - 1u);
+            // SB: the bank's item biases in one per-lane gather before its rows (epoch_body_la)
+            if constexpr (SB) bbv[bk] = Buf<T>::template ld<kSc1>(q_rs, go + kbo);
 #pragma unroll
             for (int d = 0; d < kB; ++d) {
                 const uint32_t off = readlane((int)go, d);
@@ -1619,7 +1621,6 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 br[bk][d] = readlane(gr, d);
 #pragma unroll
                 for (int v = 0; v < G; ++v) bank[bk][d][v] = L::template lds<kSc1>(q_rs, cq[v], off);
-                if constexpr (SB) bb[bk][d] = Buf<T>::template lds<kSc1>(q_rs, kbo, off);
                 if constexpr (HOT) {  // (a uniform branch: most entries are not hot)
                     if ((hm[bk] >> d) & 1u) {
 #pragma unroll
@@ -1721,7 +1722,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 part += qrow_of(0, 0, v) * (p0[v] + m0[v]);
             }
             X = wave_sum_u(L::hsum(part));
-            if constexpr (SB) X += bb[0][0];
+            if constexpr (SB) X += readlane(bbv[0], 0);
         }
         auto step = [&](auto full_c, auto bank_c, const int j0, const int d) {
             constexpr bool FULL = decltype(full_c)::value;
@@ -1756,7 +1757,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
             }
             if constexpr (SB) {
                 if constexpr (LQ) dlb[d] = err;
-                else dlb[d] = hp.lr_bi * (err - hp.reg_bi * bb[bk][d]);  // mf.pyx:489
+                else dlb[d] = hp.lr_bi * (err - hp.reg_bi * readlane(bbv[bk], d));  // mf.pyx:489
             }
             const bool hot_d = HOT && to_rep && ((hm[bk] >> d) & 1u);
             if constexpr (LQ)  // (past the user's segment: dropped)
@@ -1765,7 +1766,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 dlo[d] = valid ? (hot_d ? bo[bk][d] + rep_shift : bo[bk][d]) : bo[bk][d] + q_oob;
             T Xn, Yn;
             wave_sum2_u(L::hsum(px), L::hsum(py), Xn, Yn);  // X_{k+1}, Y_{k+1}
-            if constexpr (SB) Xn += bb[bn][dn];  // (the next item's bias: s_k's column K is 1)
+            if constexpr (SB) Xn += readlane(bbv[bn], dn);  // (the next item's bias: s_k's column K is 1)
             err_p = valid ? err : err_p;
             c0_p = valid ? c0 : c0_p;
             X = valid ? Xn : X;
