@@ -1128,3 +1128,31 @@ def test_log_and_qlog_past_64k_users_match_their_oracles(torch):
         for k in keys:
             np.testing.assert_allclose(getattr(algo, k), f[k], rtol=0, atol=1e-9,
                                        err_msg="%s %s" % (algo_cls.__name__, k))
+
+
+@pytest.mark.parametrize("lr_yj,reg_yj", [(None, None), (.004, None), (None, .05)])
+def test_svdpp_shared_step_chain_and_general_chain_match_stalelog_oracle(torch, u1, lr_yj, reg_yj):
+    """SVD++'s chain carries s = p + m alone where p and m take the same step (lr_pu = lr_yj and
+    reg_pu = reg_yj: the defaults), p_n and m_n recovered from a^n (p_0 - m_0) at the user's end;
+    with other values it carries p and m apart.  Both on the q log in fp64 against
+    oracle_svdpp_sgd_stalelog at 1e-9 (K=64: the item bias beside the lane group)."""
+    from surprise_amd import SVDpp
+    from surprise_amd.dist import chunk_users
+    ts, test = u1
+    row_ptr, items, ratings = ts.csr()
+    params = dict(n_factors=64, n_epochs=3, random_state=0)
+    if lr_yj is not None:
+        params["lr_yj"] = lr_yj
+    if reg_yj is not None:
+        params["reg_yj"] = reg_yj
+    cou = np.zeros(ts.n_users, np.int32)
+    for c, us in enumerate(chunk_users(np.arange(ts.n_users), row_ptr, 2)):
+        cou[us] = c
+    P, f = run_oracle_stalelog(params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
+                               cou, 2)
+    algo = SVDpp(**params, dtype="float64", chunks_per_epoch=2)
+    algo._engine_options = {"qlog": True}
+    algo.fit(ts)
+    assert algo._engine.qlog_pp
+    for k in ("pu", "qi", "yj", "bu", "bi"):
+        np.testing.assert_allclose(getattr(algo, k), f[k], rtol=0, atol=1e-9, err_msg=k)
