@@ -1461,7 +1461,7 @@ __device__ void pp_ring_helper(PPRing<T, G, H> *ring, int h, T *qb, int ldq, int
 // after the chunk with the recency weights, as the SVD gradient log (oracle:
 // oracle_svdpp_sgd_stalelog with every item stale).  No float atomic, no helper wave.
 template <typename T, int G, bool HX, bool HOT = false, bool SB = false, int H = kHxHelpers,
-          bool LQ = false, bool NT = false>
+          bool LQ = false, bool NT = false, bool SS = false>
 __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
@@ -1710,15 +1710,23 @@ __device__ __forceinline__ void epoch_body_pp_la(
         // Mp = dc o m_{k-1}, Dpp = lrp o q_{k-1}, Dmp = lry o q_{k-1}, X = X_k, Yb = Y_k + lr_bu
         // (k = 0: err_{-1} = 0, c0_{-1} = c_0, Pp = p_0, Mp = m_0, X_0 = <q_0, p_0 + m_0>)
         T err_p = T(0), c0_p = hp.gm + bu0, X, Yb = T(0);
-        vec Pp[G], Mp[G], Dpp[G], Dmp[G];
+        // SS (lr_pu = lr_yj and reg_pu = reg_yj, the defaults): p and m take the same step, so
+        // only s = p + m is carried -- Pp holds a o s_{k-1}, Dpp (lrp + lry) o q_{k-1} -- and
+        // p - m decays as a^k (p_0 - m_0) with no data in it: p_n, m_n come back at the end.
+        // Half the chain's vector work per rating, and four fewer row-sized registers.
+        vec Pp[G], Mp[SS ? 1 : G], Dpp[G], Dmp[SS ? 1 : G];
         {
             vec part = L::splat(T(0));
 #pragma unroll
             for (int v = 0; v < G; ++v) {
-                Pp[v] = p0[v];
-                Mp[v] = m0[v];
+                if constexpr (SS) {
+                    Pp[v] = p0[v] + m0[v];
+                } else {
+                    Pp[v] = p0[v];
+                    Mp[v] = m0[v];
+                    Dmp[v] = L::splat(T(0));
+                }
                 Dpp[v] = L::splat(T(0));
-                Dmp[v] = L::splat(T(0));
                 part += qrow_of(0, 0, v) * (p0[v] + m0[v]);
             }
             X = wave_sum_u(L::hsum(part));
@@ -1739,19 +1747,29 @@ __device__ __forceinline__ void epoch_body_pp_la(
             }
             const T err = (br[bk][d] - c0_p) - X - err_p * Yb;  // mf.pyx:483
             const T c0 = abu * (lr_bu * err_p + c0_p) + kb;     // mf.pyx:486, one rating late
-            vec P[G], M[G], Dp[G], Dm[G], px = L::splat(T(0)), py = L::splat(T(0));
+            vec P[G], M[SS ? 1 : G], Dp[G], Dm[SS ? 1 : G], px = L::splat(T(0)),
+                py = L::splat(T(0));
 #pragma unroll
             for (int v = 0; v < G; ++v) {
                 const vec q = qrow_of(bk, d, v);
-                const vec pk = Pp[v] + err_p * Dpp[v];  // p_k, m_k (one rating late)
-                const vec mk = Mp[v] + err_p * Dmp[v];
-                const vec sk = pk + mk;                 // puf + u_impl (mf.pyx:491-493)
-                P[v] = ap[v] * pk;
-                M[v] = dc * mk;
-                Dp[v] = lrp[v] * q;
-                Dm[v] = lry[v] * q;
-                px += qn[v] * (P[v] + M[v]);
-                py += qn[v] * (lrpy[v] * q);
+                vec sk;
+                if constexpr (SS) {  // s_k = a o s_{k-1} + err_{k-1} (lrp + lry) o q_{k-1}
+                    sk = Pp[v] + err_p * Dpp[v];
+                    P[v] = ap[v] * sk;
+                    Dp[v] = lrpy[v] * q;
+                    px += qn[v] * P[v];
+                    py += qn[v] * Dp[v];
+                } else {
+                    const vec pk = Pp[v] + err_p * Dpp[v];  // p_k, m_k (one rating late)
+                    const vec mk = Mp[v] + err_p * Dmp[v];
+                    sk = pk + mk;                           // puf + u_impl (mf.pyx:491-493)
+                    P[v] = ap[v] * pk;
+                    M[v] = dc * mk;
+                    Dp[v] = lrp[v] * q;
+                    Dm[v] = lry[v] * q;
+                    px += qn[v] * (P[v] + M[v]);
+                    py += qn[v] * (lrpy[v] * q);
+                }
                 if constexpr (LQ) dl[d][v] = err * sk;  // the gradient (the fold applies lr, reg)
                 else dl[d][v] = err * (lrq[v] * sk) + nrq[v] * q;  // mf.pyx:489, :492
             }
@@ -1774,9 +1792,11 @@ __device__ __forceinline__ void epoch_body_pp_la(
 #pragma unroll
             for (int v = 0; v < G; ++v) {
                 Pp[v] = valid ? P[v] : Pp[v];
-                Mp[v] = valid ? M[v] : Mp[v];
                 Dpp[v] = valid ? Dp[v] : Dpp[v];
-                Dmp[v] = valid ? Dm[v] : Dmp[v];
+                if constexpr (!SS) {
+                    Mp[v] = valid ? M[v] : Mp[v];
+                    Dmp[v] = valid ? Dm[v] : Dmp[v];
+                }
             }
         };
         int j0 = 0;
@@ -1826,9 +1846,18 @@ __device__ __forceinline__ void epoch_body_pp_la(
         double sq = 0;  // LQ with psq: |p_n|^2 over the factor columns (the fold's <p^2>)
 #pragma unroll
         for (int v = 0; v < G; ++v) {
-            const vec pn = Pp[v] + err_p * Dpp[v];
+            vec pn, mn;
+            if constexpr (SS) {  // p_n - m_n = a^n (p_0 - m_0) (column K: 1, both ways)
+                const vec sn = Pp[v] + err_p * Dpp[v];
+                const vec dn = A * (p0[v] - m0[v]) + (T(1) - A) * one[v];
+                pn = T(0.5) * (sn + dn);
+                mn = T(0.5) * (sn - dn);
+            } else {
+                pn = Pp[v] + err_p * Dpp[v];
+                mn = Mp[v] + err_p * Dmp[v];
+            }
             L::template st<0>(p_rs, cu[v], pn);
-            cacc[v] = ((Mp[v] + err_p * Dmp[v]) - A * m0[v]) * rs_n;
+            cacc[v] = (mn - A * m0[v]) * rs_n;
             if constexpr (LQ) {
 #pragma unroll
                 for (int e = 0; e < W; ++e) {
@@ -1909,7 +1938,7 @@ __global__ __launch_bounds__(kBlock) void mf_ckpt_epoch_kernel(MF_EPOCH_PARAMS)
 // SB: the lane groups cover the K factor columns only and the item bias (column K) is carried as
 // a scalar per rating (fp32 K=128: one lane group instead of two -- half the vector work and the
 // registers of a bank of 8 rows)
-template <typename T, int G, bool HOT, bool SB = false, int H = kHxHelpers>
+template <typename T, int G, bool HOT, bool SB = false, int H = kHxHelpers, bool SS = false>
 __global__ __launch_bounds__(kWave * (1 + H)) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS,
                                                                      int32_t *status,
                                                                      const uint8_t *hot)
@@ -1923,9 +1952,9 @@ __global__ __launch_bounds__(kWave * (1 + H)) void mf_svdpp_hx_kernel(MF_EPOCH_P
     }
     __syncthreads();
     if (w == 0) {
-        epoch_body_pp_la<T, G, true, HOT, SB, H>(row_ptr, items, ratings, sched, n_sched, pu, bu,
-                                                 ldu, qb, ldq, yj, elog, K, hp, n_items,
-                                                 n_waves_req, 0, &ring, status, hot);
+        epoch_body_pp_la<T, G, true, HOT, SB, H, false, false, SS>(
+            row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, elog, K, hp,
+            n_items, n_waves_req, 0, &ring, status, hot);
         if (blockIdx.x >= n_waves_req) lds_store(&ring.done, 1);  // (no chain in this workgroup)
     } else {
         pp_ring_helper<T, G, SB, H>(&ring, w - 1, qb, ldq, (HOT ? 2 : 1) * n_items, status, K);
@@ -1934,11 +1963,11 @@ __global__ __launch_bounds__(kWave * (1 + H)) void mf_svdpp_hx_kernel(MF_EPOCH_P
 
 // SVD++ with the q log (mf_svdpp_epoch_qlog): every wave a user chain, the item rows read-only,
 // each rating's gradient row stored to the chunk's log (urow[u]: the user's first log row)
-template <typename T, int G, bool SB, bool NT = false>
+template <typename T, int G, bool SB, bool NT = false, bool SS = false>
 __global__ __launch_bounds__(kBlock) void mf_svdpp_qlog_kernel(MF_EPOCH_PARAMS,
                                                               const int64_t *urow)
 {
-    epoch_body_pp_la<T, G, false, false, SB, 1, true, NT>(
+    epoch_body_pp_la<T, G, false, false, SB, 1, true, NT, SS>(
         row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, elog, K, hp, n_items,
         n_waves_req, xmask, (PPRing<T, G, 1> *)nullptr, nullptr, nullptr, qlog, urow, psq);
 }
@@ -1986,16 +2015,26 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     const bool sb = hx && !hot && whole;
     // ... and the SVD checkpoint epoch with narrow rows (the rows hold the factor columns only)
     const bool sbk = !PP && M == kLog && elog && sb_rows;
+    // SVD++: p and m take the same step where lr_pu = lr_yj and reg_pu = reg_yj (the reference's
+    // defaults, lr_all / reg_all): the shared-step chain (epoch_body_pp_la SS)
+    const bool ss = PP && hp->lr_pu == hp->lr_yj && hp->reg_pu == hp->reg_yj;
     return dispatch_g<T>(sb || sbk || (urow && whole) ? K : ldq, [&](auto gc) -> int {
         constexpr int V = decltype(gc)::value;
         if constexpr (PP && M == kAtomic && V <= kLaMaxG) {
             if (hx) {  // one workgroup per chain: wave 0 trains, waves 1..hx issue the q atomics
-                auto kern = hx == 1 ? (hot ? mf_svdpp_hx_kernel<T, V, true, false, 1>
-                                       : sb  ? mf_svdpp_hx_kernel<T, V, false, true, 1>
-                                             : mf_svdpp_hx_kernel<T, V, false, false, 1>)
-                          : hot ? mf_svdpp_hx_kernel<T, V, true>
-                          : sb  ? mf_svdpp_hx_kernel<T, V, false, true>
-                                : mf_svdpp_hx_kernel<T, V, false>;
+                // (ss: p and m share their step -- the shared-step chain of epoch_body_pp_la)
+                auto kern = hx == 1 ? (hot ? (ss ? mf_svdpp_hx_kernel<T, V, true, false, 1, true>
+                                                 : mf_svdpp_hx_kernel<T, V, true, false, 1>)
+                                       : sb  ? (ss ? mf_svdpp_hx_kernel<T, V, false, true, 1, true>
+                                                   : mf_svdpp_hx_kernel<T, V, false, true, 1>)
+                                             : (ss ? mf_svdpp_hx_kernel<T, V, false, false, 1, true>
+                                                   : mf_svdpp_hx_kernel<T, V, false, false, 1>))
+                          : hot ? (ss ? mf_svdpp_hx_kernel<T, V, true, false, kHxHelpers, true>
+                                      : mf_svdpp_hx_kernel<T, V, true>)
+                          : sb  ? (ss ? mf_svdpp_hx_kernel<T, V, false, true, kHxHelpers, true>
+                                      : mf_svdpp_hx_kernel<T, V, false, true>)
+                                : (ss ? mf_svdpp_hx_kernel<T, V, false, false, kHxHelpers, true>
+                                      : mf_svdpp_hx_kernel<T, V, false>);
                 hipLaunchKernelGGL(kern, dim3(waves), dim3(kWave * (1 + hx)), 0,
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
@@ -2009,10 +2048,14 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
         }
         if constexpr (PP && M == kLog && V <= kLaMaxG) {
             if (urow) {  // the q log: a user chain per wave, gradient rows to the chunk's log
-                auto kern = whole ? (nt ? mf_svdpp_qlog_kernel<T, V, true, true>
-                                        : mf_svdpp_qlog_kernel<T, V, true>)
-                                  : (nt ? mf_svdpp_qlog_kernel<T, V, false, true>
-                                        : mf_svdpp_qlog_kernel<T, V, false>);
+                auto kern = whole ? (nt ? (ss ? mf_svdpp_qlog_kernel<T, V, true, true, true>
+                                              : mf_svdpp_qlog_kernel<T, V, true, true>)
+                                        : (ss ? mf_svdpp_qlog_kernel<T, V, true, false, true>
+                                              : mf_svdpp_qlog_kernel<T, V, true>))
+                                  : (nt ? (ss ? mf_svdpp_qlog_kernel<T, V, false, true, true>
+                                              : mf_svdpp_qlog_kernel<T, V, false, true>)
+                                        : (ss ? mf_svdpp_qlog_kernel<T, V, false, false, true>
+                                              : mf_svdpp_qlog_kernel<T, V, false>));
                 hipLaunchKernelGGL(kern, dim3(grid_for_waves_x(waves, xmask)), dim3(kBlock), 0,
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
