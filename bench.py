@@ -132,6 +132,10 @@ def parse():
     p.add_argument("--log-nt", default="-1", choices=("-1", "0", "1", "heavy", "light"),
                    help="the log's stores non-temporal (engine option log_nt; -1: the engine's "
                         "size rule, 0 off, 1 on, heavy / light: that launch group only)")
+    p.add_argument("--cold-share", type=float, default=-1,
+                   help="SVD++ helper-wave launch: the least-rated items holding this share of a "
+                        "chunk's ratings on the cold log (engine option cold_share; -1: the "
+                        "engine's default)")
     p.add_argument("--bias-mirror", type=int, default=-1,
                    help="checkpoint log with SB rows: the item biases from a mirror array, rows "
                         "on 128-B lines (engine option bias_mirror; -1: the engine's default, on)")
@@ -775,6 +779,8 @@ def main():
                        **({"long_chain": args.long_chain} if args.long_chain >= 0 else {}),
                        **({"stagger": bool(args.stagger)} if args.stagger >= 0 else {}),
                        **({"item_align": args.item_align} if args.item_align else {}),
+                       **({"cold_share": args.cold_share} if args.cold_share >= 0 and
+                          a == "svdpp" else {}),
                        **({"bias_mirror": bool(args.bias_mirror)} if args.bias_mirror >= 0
                           else {}),
                        **({"log_nt": args.log_nt if args.log_nt in ("heavy", "light")

@@ -180,6 +180,20 @@ int mf_svdpp_epoch_qlog(const mf_csr_t *csr, const int32_t *sched, int64_t n_sch
                         double *user_sq, int32_t n_waves, int32_t flags, int32_t dtype,
                         void *stream);
 
+/* The hybrid helper-wave launch (MF_EPOCH_SVDPP_HELPERS, three helpers): mf_svdpp_epoch in
+ * MF_MODE_ATOMIC, except that the chunk's ratings with cold_row[p] >= 0 (CSR positions p of
+ * csr) belong to "cold" items whose rows stay read-only for the chunk: their q / b gradient
+ * err_k [s_k | 1] is stored to row cold_row[p] of cold_log ([rows][ldq], rows < 2^31 / (ldq *
+ * size)), and only the other items' deltas go to the helper waves' float atomics.  The caller
+ * folds the cold log after the chunk (mf_log_reduce over the cold items' row ranges with their
+ * recency weights, mf_log_apply with the cold items' counts: oracle_svdpp_sgd_stalelog with the
+ * cold items stale).  user_sq[u] = |p_u|^2 of every trained user (the fold's <p^2>). */
+int mf_svdpp_epoch_mix(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
+                       void *bu, int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
+                       const mf_hyper_t *hp, void *cold_log, const int32_t *cold_row,
+                       void *ycbuf, double *user_sq, int32_t n_waves, int32_t flags,
+                       int32_t *status, const uint8_t *hot, int32_t dtype, void *stream);
+
 /* After mf_svdpp_epoch with hot rows: row i += row n_items + i and the replica row zeroed, for
  * i in hot_items[0 .. n_hot). */
 int mf_svdpp_hot_fold(void *qb, int32_t ldq, int32_t n_items, const int32_t *hot_items,

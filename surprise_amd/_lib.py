@@ -74,6 +74,9 @@ SIGNATURES = {
     "mf_svdpp_epoch": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp, _i32,
                        ctypes.POINTER(MfHyper), _i32, _vp, _vp, _i32, _i32, _vp, _vp, _i32,
                        _vp],
+    "mf_svdpp_epoch_mix": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp,
+                           _i32, ctypes.POINTER(MfHyper), _vp, _vp, _vp, _vp, _i32, _i32, _vp,
+                           _vp, _i32, _vp],
     "mf_svdpp_epoch_qlog": [ctypes.POINTER(MfCsr), _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp,
                             _i32, ctypes.POINTER(MfHyper), _vp, _vp, _vp, _vp, _i32, _i32, _i32,
                             _vp],

@@ -41,7 +41,8 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
                     int hx, double *psq, int err_col, int ck_ld, int32_t *status,
-                    const uint8_t *hot, const int64_t *urow, bool nt, void *stream);
+                    const uint8_t *hot, const int64_t *urow, bool nt, const int32_t *crow,
+                    void *stream);
 // this unit's g_dispatch_sum (the dispatch check of the masked launches it holds)
 template <typename T, int M, bool PP>
 int dispatch_sum_tm(unsigned long long *out);
@@ -1377,21 +1378,26 @@ __device__ __forceinline__ void set_status(int32_t *status, int32_t bit) {
 // helper wave h of a chain's H: issue the atomics of the slots t = h (mod H)
 // (n_rows: the rows the slots' offsets may address -- 2 n_items with hot-row replicas;
 // SB: each slot also carries the item-bias delta of column K, added by lane 0)
-template <typename T, int G, bool SB, int H>
+// MIX (the hybrid launch): a slot whose offset has bit 31 set is a cold item's gradient row,
+// stored (plain stores) to row (off & 0x7FFFFFFF) / row size of the cold log clog instead
+constexpr uint32_t kColdSlot = 0x80000000u;
+template <typename T, int G, bool SB, int H, bool MIX = false>
 __device__ void pp_ring_helper(PPRing<T, G, H> *ring, int h, T *qb, int ldq, int n_rows,
-                               int32_t *status, int K = 0)
+                               int32_t *status, int K = 0, T *clog = nullptr)
 {
     constexpr int R = PPRing<T, G, H>::R;
     constexpr int U = Lane1<T, G>::U;
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t qrow = (uint32_t)ldq * sizeof(T), q_oob = (uint32_t)n_rows * qrow;
     const rsrc_t q_rs = make_rsrc(qb, q_oob);
-    uint32_t cq1[U];
+    uint32_t cq1[U], cq1m[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int c = lane + kWave * u;
         cq1[u] = c < ldq ? (uint32_t)c * sizeof(T) : q_oob;
+        cq1m[u] = c < ldq ? (uint32_t)c * sizeof(T) : 0x7FFFF000u;  // (MIX: past the log)
     }
+    const rsrc_t c_rs = make_rsrc(MIX ? (const void *)clog : (const void *)qb, 0x7FFFF000u);
     const T *img = (const T *)&ring->data[0][0][0];
     constexpr int kSlotT = G * kWave * (int)(sizeof(typename Lane8<T>::vec) / sizeof(T));
     const int spin_max = spin_bound(status, kSpinTestHelper);
@@ -1420,6 +1426,18 @@ __device__ void pp_ring_helper(PPRing<T, G, H> *ring, int h, T *qb, int ldq, int
             T v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) v[u] = img[slot * kSlotT + lane + kWave * u];
+            if constexpr (MIX) {
+                if (off & kColdSlot) {  // (a uniform branch)
+                    const uint32_t lo = off & ~kColdSlot;
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        Buf<T>::template sts<0>(c_rs, cq1m[u], lo, v[u]);
+                    if constexpr (SB)
+                        Buf<T>::template sts<0>(c_rs, lane == 0 ? (uint32_t)K * sizeof(T)
+                                                                : 0x7FFFF000u, lo, ring->bias[slot]);
+                    continue;
+                }
+            }
 #pragma unroll
             for (int u = 0; u < U; ++u) atom_add1(q_rs, qb, q_oob, cq1[u], off, v[u]);
             if constexpr (SB)  // (one lane: the other lanes' offset is past the table)
@@ -1461,16 +1479,22 @@ __device__ void pp_ring_helper(PPRing<T, G, H> *ring, int h, T *qb, int ldq, int
 // after the chunk with the recency weights, as the SVD gradient log (oracle:
 // oracle_svdpp_sgd_stalelog with every item stale).  No float atomic, no helper wave.
 template <typename T, int G, bool HX, bool HOT = false, bool SB = false, int H = kHxHelpers,
-          bool LQ = false, bool NT = false, bool SS = false>
+          bool LQ = false, bool NT = false, bool SS = false, bool MIX = false>
 __device__ __forceinline__ void epoch_body_pp_la(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ items,
     const T *__restrict__ ratings, const int32_t *__restrict__ sched, int64_t n_sched,
     T *__restrict__ pu, T *__restrict__ bu, int ldu, T *qb, int ldq, T *yj, T *ycbuf, int K,
     Hyper<T> hp, int n_items, int64_t n_waves_req, int xmask, PPRing<T, G, H> *ring,
     int32_t *status, const uint8_t *__restrict__ hot = nullptr, T *qlog = nullptr,
-    const int64_t *__restrict__ urow = nullptr, double *__restrict__ psq = nullptr)
+    const int64_t *__restrict__ urow = nullptr, double *__restrict__ psq = nullptr,
+    const int32_t *__restrict__ crow = nullptr)
 {
     static_assert(!(LQ && (HX || HOT)), "the q log: no helper waves, no hot replicas");
+    // MIX (the helper-wave launch, mf_svdpp_epoch_mix): the cold items' rows stay read-only for
+    // the chunk -- their ratings' q / b gradients go to the item-grouped log (row crow[p] of
+    // qlog, folded after the chunk like the q log's) -- and only the other items' deltas go to
+    // the helper waves' float atomics (oracle_svdpp_sgd_stalelog with the cold items stale)
+    static_assert(!MIX || (HX && !LQ), "the hybrid launch: helper waves, no q log");
     using L = Lane8<T>;
     using vec = typename L::vec;
     constexpr int W = L::W;
@@ -1499,7 +1523,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
     const uint32_t kbo = (uint32_t)K * sizeof(T);
     int pushed = 0;  // HX: ratings pushed to the ring
     const int chain_spins = HX ? spin_bound(status, kSpinTestChain) : 0;
-    uint32_t cq[G], cu[G], cq1[U], cy1[U];
+    uint32_t cq[G], cu[G], cq1[U], cy1[U], cqm[MIX ? G : 1];
     vec one[G], lrp[G], ap[G], lry[G], lrpy[G], lrq[G], nrq[G];
     const T dc = T(1) - hp.lr_yj * hp.reg_yj;
     // a lane past the row: its column offset is past the item table AND past any user's log
@@ -1517,6 +1541,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
         const int c0 = (lane + kWave * v) * W;
         const uint32_t b = (uint32_t)c0 * sizeof(T);
         cq[v] = c0 < ldq ? b : col_oob;
+        if constexpr (MIX) cqm[v] = c0 < ldq ? b : kColOob;  // (the cold log's: past its range)
         cu[v] = c0 < ldu ? b : y_oob;  // >= the pu / ycbuf records (K elements) too: dropped
 #pragma unroll
         for (int e = 0; e < W; ++e) {
@@ -1538,6 +1563,8 @@ __device__ __forceinline__ void epoch_body_pp_la(
     const T kb = hp.gm * (T(1) - abu);
     const rsrc_t q_rs = make_rsrc(qb, q_oob);
     const rsrc_t y_rs = make_rsrc(yj, y_oob);
+    // MIX: the cold log (rows crow[p] of qlog; a masked row's offset lies past kMaxTable)
+    const rsrc_t c_rs = make_rsrc(MIX ? (const void *)qlog : (const void *)qb, 0x7FFFF000u);
     const int prio_len = (int)(row_ptr[sched[0] + 1] - row_ptr[sched[0]]);
 
     auto do_user = [&](const int u) {
@@ -1549,6 +1576,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
         else if (n * 8 > prio_len) __builtin_amdgcn_s_setprio(1);
         const int32_t *__restrict__ it = items + s;
         const T *__restrict__ rt = ratings + s;
+        const int32_t *__restrict__ cw = crow + (MIX ? s : 0);
         const rsrc_t p_rs = make_rsrc(pu + (int64_t)u * ldu, (uint32_t)K * sizeof(T));
         const rsrc_t b_rs = make_rsrc(bu + u, sizeof(T));
         // LQ: the user's rows of the chunk's log (row k = its k-th rating)
@@ -1596,10 +1624,19 @@ __device__ __forceinline__ void epoch_body_pp_la(
             go = (uint32_t)i * qrow;
             gr = rt[j];
             if constexpr (HOT) gh = hot[i];
+            // MIX: gh < 0 marks a cold item's rating, its log row -gh - 1 (a cold item is never
+            // a hot-replica item: those are the most-rated)
+            if constexpr (MIX) {
+                if constexpr (!HOT) gh = 0;  // (gh is the caller's variable: no stale value)
+                const int c = cw[j];
+                if (c >= 0) gh = -c - 1;
+            }
         };
         vec bank[2][kB][G];
         T bbv[SB ? 2 : 1];  // SB: lane d holds the item bias of the bank's entry d
         vec rep[HOT ? 2 : 1][HOT ? kB : 1][G];  // HOT: the replica rows of a bank's entries
+        int cr[MIX ? 2 : 1][MIX ? kB : 1];  // MIX: entry d's cold log row, or -1
+        uint32_t cbits = 0;  // MIX: bit d = entry d of the bank being flushed went to the log
         T br[2][kB];
         uint32_t bo[2][kB];
         uint32_t hm[2] = {0u, 0u};  // HOT: bit d = entry d of the bank is a hot item
@@ -1611,7 +1648,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
         int gh_n1 = 0, gh_n2 = 0;
         auto fill = [&](const int bk, const uint32_t go, const T gr, const int gh) {
             if constexpr (HOT)
-                hm[bk] = (uint32_t)__builtin_amdgcn_ballot_w64(gh != 0) & ((1u << kB) - 1u);
+                hm[bk] = (uint32_t)__builtin_amdgcn_ballot_w64(gh > 0) & ((1u << kB) - 1u);
             // SB: the bank's item biases in one per-lane gather before its rows (epoch_body_la)
             if constexpr (SB) bbv[bk] = Buf<T>::template ld<kSc1>(q_rs, go + kbo);
 #pragma unroll
@@ -1619,6 +1656,10 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 const uint32_t off = readlane((int)go, d);
                 bo[bk][d] = off;
                 br[bk][d] = readlane(gr, d);
+                if constexpr (MIX) {
+                    const int g = readlane(gh, d);
+                    cr[bk][d] = g < 0 ? -g - 1 : -1;
+                }
 #pragma unroll
                 for (int v = 0; v < G; ++v) bank[bk][d][v] = L::template lds<kSc1>(q_rs, cq[v], off);
                 if constexpr (HOT) {  // (a uniform branch: most entries are not hot)
@@ -1633,6 +1674,13 @@ __device__ __forceinline__ void epoch_body_pp_la(
         auto atomics = [&]() {  // the previous bank's q deltas as float atomics, from this wave
 #pragma unroll
             for (int d = 0; d < kB; ++d) {
+                if (MIX && ((cbits >> d) & 1u)) {  // (a cold entry: its row to the log)
+#pragma unroll
+                    for (int v = 0; v < G; ++v) L::template sts<0>(c_rs, cqm[v], dlo[d], dl[d][v]);
+                    if constexpr (SB)
+                        Buf<T>::template sts<0>(c_rs, lane == 0 ? kbo : kColOob, dlo[d], dlb[d]);
+                    continue;
+                }
                 T d1[U];
                 to_lane1<G>(dl[d], d1);
 #pragma unroll
@@ -1680,7 +1728,8 @@ __device__ __forceinline__ void epoch_body_pp_la(
                     const int slot = (pushed + d) % R;
 #pragma unroll
                     for (int v = 0; v < G; ++v) ring->data[slot][v][lane] = dl[d][v];
-                    ring->off[slot] = dlo[d];
+                    // (MIX: a cold entry's row goes to the log -- the helper stores it)
+                    ring->off[slot] = MIX && ((cbits >> d) & 1u) ? dlo[d] | kColdSlot : dlo[d];
                     if constexpr (SB) ring->bias[slot] = dlb[d];
                 }
                 pushed += kB;
@@ -1746,6 +1795,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 qn[v] = qrow_of(bn, dn, v);
             }
             const T err = (br[bk][d] - c0_p) - X - err_p * Yb;  // mf.pyx:483
+            const bool cold = MIX && valid && cr[bk][d] >= 0;  // (MIX: a cold item's rating)
             const T c0 = abu * (lr_bu * err_p + c0_p) + kb;     // mf.pyx:486, one rating late
             vec P[G], M[SS ? 1 : G], Dp[G], Dm[SS ? 1 : G], px = L::splat(T(0)),
                 py = L::splat(T(0));
@@ -1771,17 +1821,21 @@ __device__ __forceinline__ void epoch_body_pp_la(
                     py += qn[v] * (lrpy[v] * q);
                 }
                 if constexpr (LQ) dl[d][v] = err * sk;  // the gradient (the fold applies lr, reg)
+                else if (MIX && cold) dl[d][v] = err * sk;  // (a cold item: its gradient, logged)
                 else dl[d][v] = err * (lrq[v] * sk) + nrq[v] * q;  // mf.pyx:489, :492
             }
             if constexpr (SB) {
-                if constexpr (LQ) dlb[d] = err;
+                if (LQ || (MIX && cold)) dlb[d] = err;
                 else dlb[d] = hp.lr_bi * (err - hp.reg_bi * readlane(bbv[bk], d));  // mf.pyx:489
             }
             const bool hot_d = HOT && to_rep && ((hm[bk] >> d) & 1u);
             if constexpr (LQ)  // (past the user's segment: dropped)
                 dlo[d] = (uint32_t)(valid ? k : n) * qrow;
+            else if (MIX && cold)
+                dlo[d] = (uint32_t)cr[bk][d] * qrow;
             else
                 dlo[d] = valid ? (hot_d ? bo[bk][d] + rep_shift : bo[bk][d]) : bo[bk][d] + q_oob;
+            if constexpr (MIX) cbits = cold ? (cbits | (1u << d)) : (cbits & ~(1u << d));
             T Xn, Yn;
             wave_sum2_u(L::hsum(px), L::hsum(py), Xn, Yn);  // X_{k+1}, Y_{k+1}
             if constexpr (SB) Xn += readlane(bbv[bn], dn);  // (the next item's bias: s_k's column K is 1)
@@ -1858,7 +1912,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
             }
             L::template st<0>(p_rs, cu[v], pn);
             cacc[v] = (mn - A * m0[v]) * rs_n;
-            if constexpr (LQ) {
+            if constexpr (LQ || MIX) {
 #pragma unroll
                 for (int e = 0; e < W; ++e) {
                     const double x = (double)L::get(pn, e);
@@ -1866,7 +1920,7 @@ __device__ __forceinline__ void epoch_body_pp_la(
                 }
             }
         }
-        if (LQ && psq) {
+        if ((LQ || MIX) && psq) {
             sq = wave_sum(sq);
             if (lane == 0) psq[u] = sq;
         }
@@ -1938,10 +1992,12 @@ __global__ __launch_bounds__(kBlock) void mf_ckpt_epoch_kernel(MF_EPOCH_PARAMS)
 // SB: the lane groups cover the K factor columns only and the item bias (column K) is carried as
 // a scalar per rating (fp32 K=128: one lane group instead of two -- half the vector work and the
 // registers of a bank of 8 rows)
-template <typename T, int G, bool HOT, bool SB = false, int H = kHxHelpers, bool SS = false>
+template <typename T, int G, bool HOT, bool SB = false, int H = kHxHelpers, bool SS = false,
+          bool MIX = false>
 __global__ __launch_bounds__(kWave * (1 + H)) void mf_svdpp_hx_kernel(MF_EPOCH_PARAMS,
                                                                      int32_t *status,
-                                                                     const uint8_t *hot)
+                                                                     const uint8_t *hot,
+                                                                     const int32_t *crow)
 {
     __shared__ PPRing<T, G, H> ring;
     const int w = threadIdx.x / kWave;
@@ -1952,12 +2008,13 @@ __global__ __launch_bounds__(kWave * (1 + H)) void mf_svdpp_hx_kernel(MF_EPOCH_P
     }
     __syncthreads();
     if (w == 0) {
-        epoch_body_pp_la<T, G, true, HOT, SB, H, false, false, SS>(
+        epoch_body_pp_la<T, G, true, HOT, SB, H, false, false, SS, MIX>(
             row_ptr, items, ratings, sched, n_sched, pu, bu, ldu, qb, ldq, yj, elog, K, hp,
-            n_items, n_waves_req, 0, &ring, status, hot);
+            n_items, n_waves_req, 0, &ring, status, hot, qlog, nullptr, psq, crow);
         if (blockIdx.x >= n_waves_req) lds_store(&ring.done, 1);  // (no chain in this workgroup)
     } else {
-        pp_ring_helper<T, G, SB, H>(&ring, w - 1, qb, ldq, (HOT ? 2 : 1) * n_items, status, K);
+        pp_ring_helper<T, G, SB, H, MIX>(&ring, w - 1, qb, ldq, (HOT ? 2 : 1) * n_items, status,
+                                         K, qlog);
     }
 }
 
@@ -1981,10 +2038,11 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                     int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                     int32_t biased, const mf_hyper_t *hp, int64_t waves, bool dups, int xmask,
                     int hx, double *psq, int err_col, int ck_ld, int32_t *status,
-                    const uint8_t *hot, const int64_t *urow, bool nt, void *stream)
+                    const uint8_t *hot, const int64_t *urow, bool nt, const int32_t *crow,
+                    void *stream)
 {
-    if ((psq || err_col) && (PP || M != kLog || !elog) && !(psq && urow && !err_col))
-        return set_err(MF_E_UNSUPPORTED, "user_sq / errors in rows: the SVD checkpoint log or the SVD++ q log only");
+    if ((psq || err_col) && (PP || M != kLog || !elog) && !(psq && (urow || crow) && !err_col))
+        return set_err(MF_E_UNSUPPORTED, "user_sq / errors in rows: the SVD checkpoint log, the SVD++ q log or the hybrid launch only");
     // the lookahead body (SVD, MF_MODE_LOG, rows <= 1 KiB) carries the user bias in column K + 1
     if (!PP && M == kLog && MF_LA && (int64_t)ldq * sizeof(T) <= 512 * kLaMaxG && ldq < K + 2)
         return set_err(MF_E_ARG, "MF_MODE_LOG: ldq >= n_factors + 2 (the user-bias column)");
@@ -2010,6 +2068,8 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
     if (hx && !(PP && M == kAtomic && elog && !dups))
         return set_err(MF_E_UNSUPPORTED, "helper waves: SVD++, MF_MODE_ATOMIC, deferred y, no repeated items");
     if (hot && !hx) return set_err(MF_E_ARG, "hot-row replicas: the helper-wave launch only");
+    if (crow && !(hx && qlog && psq))
+        return set_err(MF_E_UNSUPPORTED, "the hybrid launch: helper waves, a cold log, user_sq");
     // the helper-wave launch with the item bias beside the lane groups (SB) where the factor
     // columns fill whole groups
     const bool sb = hx && !hot && whole;
@@ -2035,12 +2095,22 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
                                       : mf_svdpp_hx_kernel<T, V, false, true>)
                                 : (ss ? mf_svdpp_hx_kernel<T, V, false, false, kHxHelpers, true>
                                       : mf_svdpp_hx_kernel<T, V, false>);
+                if (crow) {  // the hybrid launch (MIX): three helpers, any hot / SB layout
+                    kern = hot ? (ss ? mf_svdpp_hx_kernel<T, V, true, false, kHxHelpers, true, true>
+                                     : mf_svdpp_hx_kernel<T, V, true, false, kHxHelpers, false, true>)
+                         : sb  ? (ss ? mf_svdpp_hx_kernel<T, V, false, true, kHxHelpers, true, true>
+                                     : mf_svdpp_hx_kernel<T, V, false, true, kHxHelpers, false, true>)
+                               : (ss ? mf_svdpp_hx_kernel<T, V, false, false, kHxHelpers, true, true>
+                                     : mf_svdpp_hx_kernel<T, V, false, false, kHxHelpers, false, true>);
+                    if (hx != kHxHelpers)
+                        return set_err(MF_E_UNSUPPORTED, "the hybrid launch: three helper waves");
+                }
                 hipLaunchKernelGGL(kern, dim3(waves), dim3(kWave * (1 + hx)), 0,
                                    (hipStream_t)stream, csr->row_ptr, csr->items,
                                    (const T *)csr->ratings, sched, n_sched, (T *)pu, (T *)bu, ldu,
                                    (T *)qb, ldq, (T *)yj, (T *)qlog, (T *)elog, K, biased,
-                                   cast_hyper<T>(hp), csr->n_items, waves, 0, nullptr, 0, ldq,
-                                   status, hot);
+                                   cast_hyper<T>(hp), csr->n_items, waves, 0, psq, 0, ldq,
+                                   status, hot, crow);
                 return check_launch("mf_svdpp_hx_kernel");
             }
         } else {
@@ -2099,7 +2169,7 @@ int launch_epoch_tm(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, 
 template int launch_epoch_tm<MF_INST_T, MF_INST_M, (bool)MF_INST_PP>(
     const mf_csr_t *, const int32_t *, int64_t, void *, void *, int32_t, void *, int32_t, void *,
     void *, void *, int32_t, int32_t, const mf_hyper_t *, int64_t, bool, int, int, double *,
-    int, int, int32_t *, const uint8_t *, const int64_t *, bool, void *);
+    int, int, int32_t *, const uint8_t *, const int64_t *, bool, const int32_t *, void *);
 template <typename T, int M, bool PP>
 int dispatch_sum_tm(unsigned long long *out)
 {
@@ -4455,7 +4525,8 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
                  int32_t ldu, void *qb, int32_t ldq, void *yj, void *qlog, void *elog, int32_t K,
                  int32_t biased, const mf_hyper_t *hp, int32_t mode, int32_t n_waves, int32_t flags,
                  int32_t dtype, void *stream, double *psq = nullptr, int32_t *status = nullptr,
-                 const uint8_t *hot = nullptr, const int64_t *urow = nullptr)
+                 const uint8_t *hot = nullptr, const int64_t *urow = nullptr,
+                 const int32_t *crow = nullptr)
 {
     const bool dups = flags & MF_EPOCH_DUP_ITEMS;
     // helper waves per chain: 3, or 1 (MF_EPOCH_SVDPP_ONE_HELPER); 0 = no helper-wave launch
@@ -4496,7 +4567,7 @@ int launch_epoch(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, voi
         return mf_ext::launch_epoch_tm<T, M, PP>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj,
                                                   qlog, elog, K, biased, hp, waves, dups, xmask,
                                                   hx, psq, err_col, ck_ld, status, hot, urow,
-                                                  (flags & MF_EPOCH_LOG_NT) != 0, stream);
+                                                  (flags & MF_EPOCH_LOG_NT) != 0, crow, stream);
     };
     auto by_mode = [&](auto tag_t) -> int {
         switch (mode) {
@@ -4540,7 +4611,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 934; }
+int mf_version(void) { return 935; }
 
 #ifndef MF_SOURCE_HASH
 #define MF_SOURCE_HASH "unknown"
@@ -4685,6 +4756,21 @@ int mf_svdpp_epoch_qlog(const mf_csr_t *csr, const int32_t *sched, int64_t n_sch
     return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, qlog, ycbuf,
                               n_factors, 1, hp, MF_MODE_LOG, n_waves, flags, dtype, stream,
                               user_sq, nullptr, nullptr, log_row0);
+}
+
+int mf_svdpp_epoch_mix(const mf_csr_t *csr, const int32_t *sched, int64_t n_sched, void *pu,
+                       void *bu, int32_t ldu, void *qb, int32_t ldq, void *yj, int32_t n_factors,
+                       const mf_hyper_t *hp, void *cold_log, const int32_t *cold_row,
+                       void *ycbuf, double *user_sq, int32_t n_waves, int32_t flags,
+                       int32_t *status, const uint8_t *hot, int32_t dtype, void *stream)
+{
+    if (!cold_log || !cold_row || !ycbuf || !user_sq)
+        return set_err(MF_E_ARG, "the hybrid launch needs cold_log, cold_row, ycbuf and user_sq");
+    if (!(flags & MF_EPOCH_SVDPP_HELPERS) || (flags & MF_EPOCH_SVDPP_ONE_HELPER))
+        return set_err(MF_E_ARG, "the hybrid launch: MF_EPOCH_SVDPP_HELPERS (three helpers)");
+    return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, cold_log, ycbuf,
+                              n_factors, 1, hp, MF_MODE_ATOMIC, n_waves, flags, dtype, stream,
+                              user_sq, status, hot, nullptr, cold_row);
 }
 
 int mf_svdpp_hot_fold(void *qb, int32_t ldq, int32_t n_items, const int32_t *hot_items,

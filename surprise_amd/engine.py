@@ -153,6 +153,41 @@ def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS, local=Fals
     return perm, piece_beg.astype(np.int32), item_piece_ptr, counts.astype(np.int32)
 
 
+def cold_items(counts, share):
+    """The hybrid launch's cold items of one chunk: the least-rated items whose ratings add up to
+    at most `share` of the chunk's (bool[n_items]; items the chunk does not rate are not cold)."""
+    counts = np.asarray(counts, np.int64)
+    order = np.argsort(counts, kind="stable")
+    cum = np.cumsum(counts[order])
+    cold = np.zeros(len(counts), bool)
+    n = int(np.searchsorted(cum, share * max(int(counts.sum()), 1), side="right"))
+    cold[order[:n]] = True
+    return cold & (counts > 0)
+
+
+def mix_layout(row_ptr, items, users, n_items, cold, piece_rows=PIECE_ROWS):
+    """The hybrid launch's cold log of one chunk (mf_svdpp_epoch_mix): the cold items' ratings
+    grouped by item (users in order within an item), so a cold rating at CSR position p is log row
+    crow[p] (crow -1: a live item); pieces of <= piece_rows rows, each of one item, for
+    mf_log_reduce (perm = the identity), item_piece_ptr for mf_log_apply, and every row's
+    position among its item's ratings (the recency weight)."""
+    perm, pb, ipp, cnt = log_layout(row_ptr, items, users, n_items, piece_rows)
+    pitem = np.repeat(np.arange(n_items, dtype=np.int32), np.diff(ipp))
+    keep = cold[pitem]
+    lens = np.diff(pb)
+    pos_keep = np.repeat(keep, lens)
+    rows = perm[pos_keep]
+    crow = np.full(int(np.asarray(row_ptr)[-1]), -1, np.int32)
+    crow[rows] = np.arange(len(rows), dtype=np.int32)
+    rpos = (np.arange(len(perm), dtype=np.int64) - np.repeat(pb[ipp[:-1]], cnt))[pos_keep]
+    pitem_c = pitem[keep]
+    pb_c = np.concatenate([[0], np.cumsum(lens[keep])]).astype(np.int32)
+    ipp_c = np.concatenate([[0], np.cumsum(np.bincount(pitem_c, minlength=n_items))]).astype(
+        np.int32)
+    return dict(crow=crow, rows=len(rows), pb=pb_c, pitem=pitem_c, ipp=ipp_c,
+                rpos=rpos.astype(np.int32), totals=np.where(cold, cnt, 0).astype(np.int32))
+
+
 def qlog_fold_layout(counts, perm, rpos, users, hot_rows=PIECE_ROWS, piece_rows=PIECE_ROWS):
     """mf_svdpp_qlog_fold's layout of one chunk (include/surprise_amd.h mf_qlog_fold_t) from the
     q log's item-grouped positions: perm (log rows), rpos (each row's position among its item's)
@@ -432,7 +467,8 @@ class MFEngine(ItemSync, Predictor):
                  helpers=None, ydefer=True, hx_chains_per_cu=None, hot_rows=None,
                  replay_rows=None, gram=None, xcd_split=None, qlog=None, top=None,
                  exchange=None, long_chain=256, overlap_q=True, fused=True, stagger=None,
-                 light_replay_wpc=0, log_nt=None, item_align=None, bias_mirror=True):
+                 light_replay_wpc=0, log_nt=None, item_align=None, bias_mirror=True,
+                 cold_share=0.0):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -492,6 +528,10 @@ class MFEngine(ItemSync, Predictor):
                       "heavy" / "light": only that group's launch of a split chunk
           item_align  item rows padded to a multiple of this many bytes (timing probes; None:
                       ITEM_ROW_ALIGN)
+          cold_share  SVD++ helper-wave launch on one rank: the least-rated items holding up to
+                      this share of a chunk's ratings keep their rows read-only for the chunk,
+                      their gradients logged and folded after it (mf_svdpp_epoch_mix); the
+                      others take the float atomics (0: off)
           bias_mirror checkpoint log with SB rows (fp32 K=128, fp64 K=64 / 128): the item biases
                       read from a mirror array, the item rows on whole 128-B lines; False: from
                       the rows
@@ -782,6 +822,22 @@ class MFEngine(ItemSync, Predictor):
             flag = np.zeros(self.n_items, np.uint8)
             flag[hot] = 1
             self.hot_flag = to_dev(flag)
+        # the hybrid launch (cold_share: one rank, three helper waves per chain)
+        self.mix = []
+        if cold_share and self.hx and self.hx_helpers == 3 and not self.multi:
+            for c, us in enumerate(self.sched):
+                cold = cold_items(self._totals_local[c], float(cold_share))
+                if len(hot):
+                    cold[hot] = False
+                self.mix.append(mix_layout(row_ptr, items, us.cpu().numpy(), self.n_items, cold))
+            rows = max(m["rows"] for m in self.mix)
+            if rows * self.ldq * esz >= (1 << 31):  # (the log's 32-bit buffer offsets)
+                self.mix = []
+            for m in self.mix:
+                for k in ("crow", "pb", "pitem", "ipp", "rpos", "totals"):
+                    m[k] = to_dev(m[k])
+                m["perm"] = torch.arange(max(m["rows"], 1), dtype=torch.int32, device=dev)
+                m["n_pieces"] = int(m["pb"].numel()) - 1
         self.ycsc = []
         if self.ydefer:
             for us in self.sched:
@@ -823,7 +879,7 @@ class MFEngine(ItemSync, Predictor):
         # kernels (mf_user_sq_reduce, off the step's critical path; no mf_sumsq pass)
         # (the SVD++ q log too: its kernel stores |p_u|^2 of the users it trains)
         self.user_sq = (torch.zeros(max(self.n_users, 1), dtype=torch.float64, device=dev)
-                        if self.ckpt or self.qlog_pp else None)
+                        if self.ckpt or self.qlog_pp or self.mix else None)
         self._sq_valid = self._sq_pending = False
         # several ranks, checkpoint log: the next chunk's <p^2> rode in this chunk's exchange
         # buffer (already every rank's sum: no collective of its own at the chunk start)
@@ -838,6 +894,9 @@ class MFEngine(ItemSync, Predictor):
         self._qb_alloc = z(2 * I if self.hot_list is not None else I, ldq)
         self.qb = self._qb_alloc[:I]
         self.ibias = z(max(I, 1)) if self.sb_mirror else None  # (qb[:, K]'s mirror, SB rows)
+        # the hybrid launch's cold log and its piece sums
+        self.clog = z(max(max(m["rows"] for m in self.mix), 1), ldq) if self.mix else None
+        self.csums = z(max(max(m["n_pieces"] for m in self.mix), 1), ldq) if self.mix else None
         self.yj = z(I, ld) if algo == "svdpp" else None
         self.ycbuf = z(U, ld) if self.ydefer else None
         if self.ydefer:
@@ -1062,6 +1121,13 @@ class MFEngine(ItemSync, Predictor):
                       self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper), qlog,
                       self._ptr(self.urow), self._ptr(self.ycbuf), self._ptr(self.user_sq),
                       n_waves, flags, self.dtype, st)
+        elif self.mix and flags & _lib.MF_EPOCH_SVDPP_HELPERS:  # the hybrid launch
+            _lib.call("mf_svdpp_epoch_mix", ctypes.byref(self._csr), self._ptr(sched), n_sched,
+                      self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
+                      self.ldq, self._ptr(self.yj), self.K, ctypes.byref(self._hyper),
+                      self._ptr(self.clog), self._ptr(self.mix[self._chunk]["crow"]),
+                      self._ptr(self.ycbuf), self._ptr(self.user_sq), n_waves, flags,
+                      self._ptr(self._hx_status), self._ptr(self.hot_flag), self.dtype, st)
         else:
             _lib.call("mf_svdpp_epoch", ctypes.byref(self._csr), self._ptr(sched), n_sched,
                       self._ptr(self.pu), self._ptr(self.bu), self.ld, self._ptr(self.qb),
@@ -1090,7 +1156,7 @@ class MFEngine(ItemSync, Predictor):
         if self.ckpt:
             self._run_chunk_ckpt(c, ev)
             return
-        if self.qlog_pp:  # <p^2> of the chunk start from user_sq (as the checkpoint log)
+        if self.qlog_pp or self.mix:  # <p^2> of the chunk start from user_sq (as the ckpt log)
             self._sq_prologue(st)
         elif self.is_log:
             self.work = self._works[self._wt % 2]
@@ -1127,6 +1193,8 @@ class MFEngine(ItemSync, Predictor):
             if self.hot_list is not None:
                 _lib.call("mf_svdpp_hot_fold", self._ptr(self.qb), self.ldq, self.n_items,
                           self._ptr(self.hot_list), self.hot_list.numel(), self.dtype, st)
+            if self.mix:
+                self._cold_fold(c, st)
         else:
             self._epoch(s, s.numel(), self.n_waves, 0, st, lx)
         if "end" in ev:
@@ -1150,6 +1218,25 @@ class MFEngine(ItemSync, Predictor):
             self.stream.wait_event(join)
         if "end_r" in ev:
             ev["end_r"].record(self.stream)
+
+    def _cold_fold(self, c, st):
+        """The hybrid launch's cold items after chunk c: their logged gradients summed per piece
+        with the recency weights (mf_log_reduce over the item-grouped cold log), then each cold
+        item's step (mf_log_apply with the cold items' counts: a live item's count is 0, its row
+        untouched); the same launch sums user_sq into the next chunk's <p^2>."""
+        m = self.mix[c]
+        if m["n_pieces"] > 0:
+            totals = self._totals()[c]
+            rec = _lib.MfRecency(m["rpos"].data_ptr(), None, totals.data_ptr(),
+                                 self.work.data_ptr())
+            _lib.call("mf_log_reduce", self._ptr(self.clog), self.ldq, self.K + 1,
+                      self._ptr(m["perm"]), self._ptr(m["pb"]), m["n_pieces"],
+                      self._ptr(self.csums), self._ptr(m["pitem"]), ctypes.byref(self._hyper),
+                      ctypes.byref(rec), self.dtype, st)
+        _lib.call("mf_log_apply", self._ptr(self.qb), self.n_items, self.ldq, self.K,
+                  self._bias_col, self._ptr(self.csums), self._ptr(m["ipp"]), None, None,
+                  self._ptr(m["totals"]), ctypes.byref(self._hyper), self._ptr(self.work),
+                  _lib.MF_MERGE_RECENCY, None, 1, *self._stat_args(True), None, self.dtype, st)
 
     def _epoch_sq(self, sched, n_sched, n_waves, st, xmask=0, group=None):
         """The checkpoint-log epoch kernel keeping user_sq current (mf_svd_epoch_sq); group: the

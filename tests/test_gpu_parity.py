@@ -1156,3 +1156,49 @@ def test_svdpp_shared_step_chain_and_general_chain_match_stalelog_oracle(torch, 
     assert algo._engine.qlog_pp
     for k in ("pu", "qi", "yj", "bu", "bi"):
         np.testing.assert_allclose(getattr(algo, k), f[k], rtol=0, atol=1e-9, err_msg=k)
+
+
+@pytest.mark.parametrize("K", [10, 64])
+def test_svdpp_hybrid_launch_all_cold_matches_stalelog_oracle(torch, u1, K):
+    """The hybrid helper-wave launch (mf_svdpp_epoch_mix) with every item cold (cold_share 1, no
+    hot replicas): no float atomic is left, every gradient goes to the item-grouped cold log and
+    the cold fold (mf_log_reduce + mf_log_apply) -- oracle_svdpp_sgd_stalelog with every item
+    stale, to 1e-9 in fp64, over 2 chunks."""
+    from surprise_amd import SVDpp
+    from surprise_amd.dist import chunk_users
+    ts, test = u1
+    row_ptr, items, ratings = ts.csr()
+    params = dict(n_factors=K, n_epochs=3, random_state=0)
+    cou = np.zeros(ts.n_users, np.int32)
+    for c, us in enumerate(chunk_users(np.arange(ts.n_users), row_ptr, 2)):
+        cou[us] = c
+    P, f = run_oracle_stalelog(params, row_ptr, items, ratings, ts.n_items, ts.global_mean,
+                               cou, 2)
+    algo = SVDpp(**params, dtype="float64", chunks_per_epoch=2, mode="atomic")
+    algo._engine_options = {"cold_share": 1.0, "hot_rows": 0, "helpers": True, "qlog": False}
+    algo.fit(ts)
+    eng = algo._engine
+    assert eng.hx and eng.mix and eng.hot_list is None
+    assert all(int((m["crow"] >= 0).sum()) == int(m["totals"].sum()) for m in eng.mix)
+    for k in ("pu", "qi", "yj", "bu", "bi"):
+        np.testing.assert_allclose(getattr(algo, k), f[k], rtol=0, atol=1e-9, err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["svdpp_k20_e20", "svdpp_k100_e20"])
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_svdpp_hybrid_launch_rmse_within_1e3(torch, golden, u1, name, dtype):
+    """The hybrid launch with the least-rated items holding half the ratings cold (their rows
+    read-only per chunk, gradients logged and folded) and the rest on the helper waves' float
+    atomics, hot replicas included: held-out RMSE within 1e-3 of the reference's."""
+    from surprise_amd import SVDpp
+    meta, _ = golden
+    case = meta["cases"][name]
+    ts, test = u1
+    algo = SVDpp(**case["params"], dtype=dtype, mode="atomic")
+    algo._engine_options = {"cold_share": 0.5, "qlog": False}
+    algo.fit(ts)
+    eng = algo._engine
+    assert eng.hx and eng.mix
+    cold = int((eng.mix[0]["crow"] >= 0).sum())
+    assert 0.3 * ts.n_ratings < cold <= 0.5 * ts.n_ratings, cold
+    assert abs(_rmse(algo.test(test)) - case["rmse"]) < RMSE_TOL
