@@ -3,7 +3,7 @@
 # smoke(), then the default bench line and the rocprofv3 kernel trace + stats of that command
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-tag=r5f
+tag=${TAG:-r5f}
 fatal() { case $1 in 124|137|134|139) echo "step rc $1: stopping"; exit $1;; esac; }
 timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests --ignore=tests/test_gpu_scale.py -p no:cacheprovider > gpurun_out/${tag}_pytest.log 2>&1; rc=$?; echo "pytest rc $rc"; grep -E "FAILED|passed|failed" gpurun_out/${tag}_pytest.log | tail -4; fatal $rc; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1; rc=$?; tail -1 gpurun_out/${tag}_smoke.log; fatal $rc; [ $rc -eq 0 ] || exit $rc
