@@ -4768,6 +4768,12 @@ int mf_svdpp_epoch_mix(const mf_csr_t *csr, const int32_t *sched, int64_t n_sche
         return set_err(MF_E_ARG, "the hybrid launch needs cold_log, cold_row, ycbuf and user_sq");
     if (!(flags & MF_EPOCH_SVDPP_HELPERS) || (flags & MF_EPOCH_SVDPP_ONE_HELPER))
         return set_err(MF_E_ARG, "the hybrid launch: MF_EPOCH_SVDPP_HELPERS (three helpers)");
+    // ring slots carry byte offsets with bit 31 marking a cold-log row (kColdSlot): every q
+    // offset, hot-row replicas included, must stay below 2 GiB
+    const uint64_t esz = dtype == MF_F32 ? 4 : 8;
+    if (csr && (uint64_t)csr->n_items * (hot ? 2 : 1) * (uint64_t)(ldq > 0 ? ldq : 0) * esz >=
+                   kMaxTable)
+        return set_err(MF_E_UNSUPPORTED, "the hybrid launch: item table (with replicas) >= 2 GiB");
     return launch_epoch<true>(csr, sched, n_sched, pu, bu, ldu, qb, ldq, yj, cold_log, ycbuf,
                               n_factors, 1, hp, MF_MODE_ATOMIC, n_waves, flags, dtype, stream,
                               user_sq, status, hot, nullptr, cold_row);

@@ -831,7 +831,9 @@ class MFEngine(ItemSync, Predictor):
                     cold[hot] = False
                 self.mix.append(mix_layout(row_ptr, items, us.cpu().numpy(), self.n_items, cold))
             rows = max(m["rows"] for m in self.mix)
-            if rows * self.ldq * esz >= (1 << 31):  # (the log's 32-bit buffer offsets)
+            # (the cold log's and the q table's offsets, replicas included, share the helper
+            # ring's 31 bits: beyond them the atomic launch runs)
+            if max(rows, 2 * self.n_items) * self.ldq * esz >= (1 << 31) - 4096:
                 self.mix = []
             for m in self.mix:
                 for k in ("crow", "pb", "pitem", "ipp", "rpos", "totals"):

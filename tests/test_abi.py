@@ -57,6 +57,17 @@ def test_version_and_error_without_device(lib):
     rc = lib.mf_svdpp_epoch(ctypes.byref(csr), None, 1, None, None, 16, None, 16, None, 10, None,
                             1, None, None, 0, 0, None, None, 0, None)
     assert rc == 1001 and b"null csr" in lib.mf_last_error()
+    # the hybrid launch: its buffers, three helper waves, and q offsets below bit 31 (ring flag)
+    rc = lib.mf_svdpp_epoch_mix(ctypes.byref(csr), None, 1, None, None, 16, None, 16, None, 10,
+                                None, None, None, None, None, 0, 0, None, None, 0, None)
+    assert rc == 1001 and b"needs cold_log" in lib.mf_last_error()
+    rc = lib.mf_svdpp_epoch_mix(ctypes.byref(csr), None, 1, None, None, 16, None, 16, None, 10,
+                                None, 1, 1, 1, 1, 0, 0, None, None, 0, None)
+    assert rc == 1001 and b"three helpers" in lib.mf_last_error()
+    big = _lib.MfCsr(1, 1, 1, 10, 1_100_000)  # 2 x 1.1M rows x 1 KiB: past 2 GiB with replicas
+    rc = lib.mf_svdpp_epoch_mix(ctypes.byref(big), None, 1, None, None, 256, None, 256, None, 200,
+                                None, 1, 1, 1, 1, 0, _lib.MF_EPOCH_SVDPP_HELPERS, None, 1, 0, None)
+    assert rc != 0 and b"with replicas" in lib.mf_last_error()
     rc = lib.mf_sumsq(None, 4, 8, 4, None, 0, None)
     assert rc == 1001
     rc = lib.mf_svd_epoch_sq(ctypes.byref(csr), None, 1, None, None, 16, None, 16, 10, 1, None,
