@@ -585,6 +585,39 @@ int mf_launch_event(void *event);
  * is then invalid and the caller must fail.  words = NULL: no join. */
 int mf_launch_join(void *words, int32_t role, uint32_t epoch);
 
+/* mf_launch_fold(f): the chunk's fold (mf_log_apply, the same arithmetic and sum order) runs
+ * inside the next mf_log_replay launch(es) of the calling thread instead of a launch of its own.
+ * A piece's wave stores its sums through to the coherence point, then counts the piece in
+ * item_count[item]; the wave that completes an item's pieces (over sums / item_piece_ptr and,
+ * split chunk, sums2 / item_piece_ptr2 -- each group's replay is one launch, role 1 and 2 of
+ * n_launches) applies that item.  No wave waits.  With stat_next, the last block of the
+ * n_launches launches sums user_sq into it (mf_log_apply's <p^2> for the next chunk; fewer than
+ * MF_SQ_PARTS_MIN users).  item_count: n_items zeroed int32 and words: MF_FOLD_WORDS zeroed
+ * uint32, device memory owned by the caller (zero again after every complete fold).  Later
+ * launches read q only after both replays have completed (the caller orders the streams).
+ * Not with mf_launch_join.  f = NULL clears a pending fold.  Same fields as mf_log_apply (apply
+ * = 1, no delta_out; hp read here, on the host). */
+#define MF_FOLD_WORDS 1024
+typedef struct mf_fold_t {
+    void *qb;
+    int32_t ld, n_factors, bias_col, rule;
+    const void *sums;
+    const int32_t *item_piece_ptr;
+    const void *sums2;              /* nullable: one launch group */
+    const int32_t *item_piece_ptr2;
+    const int32_t *totals;
+    const mf_hyper_t *hp;
+    const double *p2stat;
+    double *stat_next;              /* nullable */
+    const double *user_sq;
+    int64_t n_users;
+    void *bias_out;                 /* nullable: the item-bias mirror */
+    int32_t *item_count;
+    uint32_t *words;
+    int32_t role, n_launches;
+} mf_fold_t;
+int mf_launch_fold(const mf_fold_t *f);
+
 #ifdef __cplusplus
 }
 #endif

@@ -26,6 +26,8 @@ MF_EPOCH_ERR_IN_ROW = 4  # checkpoint log: errors in the checkpoint rows' paddin
 MF_EPOCH_CKPT_NARROW = 16  # checkpoint log: rows of the factor columns only (errors in elog)
 MF_REPLAY_WPC_SHIFT = 16  # mf_log_replay flags bits 16..23: waves per CU (0: 16)
 MF_EPOCH_LOG_NT = 64  # the epoch kernels' log stores non-temporal (streamed past L2 / MALL)
+MF_FOLD_WORDS = 1024  # mf_launch_fold's arrival counters (uint32)
+MF_SQ_PARTS_MIN = 65536  # users from which the <p^2> sum runs in MF_SQ_PARTS fixed-range parts
 MF_SQ_PARTS = 256  # scratch doubles after a {sum, count} statistic buffer (from MF_SQ_PARTS_MIN rows)
 MF_HX_HELPER_TIMEOUT, MF_HX_CHAIN_FALLBACK = 1, 2  # mf_svdpp_epoch status word bits
 
@@ -50,6 +52,19 @@ class MfCsr(ctypes.Structure):
     _fields_ = [("row_ptr", ctypes.c_void_p), ("items", ctypes.c_void_p),
                 ("ratings", ctypes.c_void_p), ("n_users", ctypes.c_int32),
                 ("n_items", ctypes.c_int32)]
+
+
+class MfFold(ctypes.Structure):
+    """mf_fold_t (include/surprise_amd.h): the fold inside the next mf_log_replay launches."""
+    _fields_ = [("qb", ctypes.c_void_p), ("ld", ctypes.c_int32), ("n_factors", ctypes.c_int32),
+                ("bias_col", ctypes.c_int32), ("rule", ctypes.c_int32),
+                ("sums", ctypes.c_void_p), ("item_piece_ptr", ctypes.c_void_p),
+                ("sums2", ctypes.c_void_p), ("item_piece_ptr2", ctypes.c_void_p),
+                ("totals", ctypes.c_void_p), ("hp", ctypes.c_void_p), ("p2stat", ctypes.c_void_p),
+                ("stat_next", ctypes.c_void_p), ("user_sq", ctypes.c_void_p),
+                ("n_users", ctypes.c_int64), ("bias_out", ctypes.c_void_p),
+                ("item_count", ctypes.c_void_p), ("words", ctypes.c_void_p),
+                ("role", ctypes.c_int32), ("n_launches", ctypes.c_int32)]
 
 
 class MfRecency(ctypes.Structure):
@@ -127,6 +142,7 @@ SIGNATURES = {
     "mf_stream_wait_event": [_vp, _vp],
     "mf_launch_event": [_vp],
     "mf_launch_join": [_vp, _i32, ctypes.c_uint32],
+    "mf_launch_fold": [ctypes.POINTER(MfFold)],
     "mf_version": [],
     "mf_last_error": [],
     "mf_source_hash": [],

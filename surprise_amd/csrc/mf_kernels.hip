@@ -2195,6 +2195,28 @@ JoinArgs take_join() {
     g_join = JoinArgs{};
     return j;
 }
+// mf_launch_fold: the fold inside the next mf_log_replay launch of this thread (cnt == NULL: off)
+struct FoldArgs {
+    void *qb = nullptr;
+    const int32_t *ipp_a = nullptr, *ipp_b = nullptr;  // per item: its pieces in sums_a / sums_b
+    const void *sums_a = nullptr, *sums_b = nullptr;
+    const int32_t *totals = nullptr;
+    int32_t *cnt = nullptr;    // per item: its pieces completed so far (0 between folds)
+    uint32_t *blk = nullptr;   // the launches' block-arrival counters (MF_FOLD_WORDS)
+    const double *p2stat = nullptr;
+    double *stat_next = nullptr;
+    const double *user_sq = nullptr;
+    void *bias_out = nullptr;
+    int64_t n_users = 0;
+    int ld = 0, n_fac = 0, bias_col = -1, count_rule = 0, role = 0, n_launch = 0;
+    double eta_b = 0, lr_c = 0, reg_c = 0, lr_f = 0, reg_f = 0, lr_b = 0, reg_b = 0;
+};
+thread_local FoldArgs g_fold;
+FoldArgs take_fold() {
+    const FoldArgs f = g_fold;
+    g_fold = FoldArgs{};
+    return f;
+}
 }
 
 namespace {
@@ -2262,7 +2284,9 @@ __global__ __launch_bounds__(kBlock) void sumsq_kernel(const T *__restrict__ x, 
 }
 
 // sum of sq[0..n) in a fixed order by one whole workgroup (per-thread strided sums, 32 loads in
-// flight, then a fixed tree in LDS); the result in thread 0
+// flight, then a fixed tree in LDS); the result in thread 0.  COH: loads at the agent's coherence
+// point (sq written by another launch still running beside this one: the replay's fold)
+template <bool COH = false>
 __device__ __forceinline__ double block_sum(const double *__restrict__ sq, int64_t n)
 {
     __shared__ double part[kBlock];
@@ -2273,7 +2297,11 @@ __device__ __forceinline__ double block_sum(const double *__restrict__ sq, int64
 #pragma unroll
         for (int a = 0; a < kU; ++a) {
             const int64_t i = i0 + (int64_t)a * kBlock;
-            v[a] = i < n ? sq[i] : 0.0;
+            if constexpr (COH)
+                v[a] = i < n ? __hip_atomic_load(sq + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : 0.0;
+            else
+                v[a] = i < n ? sq[i] : 0.0;
         }
 #pragma unroll
         for (int a = 0; a < kU; ++a) acc += v[a];
@@ -2294,6 +2322,7 @@ __device__ __forceinline__ double block_sum(const double *__restrict__ sq, int64
 // 0 adds them in order.  Either way bit-reproducible.
 constexpr int kSqParts = MF_SQ_PARTS;
 constexpr int64_t kSqPartsMin = MF_SQ_PARTS_MIN;
+template <bool COH = false>
 __device__ __forceinline__ void block_sum_sq(const double *__restrict__ sq, int64_t n, int K,
                                              double *out)
 {
@@ -2306,7 +2335,7 @@ __device__ __forceinline__ void block_sum_sq(const double *__restrict__ sq, int6
         }
         return;
     }
-    const double t = block_sum(sq, n);
+    const double t = block_sum<COH>(sq, n);
     if (threadIdx.x == 0) {
         out[0] = t;
         out[1] = (double)n * K;
@@ -2616,6 +2645,132 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
 #define MF_REPLAY_ROW_NT 1
 #endif
 
+// ---------------------------------------------------------------- the per-item fold
+//
+// One item of mf_log_apply: its piece sums in a fixed order -- sums' pieces [a0, a1), then (TWO)
+// sums2's [b0, b1) -- then q += lr (S - W reg q) by the merge rule.  Run by log_apply_kernel (one
+// wave per item) and by the replay wave that completes an item's last piece (mf_launch_fold);
+// COH: the piece sums read at the agent's coherence point (written by waves of launches still
+// running).  KU pieces in flight per group; the sum order does not depend on it.
+struct FoldRule {
+    int count_rule;
+    double eta_fac, l_fac, l_bias, eta_bias, lr_f, reg_f, lr_b, reg_b;
+};
+__device__ __forceinline__ FoldRule fold_rule(int count_rule, const double *p2stat, double eta_bias,
+                                              double lr_fac, double reg_fac, double lr_f,
+                                              double reg_f, double lr_b, double reg_b)
+{
+    FoldRule r{count_rule, 0, 0, 0, eta_bias, lr_f, reg_f, lr_b, reg_b};
+    if (count_rule) {
+        r.eta_fac = lr_fac * (p2stat[0] / p2stat[1] + reg_fac);
+        r.l_fac = log1p(-r.eta_fac);
+        r.l_bias = log1p(-eta_bias);
+    }
+    return r;
+}
+template <typename T, bool COH>
+__device__ __forceinline__ T fold_ld(const T *p)
+{
+    if constexpr (COH)
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        return *p;
+}
+template <typename T, int V, bool TWO, bool COH, int KU>
+__device__ __forceinline__ void apply_item(
+    int64_t i, int lane, T *__restrict__ qb, int ld, int n_fac, int bias_col,
+    const T *__restrict__ sums, const int32_t *__restrict__ item_piece_ptr,
+    const T *__restrict__ sums2, const int32_t *__restrict__ item_piece_ptr2,
+    const int32_t *__restrict__ totals, const FoldRule &r, T *__restrict__ delta_out, int apply,
+    T *__restrict__ bias_out)
+{
+    // every load that does not depend on another first: both groups' piece ranges, the count and
+    // the item row; then the first KU pieces of each group together
+    const int a0 = item_piece_ptr ? item_piece_ptr[i] : (int)i;
+    const int a1 = item_piece_ptr ? item_piece_ptr[i + 1] : (int)i + 1;
+    const int b0 = TWO ? item_piece_ptr2[i] : 0, b1 = TWO ? item_piece_ptr2[i + 1] : 0;
+    const double N = totals ? (double)totals[i] : 0.0;
+    T q[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int c = lane + kWave * v;
+        q[v] = apply && c < ld ? qb[i * ld + c] : T(0);
+    }
+    auto load = [&](const T *__restrict__ sp, int pc, int p1, T (&g)[KU][V]) {
+#pragma unroll
+        for (int a = 0; a < KU; ++a)
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                g[a][v] = (pc + a < p1 && lane + kWave * v < ld)
+                              ? fold_ld<T, COH>(sp + (int64_t)(pc + a) * ld + lane + kWave * v)
+                              : T(0);
+    };
+    T acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = T(0);
+    auto add = [&](T (&g)[KU][V]) {
+#pragma unroll
+        for (int a = 0; a < KU; ++a)
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[v] += g[a][v];
+    };
+    // the item's pieces in sums, then (split log) its pieces in sums2, in that fixed order
+    T ga[KU][V];
+    load(sums, a0, a1, ga);
+    if constexpr (TWO) {
+        T gb[KU][V];
+        load(sums2, b0, b1, gb);
+        add(ga);
+        for (int pc = a0 + KU; pc < a1; pc += KU) {
+            load(sums, pc, a1, ga);
+            add(ga);
+        }
+        add(gb);
+        for (int pc = b0 + KU; pc < b1; pc += KU) {
+            load(sums2, pc, b1, gb);
+            add(gb);
+        }
+    } else {
+        add(ga);
+        for (int pc = a0 + KU; pc < a1; pc += KU) {
+            load(sums, pc, a1, ga);
+            add(ga);
+        }
+    }
+    // the count-aware weights (one per column kind, the same for every factor column);
+    // recency (count_rule 2): the sums arrive weighted, the reg term takes the weights' sum
+    // sum_k (1 - eta)^(N-1-k) = (1 - (1 - eta)^N) / eta = w N
+    double w_fac = 1.0, w_bias = 1.0;
+    if (r.count_rule && N > 1.0) {
+        w_fac = -expm1(N * r.l_fac) / (N * r.eta_fac);
+        w_bias = -expm1(N * r.l_bias) / (N * r.eta_bias);
+    }
+    const bool rec = r.count_rule == 2;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int c = lane + kWave * v;
+        if (c >= ld) continue;
+        const int64_t x = i * ld + c;
+        if (delta_out) delta_out[x] = acc[v];
+        if (apply && (c < n_fac || c == bias_col)) {
+            const bool b = c == bias_col;
+            const double w = b ? w_bias : w_fac;
+            // the log holds gradients g_k = err_k pe_k: sum_k d_k = lr (S - N reg q)
+            T nq;
+            if (rec) {
+                nq = q[v] + (T)(b ? r.lr_b : r.lr_f) *
+                                (acc[v] - (T)(w * N) * (T)(b ? r.reg_b : r.reg_f) * q[v]);
+            } else {
+                const T d = (T)(b ? r.lr_b : r.lr_f) *
+                            (acc[v] - (T)N * (T)(b ? r.reg_b : r.reg_f) * q[v]);
+                nq = q[v] + (T)w * d;
+            }
+            qb[x] = nq;
+            if (b && bias_out) bias_out[i] = nq;  // (the item-bias mirror of the SB epoch)
+        }
+    }
+}
+
 // ---------------------------------------------------------------- checkpoint-log replay
 //
 // The SVD log in checkpoint form (mf_svd_epoch with elog != NULL): per pair (c, c + 1) of a
@@ -2637,14 +2792,14 @@ __global__ __launch_bounds__(kBlock) void log_reduce_kernel(
 // rating costs two v_readlane broadcasts, the row gather and 2 (packed) FMAs per element; the
 // undone step enters once per piece: sum_even w err_k p_k = iap o (sum_even w err p_{c+1} -
 // D sum_even w err^2).  Two groups of MF_REPLAY_U rows are in flight per wave.
-template <typename T, int G, bool REC>
+template <typename T, int G, bool REC, bool FOLD = false>
 __device__ __forceinline__ void log_replay_body(
     const T *__restrict__ ckpt, const T *__restrict__ elog, int ldq, int K,
     const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T inv_ap,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
     const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int err_col,
     const int32_t *__restrict__ piece_item, const int64_t wave, const int64_t n_waves,
-    const bool wt, const Recency &rc, const int ldc)
+    const bool wt, const Recency &rc, const int ldc, const mf_ext::FoldArgs &fa)
 {
     using L = Lane8<T>;
     using vec = typename L::vec;
@@ -2678,6 +2833,13 @@ __device__ __forceinline__ void log_replay_body(
     // lane groups the checkpoint rows fill (G = kLaMaxG + 1 only with narrow rows of kLaMaxG
     // groups -- fp64 K = 128 -- whose last group holds the bias column alone)
     constexpr int GR = G > kLaMaxG ? kLaMaxG : G;
+    // the fold inside the replay (mf_launch_fold): the wave that completes an item's last piece
+    // -- of either launch group -- applies the item (apply_item, mf_log_apply's arithmetic)
+    constexpr bool fold = FOLD;
+    FoldRule fr{};
+    if constexpr (fold)
+        fr = fold_rule(fa.count_rule, fa.p2stat, fa.eta_b, fa.lr_c, fa.reg_c, fa.lr_f, fa.reg_f,
+                       fa.lr_b, fa.reg_b);
     for (int64_t pc = wave; pc < n_pieces; pc += n_waves) {
         // a piece: >= 1 ratings of ONE item, taken 64 at a time (lane x: rating x of the
         // sub-piece); the undone step's and the bias column's scalar sums accumulate per lane
@@ -2778,8 +2940,37 @@ __device__ __forceinline__ void log_replay_body(
                         sums[pc * ldq + c0 + e] = x;
                 }
         }
+        if constexpr (fold) {
+            // this piece's sums have reached the coherence point before the item's count moves;
+            // the wave that moves it to the item's piece total is the last and folds the item
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            int last = 0;
+            if (lane == 0) {
+                const int n = (fa.ipp_a[item + 1] - fa.ipp_a[item]) +
+                              (fa.ipp_b ? fa.ipp_b[item + 1] - fa.ipp_b[item] : 0);
+                const int old = __hip_atomic_fetch_add(fa.cnt + item, 1, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                if (old == n - 1) {
+                    __hip_atomic_store(fa.cnt + item, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    last = 1;
+                }
+            }
+            if (__builtin_amdgcn_readfirstlane(last)) {
+                constexpr int VA = G * W;  // (>= mf_log_apply's ceil(ld / 64): masked past ld)
+                if (fa.ipp_b)
+                    apply_item<T, VA, true, true, 4>(
+                        item, lane, (T *)fa.qb, fa.ld, fa.n_fac, fa.bias_col, (const T *)fa.sums_a,
+                        fa.ipp_a, (const T *)fa.sums_b, fa.ipp_b, fa.totals, fr, nullptr, 1,
+                        (T *)fa.bias_out);
+                else
+                    apply_item<T, VA, false, true, 4>(
+                        item, lane, (T *)fa.qb, fa.ld, fa.n_fac, fa.bias_col, (const T *)fa.sums_a,
+                        fa.ipp_a, nullptr, nullptr, fa.totals, fr, nullptr, 1, (T *)fa.bias_out);
+            }
+        }
     }
 }
+
 
 // In-kernel join of the two-stream SVD step (mf_launch_join): the light replay (role 1) and the
 // heavy replay (role 2) of one chunk meet without a barrier packet in the main stream's queue.
@@ -2830,24 +3021,49 @@ __device__ __forceinline__ void join_arrive(uint32_t *join, int role, uint32_t e
     }
 }
 
-template <typename T, int G, bool REC>
+// The in-replay fold's last step: the next chunk's <p^2> statistic, summed by the last block to
+// finish of the fold's launches (two levels of arrival counters per launch, as join_arrive, then
+// one over the launches); no block waits.  Both epoch kernels have ended by then (each launch
+// follows its own group's epoch), so user_sq is final; it is read at the coherence point.
+__device__ __forceinline__ void fold_arrive(const mf_ext::FoldArgs &fa)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int last = 0;
+        const uint32_t G = gridDim.x, c = blockIdx.x & 7;
+        uint32_t *w = fa.blk + 320 * (fa.role - 1);
+        if (join_count(w + 32 * c, (G - c + 7) / 8) && join_count(w + 256, G < 8 ? G : 8))
+            last = join_count(fa.blk + 640, (uint32_t)fa.n_launch) ? 1 : 0;
+        s_last = last;
+    }
+    __syncthreads();
+    if (s_last) block_sum_sq<true>(fa.user_sq, fa.n_users, fa.n_fac, fa.stat_next);
+}
+
+template <typename T, int G, bool REC, bool FOLD>
 __global__ __launch_bounds__(kBlock) void log_replay_kernel(
     const T *__restrict__ ckpt, const T *__restrict__ elog, int ldq, int K,
     const int32_t *__restrict__ items, const T *__restrict__ qb, int n_items, T lr_pu, T inv_ap,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ ck_pos,
     const int32_t *__restrict__ piece_beg, int64_t n_pieces, T *__restrict__ sums, int xmask,
     int err_col, const int32_t *__restrict__ piece_item, uint32_t *join, int join_role,
-    uint32_t join_epoch, Recency rc, int ldc)
+    uint32_t join_epoch, Recency rc, int ldc, mf_ext::FoldArgs fa)
 {
     int64_t wave, n_waves;
     if (wave_slot(xmask, wave, n_waves)) {
         SlotSettle settle((threadIdx.x & (kWave - 1)) == 0 ? xmask : 0, wave, n_waves,
                           wave_grid_index());
-        log_replay_body<T, G, REC>(ckpt, elog, ldq, K, items, qb, n_items, lr_pu, inv_ap, perm,
-                                   ck_pos, piece_beg, n_pieces, sums, err_col, piece_item, wave,
-                                   n_waves, join && join_role == 1, rc, ldc);
+        log_replay_body<T, G, REC, FOLD>(ckpt, elog, ldq, K, items, qb, n_items, lr_pu, inv_ap,
+                                         perm, ck_pos, piece_beg, n_pieces, sums, err_col,
+                                         piece_item, wave, n_waves,
+                                         FOLD || (join && join_role == 1), rc, ldc, fa);
     }
     if (join) join_arrive(join, join_role, join_epoch);
+    if constexpr (FOLD) {
+        if (fa.stat_next) fold_arrive(fa);
+    }
 }
 
 #ifndef MF_APPLY_U
@@ -2878,98 +3094,12 @@ __global__ __launch_bounds__(kBlock) void log_apply_kernel(
     const int64_t wave = (int64_t)(blockIdx.x - blk0) * (kBlock / kWave) +
                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int64_t n_waves = ((int64_t)(gridDim.x - blk0) * kBlock) / kWave;
-    double eta_fac = 0, l_fac = 0, l_bias = 0;
-    if (count_rule) {
-        eta_fac = lr_fac * (p2stat[0] / p2stat[1] + reg_fac);
-        l_fac = log1p(-eta_fac);
-        l_bias = log1p(-eta_bias);
-    }
-    constexpr int kU = MF_APPLY_U;  // independent piece loads in flight per group
-    for (int64_t i = wave; i < n_items; i += n_waves) {
-        // every load that does not depend on another first: both groups' piece ranges, the
-        // count and the item row; then the first kU pieces of each group together
-        const int a0 = item_piece_ptr ? item_piece_ptr[i] : (int)i;
-        const int a1 = item_piece_ptr ? item_piece_ptr[i + 1] : (int)i + 1;
-        const int b0 = TWO ? item_piece_ptr2[i] : 0, b1 = TWO ? item_piece_ptr2[i + 1] : 0;
-        const double N = totals ? (double)totals[i] : 0.0;
-        T q[V];
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-            const int c = lane + kWave * v;
-            q[v] = apply && c < ld ? qb[i * ld + c] : T(0);
-        }
-        auto load = [&](const T *__restrict__ sp, int pc, int p1, T (&g)[kU][V]) {
-#pragma unroll
-            for (int a = 0; a < kU; ++a)
-#pragma unroll
-                for (int v = 0; v < V; ++v)
-                    g[a][v] = (pc + a < p1 && lane + kWave * v < ld)
-                                  ? sp[(int64_t)(pc + a) * ld + lane + kWave * v] : T(0);
-        };
-        T acc[V];
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[v] = T(0);
-        auto add = [&](T (&g)[kU][V]) {
-#pragma unroll
-            for (int a = 0; a < kU; ++a)
-#pragma unroll
-                for (int v = 0; v < V; ++v) acc[v] += g[a][v];
-        };
-        // the item's pieces in sums, then (split log) its pieces in sums2, in that fixed order
-        T ga[kU][V];
-        load(sums, a0, a1, ga);
-        if constexpr (TWO) {
-            T gb[kU][V];
-            load(sums2, b0, b1, gb);
-            add(ga);
-            for (int pc = a0 + kU; pc < a1; pc += kU) {
-                load(sums, pc, a1, ga);
-                add(ga);
-            }
-            add(gb);
-            for (int pc = b0 + kU; pc < b1; pc += kU) {
-                load(sums2, pc, b1, gb);
-                add(gb);
-            }
-        } else {
-            add(ga);
-            for (int pc = a0 + kU; pc < a1; pc += kU) {
-                load(sums, pc, a1, ga);
-                add(ga);
-            }
-        }
-        // the count-aware weights (one per column kind, the same for every factor column);
-        // recency (count_rule 2): the sums arrive weighted, the reg term takes the weights' sum
-        // sum_k (1 - eta)^(N-1-k) = (1 - (1 - eta)^N) / eta = w N
-        double w_fac = 1.0, w_bias = 1.0;
-        if (count_rule && N > 1.0) {
-            w_fac = -expm1(N * l_fac) / (N * eta_fac);
-            w_bias = -expm1(N * l_bias) / (N * eta_bias);
-        }
-        const bool rec = count_rule == 2;
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-            const int c = lane + kWave * v;
-            if (c >= ld) continue;
-            const int64_t x = i * ld + c;
-            if (delta_out) delta_out[x] = acc[v];
-            if (apply && (c < n_fac || c == bias_col)) {
-                const bool b = c == bias_col;
-                const double w = b ? w_bias : w_fac;
-                // the log holds gradients g_k = err_k pe_k: sum_k d_k = lr (S - N reg q)
-                T nq;
-                if (rec) {
-                    nq = q[v] + (T)(b ? lr_b : lr_f) *
-                                    (acc[v] - (T)(w * N) * (T)(b ? reg_b : reg_f) * q[v]);
-                } else {
-                    const T d = (T)(b ? lr_b : lr_f) * (acc[v] - (T)N * (T)(b ? reg_b : reg_f) * q[v]);
-                    nq = q[v] + (T)w * d;
-                }
-                qb[x] = nq;
-                if (b && bias_out) bias_out[i] = nq;  // (the item-bias mirror of the SB epoch)
-            }
-        }
-    }
+    const FoldRule r = fold_rule(count_rule, p2stat, eta_bias, lr_fac, reg_fac, lr_f, reg_f, lr_b,
+                                 reg_b);
+    for (int64_t i = wave; i < n_items; i += n_waves)
+        apply_item<T, V, TWO, false, MF_APPLY_U>(i, lane, qb, ld, n_fac, bias_col, sums,
+                                                 item_piece_ptr, sums2, item_piece_ptr2, totals, r,
+                                                 delta_out, apply, bias_out);
 }
 
 // ---------------------------------------------------------------- blocked solve (heaviest users)
@@ -4611,7 +4741,7 @@ int elementwise_grid(int64_t total) {
 
 extern "C" {
 
-int mf_version(void) { return 935; }
+int mf_version(void) { return 936; }
 
 #ifndef MF_SOURCE_HASH
 #define MF_SOURCE_HASH "unknown"
@@ -4661,6 +4791,60 @@ int mf_launch_join(void *words, int32_t role, uint32_t epoch)
 {
     if (words && role != 1 && role != 2) return set_err(MF_E_ARG, "join role must be 1 or 2");
     mf_ext::g_join = mf_ext::JoinArgs{(uint32_t *)words, words ? role : 0, epoch};
+    return 0;
+}
+
+int mf_launch_fold(const mf_fold_t *f)
+{
+    mf_ext::g_fold = mf_ext::FoldArgs{};
+    if (!f) return 0;
+    if (!f->item_count || !f->words || !f->qb || !f->sums || !f->item_piece_ptr || !f->totals ||
+        !f->hp)
+        return set_err(MF_E_ARG, "mf_launch_fold: null argument");
+    if (f->sums2 && !f->item_piece_ptr2) return set_err(MF_E_ARG, "sums2 needs item_piece_ptr2");
+    if (f->role < 1 || f->role > 2 || f->n_launches < 1 || f->n_launches > 2 ||
+        f->role > f->n_launches)
+        return set_err(MF_E_ARG, "mf_launch_fold: role / n_launches");
+    if (f->ld < 1 || f->n_factors < 0 || f->n_factors > f->ld || f->bias_col >= f->ld)
+        return set_err(MF_E_ARG, "bad shape");
+    if (f->rule != MF_MERGE_SUM && f->rule != MF_MERGE_COUNT && f->rule != MF_MERGE_RECENCY)
+        return set_err(MF_E_ARG, "bad merge rule");
+    const int count_rule = f->rule == MF_MERGE_COUNT ? 1 : (f->rule == MF_MERGE_RECENCY ? 2 : 0);
+    if (count_rule && !f->p2stat) return set_err(MF_E_ARG, "count-aware rule needs p2stat");
+    if (f->stat_next && f->stat_next == f->p2stat) return set_err(MF_E_ARG, "stat_next aliases p2stat");
+    if (f->stat_next && (!f->user_sq || f->n_users < 0 || f->n_users >= kSqPartsMin))
+        return set_err(MF_E_UNSUPPORTED, "mf_launch_fold: stat_next needs user_sq of < MF_SQ_PARTS_MIN users");
+    if (f->bias_out && f->bias_col < 0) return set_err(MF_E_ARG, "bias_out needs bias_col");
+    const mf_hyper_t *hp = f->hp;
+    mf_ext::FoldArgs a;
+    a.qb = f->qb;
+    a.ipp_a = f->item_piece_ptr;
+    a.ipp_b = f->sums2 ? f->item_piece_ptr2 : nullptr;
+    a.sums_a = f->sums;
+    a.sums_b = f->sums2;
+    a.totals = f->totals;
+    a.cnt = f->item_count;
+    a.blk = f->words;
+    a.p2stat = f->p2stat;
+    a.stat_next = f->stat_next;
+    a.user_sq = f->user_sq;
+    a.bias_out = f->bias_out;
+    a.n_users = f->n_users;
+    a.ld = f->ld;
+    a.n_fac = f->n_factors;
+    a.bias_col = f->bias_col;
+    a.count_rule = count_rule;
+    a.role = f->role;
+    a.n_launch = f->n_launches;
+    // (mf_log_apply's constants)
+    a.eta_b = count_rule ? hp->lr_bi * (1.0 + hp->reg_bi) : 0.0;
+    a.lr_c = count_rule ? hp->lr_qi : 0.0;
+    a.reg_c = count_rule ? hp->reg_qi : 0.0;
+    a.lr_f = hp->lr_qi;
+    a.reg_f = hp->reg_qi;
+    a.lr_b = hp->lr_bi;
+    a.reg_b = hp->reg_bi;
+    mf_ext::g_fold = a;
     return 0;
 }
 
@@ -4888,10 +5072,15 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
 {
     StopEvent stop(stream);  // (mf_launch_event)
     const mf_ext::JoinArgs join = mf_ext::take_join();  // (mf_launch_join)
+    const mf_ext::FoldArgs fold = mf_ext::take_fold();  // (mf_launch_fold)
     if (n_pieces < 0 || ldq < n_factors + 1 || n_factors < 0) return set_err(MF_E_ARG, "bad shape");
+    if (fold.cnt && join.words) return set_err(MF_E_ARG, "mf_launch_fold with mf_launch_join");
+    if (fold.cnt && fold.ld != ldq) return set_err(MF_E_ARG, "mf_launch_fold: ld != ldq");
+    if (fold.cnt && !rec) return set_err(MF_E_UNSUPPORTED, "mf_launch_fold: recency weights only");
     const int xmask = (flags >> MF_EPOCH_XCD_SHIFT) & 0xFF;
     if (int rc = check_xmask(xmask)) return rc;
-    if (n_pieces == 0 && !join.words) return 0;  // (a join still launches: its partner waits)
+    // (a join or a fold still launches: its partner waits / its blocks count for the statistic)
+    if (n_pieces == 0 && !join.words && !fold.cnt) return 0;
     if (!qlog || !elog || !csr || !qb || !hp || !perm || !ck_pos || !piece_beg || !sums)
         return set_err(MF_E_ARG, "null argument");
     const int err_col = (flags & MF_EPOCH_ERR_IN_ROW) ? err_column(n_factors, ldq, dtype) : 0;
@@ -4921,13 +5110,16 @@ int mf_log_replay(const void *qlog, const void *elog, int32_t ldq, int32_t n_fac
                 return set_err(MF_E_UNSUPPORTED, "checkpoint log: row too long");
             } else {
                 // (V = kLaMaxG + 1 only for narrow rows: their groups stop at kLaMaxG)
-                auto kern = rec ? log_replay_kernel<T, V, true> : log_replay_kernel<T, V, false>;
+                // (the fold inside the replay: recency rule only -- the default)
+                auto kern = fold.cnt ? log_replay_kernel<T, V, true, true>
+                            : rec    ? log_replay_kernel<T, V, true, false>
+                                     : log_replay_kernel<T, V, false, false>;
                 launch_ev(stop.take(), kern, dim3(g), dim3(kBlock), st,
                                    (const T *)qlog, (const T *)elog, ldq, n_factors, csr->items,
                                    (const T *)qb, csr->n_items, (T)hp->lr_pu,
                                    (T)(1.0 / (1.0 - hp->lr_pu * hp->reg_pu)), perm,
                                    ck_pos, piece_beg, n_pieces, (T *)sums, xmask, err_col,
-                                   piece_item, join.words, join.role, join.epoch, rc, ldc);
+                                   piece_item, join.words, join.role, join.epoch, rc, ldc, fold);
                 return check_launch("log_replay_kernel");
             }
         });

@@ -153,6 +153,11 @@ def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS, local=Fals
     return perm, piece_beg.astype(np.int32), item_piece_ptr, counts.astype(np.int32)
 
 
+def _vp_int(p):
+    """A ctypes.c_void_p (or None) as the int a c_void_p structure field takes."""
+    return None if p is None else (p.value if isinstance(p, ctypes.c_void_p) else int(p))
+
+
 def cold_items(counts, share):
     """The hybrid launch's cold items of one chunk: the least-rated items whose ratings add up to
     at most `share` of the chunk's (bool[n_items]; items the chunk does not rate are not cold)."""
@@ -468,7 +473,7 @@ class MFEngine(ItemSync, Predictor):
                  replay_rows=None, gram=None, xcd_split=None, qlog=None, top=None,
                  exchange=None, long_chain=256, overlap_q=True, fused=True, stagger=None,
                  light_replay_wpc=0, log_nt=None, item_align=None, bias_mirror=True,
-                 cold_share=0.0):
+                 cold_share=0.0, replay_fold=False):
         """csr: this rank's rows only (rank-local row_ptr from 0; dist.local_csr) -- the whole
         trainset for one GPU.  pu / bu hold exactly those rows; get_factors(ctx) gathers.
 
@@ -532,6 +537,10 @@ class MFEngine(ItemSync, Predictor):
                       this share of a chunk's ratings keep their rows read-only for the chunk,
                       their gradients logged and folded after it (mf_svdpp_epoch_mix); the
                       others take the float atomics (0: off)
+          replay_fold checkpoint log, split chunk on one rank: the chunk's fold (mf_log_apply's
+                      arithmetic) inside the two log replays -- the wave that completes an
+                      item's last piece applies it (mf_launch_fold) -- instead of a launch of its
+                      own after them; False: the separate fold
           bias_mirror checkpoint log with SB rows (fp32 K=128, fp64 K=64 / 128): the item biases
                       read from a mirror array, the item rows on whole 128-B lines; False: from
                       the rows
@@ -727,6 +736,16 @@ class MFEngine(ItemSync, Predictor):
         # instead (mf_launch_join: the heavy replay's last block waits for the light replay's;
         # no barrier packet before the fold) -- measured equal (the write-through stores of the
         # light replay cost what the barrier packet did), so off by default
+        # the fold inside the replays (replay_fold): per-item piece counters and the launches'
+        # arrival counters, zero between folds
+        self.replay_fold = bool(replay_fold) and self.side is not None and join == "event" and \
+            events == "native"
+        self._fold_cnt = self._fold_words = None
+        self._folded = False
+        self.replay_folds_run = 0  # (chunks folded inside their replays)
+        if self.replay_fold:
+            self._fold_cnt = torch.zeros(max(self.n_items, 1), dtype=torch.int32, device=dev)
+            self._fold_words = torch.zeros(_lib.MF_FOLD_WORDS, dtype=torch.int32, device=dev)
         self._join_words = None
         if self.side is not None and join == "kernel":
             self._join_words = torch.zeros(1024, dtype=torch.int32, device=dev)
@@ -1343,6 +1362,9 @@ class MFEngine(ItemSync, Predictor):
                 _lib.call("mf_launch_join", self._ptr(jw), 1, self._join_epoch)
             elif self._nev is not None:
                 _lib.call("mf_launch_event", self._nev["join"])  # completed by the light replay
+            folds = self._replay_folds(c, lg, hv, sums_h)
+            if folds:
+                _lib.call("mf_launch_fold", ctypes.byref(folds[0]))
             self._reduce_log(lg, self.sums.data_ptr(), sh, lx, self.light_replay_wpc)
             if jw is None and self._nev is None:
                 self._ev_record("join", side)
@@ -1350,6 +1372,12 @@ class MFEngine(ItemSync, Predictor):
             # work is (nearly) done, so it may spread over every XCD)
             if jw is not None:  # (it ends once the light replay of this chunk has published)
                 _lib.call("mf_launch_join", self._ptr(jw), 2, self._join_epoch)
+            if folds:  # (the heavy replay completes "fork": the item table is final after it
+                # and after the light replay, which the side stream runs before its next epoch)
+                self._bind_fork()
+                _lib.call("mf_launch_fold", ctypes.byref(folds[1]))
+                self._folded = True
+                self.replay_folds_run += 1
             self._reduce_log(hv, sums_h, st)
             if jw is None and self._nev is None:
                 self._ev_wait(self.stream, "join")
@@ -1588,6 +1616,25 @@ class MFEngine(ItemSync, Predictor):
                   *self._stat_args(apply if stat is None else stat),
                   self._bias_out(apply), self.dtype, self._st())
 
+    def _replay_folds(self, c, lg, hv, sums_h):
+        """mf_fold_t of the light (role 1) and heavy (role 2) replays of split chunk c when the
+        fold runs inside them (replay_fold), else None."""
+        if not (self.replay_fold and self.ckpt and self.is_log and self.user_sq is not None
+                and self.n_users < _lib.MF_SQ_PARTS_MIN and self.recency
+                and not self._exchanging(self._ctx)):
+            return None
+        stat_next, user_sq, n_users = self._stat_args(True)
+        bo = self._bias_out(True)
+        out = []
+        for role in (1, 2):
+            out.append(_lib.MfFold(
+                self.qb.data_ptr(), self.ldq, self.K, self._bias_col, self._log_rule(),
+                self.sums.data_ptr(), lg["ipp"].data_ptr(), sums_h, hv["ipp"].data_ptr(),
+                self._totals()[c].data_ptr(), ctypes.addressof(self._hyper),
+                self.work.data_ptr(), _vp_int(stat_next), _vp_int(user_sq), n_users,
+                _vp_int(bo), self._fold_cnt.data_ptr(), self._fold_words.data_ptr(), role, 2))
+        return out
+
     def _bind_fork(self):
         """The next mf_log_apply completes the "fork" event the side stream waits for (the item
         table the next chunk's light users read); call right before that launch."""
@@ -1627,6 +1674,9 @@ class MFEngine(ItemSync, Predictor):
         return self.qlog_pp and self.fused and self.recency and not self._exchanging(self._ctx)
 
     def _merge_local(self):
+        if self._folded:  # (the fold ran inside the chunk's replays: replay_fold)
+            self._folded = False
+            return
         if self._fused_fold():
             c = getattr(self, "_chunk", 0)
             f = self.logs[c]["fold"]

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_without_device(lib):
-    assert lib.mf_version() == 935
+    assert lib.mf_version() == 936
     rc = lib.mf_item_affine(None, None, 10, 16, None, None, None, 0, 0, None)
     assert rc == 1001 and b"bad argument" in lib.mf_last_error()
     # argument validation happens before any device call

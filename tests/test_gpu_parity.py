@@ -723,6 +723,47 @@ def test_heavy_user_split_matches_single_launch(torch, u1):
         np.testing.assert_allclose(out[0][k], out[1][k], rtol=0, atol=1e-10, err_msg=k)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("which,K,dtype,chunks", [("ml1m", 100, "float64", 1),
+                                                  ("ml1m", 100, "float32", 2),
+                                                  ("u1", 128, "float32", 1),
+                                                  ("u1", 128, "float64", 2)])
+def test_replay_fold_equals_separate_fold(torch, request, which, K, dtype, chunks):
+    """The split chunk's fold inside its two log replays (engine option replay_fold,
+    mf_launch_fold: the wave that completes an item's last piece applies the item, the last
+    block of both replays sums the next chunk's <p^2>) against the separate mf_log_apply launch:
+    the same arithmetic in the same order (apply_item), so the fits are bit-identical -- with a
+    batched predict between epochs, several chunks (the <p^2> slots), fp32 K=128's item-bias
+    mirror and fp64 K=128's narrow rows."""
+    from surprise_amd.engine import MFEngine
+    ts, _ = request.getfixturevalue(which)
+    row_ptr, items, ratings = ts.csr()
+    hyper = dict(lr_bu=.005, lr_bi=.005, lr_pu=.005, lr_qi=.005, reg_bu=.02, reg_bi=.02,
+                 reg_pu=.02, reg_qi=.02, global_mean=float(ts.global_mean))
+    heavy = 0.25 if which == "u1" else None
+    rng = np.random.RandomState(5)
+    pu0, qi0 = rng.normal(0, .1, (ts.n_users, K)), rng.normal(0, .1, (ts.n_items, K))
+    uu = np.arange(ts.n_users, dtype=np.int32) % ts.n_users
+    ii = np.arange(ts.n_users, dtype=np.int32) % ts.n_items
+    out = []
+    for rf in (True, False):
+        eng = MFEngine((row_ptr, items, ratings), ts.n_items, K, hyper=hyper, dtype=dtype,
+                       mode="log", n_chunks=chunks, heavy=heavy, replay_fold=rf)
+        assert eng.ckpt and eng.logs[0]["heavy"] is not None
+        eng.set_factors(pu0, qi0)
+        ests = [None]
+        eng.run_epochs(2)
+        ests[0] = eng.predict(uu, ii, ts.global_mean)[0]
+        eng.run_epochs(2)
+        f = eng.get_factors()
+        f["est"] = ests[0]
+        assert eng.replay_folds_run == (4 * chunks if rf else 0), eng.replay_folds_run
+        assert int(eng._fold_cnt.abs().sum()) == 0 if rf else True  # (counters back to 0)
+        out.append(f)
+    for k in ("pu", "qi", "bu", "bi", "est"):
+        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
+
+
 @pytest.mark.parametrize("which,chunks", [("u1", 1), ("u1", 3), ("ml1m", 1)])
 @pytest.mark.parametrize("top", [0, 16])
 def test_native_fork_and_kernel_join_equal_torch_events(torch, request, monkeypatch, which,

@@ -1,7 +1,8 @@
 """Round-5 probe (GPU box): the headline step's join between the light replay (side stream) and
 the fold (main stream).  The product step waits on a HIP event (engine join="event", events
 "native"); the alternatives are the in-kernel join (join="kernel": the heavy replay's last block
-waits for the light replay) and torch events.  ML-1M fold 0, SVD K=100, fp64 and fp32, 60 timed
+waits for the light replay), torch events, and the fold inside the replays (replay_fold: no
+fold launch, no join before it).  ML-1M fold 0, SVD K=100, fp64 and fp32, 60 timed
 steps x 3 repeats each (bench.run_steps)."""
 import json
 import os
@@ -23,7 +24,8 @@ ts, _ = next(KFold(5, random_state=0).split(Dataset.load_from_arrays(u, i, r)))
 rp, it, rt = ts.csr()
 for dt in ("float64", "float32"):
     for name, kw in (("event (product)", {}), ("kernel join", {"join": "kernel"}),
-                     ("torch events", {"events": "torch"})):
+                     ("torch events", {"events": "torch"}),
+                     ("fold in the replays", {"replay_fold": True})):
         rng = np.random.RandomState(0)
         eng = MFEngine((rp, it, rt), ts.n_items, 100,
                        hyper=bench.hyper_for("svd", float(ts.global_mean)), dtype=dt, **kw)
