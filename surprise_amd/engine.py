@@ -153,6 +153,28 @@ def log_layout(row_ptr, items, users, n_items, piece_rows=PIECE_ROWS, local=Fals
     return perm, piece_beg.astype(np.int32), item_piece_ptr, counts.astype(np.int32)
 
 
+# The split step's side stream.  HIP deals streams over GPU_MAX_HW_QUEUES hardware queues; a side
+# stream that lands on the main stream's queue serialises the two launch groups (the headline
+# step ~1.75x slower, about one engine in four when each engine takes a fresh pool stream:
+# profiles/r5bm_bimodal.jsonl).  "cached": one side stream per device for the process, made
+# when the first engine needs it; "-high": at high priority; "pool": a fresh pool stream per
+# engine (the round-4 behaviour).
+SIDE_STREAM_POLICY = "cached"
+_SIDE_STREAMS = {}
+
+
+def side_stream(torch, dev, which=0, policy=None):
+    policy = policy or SIDE_STREAM_POLICY
+    prio = -1 if policy.endswith("high") else 0
+    if not policy.startswith("cached"):
+        return torch.cuda.Stream(device=dev, priority=prio)
+    key = (torch.device(dev).index, which, prio)
+    s = _SIDE_STREAMS.get(key)
+    if s is None:
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=dev, priority=prio)
+    return s
+
+
 def _vp_int(p):
     """A ctypes.c_void_p (or None) as the int a c_void_p structure field takes."""
     return None if p is None else (p.value if isinstance(p, ctypes.c_void_p) else int(p))
@@ -715,7 +737,7 @@ class MFEngine(ItemSync, Predictor):
         if stagger is None:
             stagger = False
         self.stagger = bool(stagger) and self.ckpt and heavy <= 0
-        self.side = torch.cuda.Stream(device=dev) if self.ckpt and (heavy > 0 or self.stagger) \
+        self.side = side_stream(torch, dev) if self.ckpt and (heavy > 0 or self.stagger) \
             else None
         # the top users of the heavy launch on the main stream, the rest of it on a third stream
         # (its replay and the pre-fold then overlap the top chains)
@@ -723,7 +745,7 @@ class MFEngine(ItemSync, Predictor):
             top = self.HEAVY_TOP_USERS
         self.top = (int(top) if self.side is not None and heavy >= 1 and int(top) > 0
                     and int(top) < heavy and not self.gram and join == "event" else 0)
-        self.side2 = torch.cuda.Stream(device=dev) if self.top else None
+        self.side2 = side_stream(torch, dev, 1) if self.top else None
         # the fork / join between the two streams as native events bound to the kernels that
         # complete them (mf_launch_event: no marker packet in the main stream's queue);
         # events="torch": torch.cuda.Event record / wait_event

@@ -1,5 +1,6 @@
 """Round-5 probe (GPU box): the headline step's join between the light replay (side stream) and
-the fold (main stream).  The product step waits on a HIP event (engine join="event", events
+the fold (main stream), and (replay_rows) shorter replay pieces: the heavy replay is bound by its
+longest piece's chain of row gathers.  The product step waits on a HIP event (engine join="event", events
 "native"); the alternatives are the in-kernel join (join="kernel": the heavy replay's last block
 waits for the light replay), torch events, and the fold inside the replays (replay_fold: no
 fold launch, no join before it).  ML-1M fold 0, SVD K=100, fp64 and fp32, 60 timed
@@ -25,7 +26,9 @@ rp, it, rt = ts.csr()
 for dt in ("float64", "float32"):
     for name, kw in (("event (product)", {}), ("kernel join", {"join": "kernel"}),
                      ("torch events", {"events": "torch"}),
-                     ("fold in the replays", {"replay_fold": True})):
+                     ("fold in the replays", {"replay_fold": True}),
+                     ("replay pieces of 32", {"replay_rows": 32}),
+                     ("replay pieces of 16", {"replay_rows": 16})):
         rng = np.random.RandomState(0)
         eng = MFEngine((rp, it, rt), ts.n_items, 100,
                        hyper=bench.hyper_for("svd", float(ts.global_mean)), dtype=dt, **kw)
