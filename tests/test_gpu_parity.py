@@ -1243,3 +1243,18 @@ def test_svdpp_hybrid_launch_rmse_within_1e3(torch, golden, u1, name, dtype):
     cold = int((eng.mix[0]["crow"] >= 0).sum())
     assert 0.3 * ts.n_ratings < cold <= 0.5 * ts.n_ratings, cold
     assert abs(_rmse(algo.test(test)) - case["rmse"]) < RMSE_TOL
+
+
+def test_split_engines_share_one_side_stream(torch, u1):
+    """The split step's side stream is one per device for the process (engine.side_stream,
+    SIDE_STREAM_POLICY "cached"): a fresh pool stream per engine landed on the main stream's
+    hardware queue in about one engine of four and serialised the two launch groups
+    (profiles/r5bm_bimodal.jsonl)."""
+    from surprise_amd import engine as E
+    ts, _ = u1
+    csr = ts.csr()
+    engs = [E.MFEngine(csr, ts.n_items, 16, dtype="float32", mode="log", heavy=0.25)
+            for _ in range(3)]
+    assert all(e.side is not None for e in engs)
+    assert len({e.side.cuda_stream for e in engs}) == 1
+    assert engs[0].side.cuda_stream != torch.cuda.current_stream().cuda_stream
